@@ -1,0 +1,184 @@
+/*
+ * rq.h -- C ABI of librq.so, the MI355X (gfx950) RedQueen Monte-Carlo engine.
+ *
+ * The reference (MPI-SWS/RedQueen) is pure Python with no FFI; these entry
+ * points replace the following in-process Python calls (file:line into the
+ * reference):
+ *
+ *   rq_graph_build      SimOpts(**kw)                      opt_model.py:773-780
+ *                       + Manager.__init__ validation       opt_model.py:145-181
+ *                       + Broadcaster.init_state sink lists opt_model.py:340-344
+ *   rq_run_batch        SimOpts.create_manager_with_opt     opt_model.py:806-811
+ *                       / _with_poisson :821-837 / _for_wall :886-891
+ *                       / _with_times :893-898 / _with_piecewise_const :839-848
+ *                       -> Manager.run_dynamic              opt_model.py:241-314
+ *                       -> State.get_dataframe              opt_model.py:85-97
+ *                       -> utils.time_in_top_k / average_rank / int_r_2 /
+ *                          num_tweets_of                    utils.py:84-121,170-176
+ *                       over a seeds x q x s grid, i.e. the loops of
+ *                       utils.calc_q_capacity_iter          utils.py:447-470 and
+ *                       opt_runs.worker_opt/worker_poisson  opt_runs.py:51-126
+ *                       with opt_runs.add_perf's fields     opt_runs.py:41-48
+ *   rq_metrics_replay   utils.time_in_top_k(df, K, ...)     utils.py:84-98
+ *                       utils.average_rank(df, ...)         utils.py:101-114
+ *                       utils.int_r_2(df, ...)              utils.py:117-121
+ *                       utils.num_tweets_of(df, ...)        utils.py:170-176
+ *                       on a dataframe in the reference's row layout.
+ *
+ * Conventions
+ *   - every function returns 0 (RQ_OK) or a negative rq_status; no C++
+ *     exception crosses the ABI; rq_strerror() names a code.
+ *   - rq_graph_t handles are immutable after build and may be shared by threads.
+ *   - rq_run_batch / rq_metrics_replay are stream-ordered and asynchronous:
+ *     they only enqueue work on `hip_stream` (a hipStream_t, NULL = default
+ *     stream) and never allocate, free or synchronise.  The caller owns every
+ *     device buffer (workspace and outputs) and must keep them alive until the
+ *     stream has passed the work.  One device per process; the caller selects it.
+ *   - "device pointer" = memory allocated on the current HIP device
+ *     (e.g. torch.empty(..., device="cuda").data_ptr()).
+ */
+#ifndef RQ_H
+#define RQ_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RQ_ABI_VERSION 1
+#define RQ_MAX_K 4 /* at most 4 K values (perf_opts.Ks, opt_runs.py:31-38) per run */
+
+typedef enum {
+    RQ_OK = 0,
+    RQ_EINVAL = -1,       /* bad argument / reference would raise (assert, ValueError, KeyError) */
+    RQ_EOVERFLOW = -2,    /* a capacity was too small (see per-replica status bits)    */
+    RQ_EHIP = -3,         /* a HIP runtime call failed                                   */
+    RQ_ENOMEM = -4,       /* host or device allocation failed                            */
+    RQ_EUNSORTED = -5,    /* replay: df 't' column is not non-decreasing                 */
+    RQ_EUNSUPPORTED = -6  /* valid for the reference, not supported by this engine       */
+} rq_status;
+
+/* broadcaster kinds (SimOpts.broadcasters, opt_model.py:758-766) */
+typedef enum {
+    RQ_SRC_NONE = 0,      /* controlled slot only: create_manager_for_wall          */
+    RQ_SRC_POISSON = 1,   /* Poisson        opt_model.py:424-433 (dynamic)          */
+    RQ_SRC_POISSON2 = 2,  /* Poisson2       opt_model.py:381-421 (static)           */
+    RQ_SRC_HAWKES = 3,    /* Hawkes         opt_model.py:458-490                    */
+    RQ_SRC_PWCONST = 4,   /* PiecewiseConst opt_model.py:626-689                    */
+    RQ_SRC_REALDATA = 5,  /* RealData       opt_model.py:711-750                    */
+    RQ_SRC_OPT = 6        /* Opt = RedQueen opt_model.py:493-544 (controlled only)  */
+} rq_src_kind;
+
+typedef struct rq_source_desc {
+    int32_t kind;        /* rq_src_kind                                                   */
+    int32_t n_arr;       /* PWCONST: #segments; REALDATA: #times                           */
+    int64_t src_id;
+    uint32_t seed;       /* kwargs['seed'] (RandomState seed, opt_model.py:329)            */
+    uint32_t reserved;
+    double p0, p1, p2;   /* POISSON/POISSON2: rate; HAWKES: l_0, alpha, beta               */
+    const double* a;     /* host: PWCONST change_times[n_arr]; REALDATA times[n_arr]       */
+    const double* b;     /* host: PWCONST rates[n_arr]                                     */
+} rq_source_desc;
+
+typedef struct rq_graph_desc {
+    int32_t n_sources;                /* SimOpts.other_sources, in list order          */
+    const rq_source_desc* sources;    /* host                                           */
+    int32_t n_sinks;
+    const int64_t* sink_ids;          /* host, SimOpts.sink_ids                          */
+    int64_t n_edges;
+    const int64_t* edge_src;          /* host, SimOpts.edge_list in list order           */
+    const int64_t* edge_sink;
+    int64_t ctrl_src_id;              /* SimOpts.src_id                                  */
+    double start_time;                /* Manager start_time (0 in every reference call)  */
+    double end_time;                  /* SimOpts.end_time                                */
+    /* controlled broadcaster parameters used by RQ_SRC_PWCONST / RQ_SRC_REALDATA runs */
+    int32_t ctrl_n_arr;
+    const double* ctrl_a;             /* host: change_times or event_times               */
+    const double* ctrl_b;             /* host: rates                                     */
+} rq_graph_desc;
+
+typedef struct rq_graph* rq_graph_t;
+
+/* status bits written per replica into rq_outputs.status */
+#define RQ_ST_ROWS_OVERFLOW 1    /* metric-row / event-log capacity exceeded: rerun with larger cap_scale */
+#define RQ_ST_STREAM_OVERFLOW 2  /* a source's arrival stream exceeded its capacity: rerun      */
+#define RQ_ST_TIE 4              /* two events at the same time merged into one pivot row       */
+#define RQ_ST_EMPTY 8            /* no event reached any sink: the reference's df is empty      */
+
+#define RQ_RUN_EVENT_LOG 1       /* also write the (t, source) event log (for get_dataframe)    */
+
+typedef struct rq_batch_desc {
+    int32_t ctrl_kind;           /* RQ_SRC_OPT / POISSON2 / PWCONST / REALDATA / NONE           */
+    int32_t n_grid;              /* grid points                                                  */
+    const double* q;             /* host [n_grid] (OPT)                                          */
+    const double* s;             /* host [n_grid * n_followers], sorted-follower order (OPT)     */
+    int64_t n_rep;               /* replicas per grid point; replica id i = g * n_rep + r        */
+    const uint32_t* ctrl_seed;   /* device [n_grid*n_rep] or NULL: ctrl_seed0 + k(i)             */
+    uint32_t ctrl_seed0;
+    int32_t randomize_world;     /* 1: world seeds = u_i + 99*idx (randomize_other_sources,      */
+                                 /*    opt_model.py:795-804); 0: the graph's fixed seeds         */
+    const uint32_t* world_seed;  /* device [n_grid*n_rep] u_i, or NULL: world_seed0 + k(i)       */
+    uint32_t world_seed0;
+    int64_t seed_mod;            /* k(i) = i % seed_mod if > 0 else i; seed_mod = n_rep gives    */
+                                 /* every grid point the same seeds (calc_q_capacity_iter)       */
+    const double* ctrl_rate;     /* device [n_grid*n_rep] Poisson2 rate (RQ_SRC_POISSON2)        */
+    double ctrl_rate_max;        /* host: max of ctrl_rate, sizes the stream capacity            */
+    const int32_t* Ks;           /* host [nK], nK <= RQ_MAX_K                                     */
+    int32_t nK;
+    int64_t max_events;          /* run_dynamic(max_events); < 0 = unbounded                     */
+    int32_t flags;               /* RQ_RUN_EVENT_LOG                                              */
+    double cap_scale;            /* >= 1: multiplies every auto-sized capacity                   */
+    int64_t chunk;               /* replicas in flight per launch wave (0 = library default)     */
+} rq_batch_desc;
+
+typedef struct rq_outputs {
+    double* metrics;   /* device [R][nK + 2]: top_K..., avg_rank, r_2     (R = n_grid*n_rep) */
+    int64_t* counts;   /* device [R][4]: num_events (own posts that reached a sink = the   */
+                       /* reference 'capacity'), world_events, n_events (all), pivot rows   */
+    int32_t* status;   /* device [R]: RQ_ST_* bits                                            */
+    double* ev_t;      /* device [R][ev_cap] event times   (RQ_RUN_EVENT_LOG)                */
+    int32_t* ev_src;   /* device [R][ev_cap] source index  (rq_graph_source_ids order)       */
+    int64_t ev_cap;
+} rq_outputs;
+
+int rq_abi_version(void);
+const char* rq_strerror(int code);
+
+int rq_graph_build(const rq_graph_desc* desc, rq_graph_t* out);
+int rq_graph_free(rq_graph_t g);
+/* info[0] n_streams, [1] n_sinks, [2] n_followers, [3] n_edges, [4] ctrl stream index or -1 */
+int rq_graph_info(rq_graph_t g, int64_t* info);
+/* src_id of every stream index (the ev_src values); ids[n_streams], host */
+int rq_graph_source_ids(rq_graph_t g, int64_t* ids);
+/* sink ids in follower order (the order of rq_batch_desc.s), host */
+int rq_graph_followers(rq_graph_t g, int64_t* ids);
+
+/* bytes of device workspace rq_run_batch needs for this graph/batch */
+int rq_workspace_size(rq_graph_t g, const rq_batch_desc* b, size_t* bytes);
+/* suggested per-replica event-log capacity for RQ_RUN_EVENT_LOG */
+int rq_event_capacity(rq_graph_t g, const rq_batch_desc* b, int64_t* cap);
+
+int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out,
+                 void* workspace, size_t workspace_bytes, void* hip_stream);
+
+/* Metrics on a dataframe in the reference's row layout (State.get_dataframe):
+ * one row per (event, sink), rows in df order, 't' non-decreasing.
+ *   t, src, event_id : device [n_rows]  (event_id may be NULL: counts[0..1] = -1)
+ *   sink_col         : device [n_rows]  column of the row's sink_id among the
+ *                      sorted unique sink ids of the df (pivot_table columns)
+ *   out              : device [nK + 2]  top_K..., avg_rank, r_2
+ *   counts           : device [4]       num_tweets_of(src), world events, pivot rows, columns
+ * Workspace: rq_replay_workspace_size(). */
+int rq_replay_workspace_size(int64_t n_rows, int32_t n_cols, size_t* bytes);
+int rq_metrics_replay(const double* t, const int64_t* src, const int32_t* sink_col,
+                      const int64_t* event_id, int64_t n_rows, int32_t n_cols,
+                      int64_t src_id, double end_time, const int32_t* Ks, int32_t nK,
+                      double* out, int64_t* counts, void* workspace, size_t workspace_bytes,
+                      void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RQ_H */

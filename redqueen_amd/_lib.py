@@ -1,0 +1,114 @@
+"""ctypes binding of librq.so (include/rq.h).
+
+The product path has exactly one implementation: the gfx950 kernels in
+librq.so.  If the shared object is missing this module raises at import --
+there is no CPU fallback.
+"""
+import ctypes as C
+import os
+
+import torch  # noqa: F401  -- load torch's HIP runtime first so librq.so binds to it
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+SO_PATH = os.path.join(_HERE, "librq.so")
+
+RQ_OK, RQ_EINVAL, RQ_EOVERFLOW, RQ_EHIP, RQ_ENOMEM, RQ_EUNSORTED, RQ_EUNSUPPORTED = (
+    0, -1, -2, -3, -4, -5, -6)
+SRC_NONE, SRC_POISSON, SRC_POISSON2, SRC_HAWKES, SRC_PWCONST, SRC_REALDATA, SRC_OPT = range(7)
+ST_ROWS_OVERFLOW, ST_STREAM_OVERFLOW, ST_TIE, ST_EMPTY = 1, 2, 4, 8
+RUN_EVENT_LOG = 1
+MAX_K = 4
+
+_P = C.c_void_p
+_pd = C.POINTER(C.c_double)
+_pi64 = C.POINTER(C.c_int64)
+_pi32 = C.POINTER(C.c_int32)
+_pu32 = C.POINTER(C.c_uint32)
+
+
+class SourceDesc(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("n_arr", C.c_int32), ("src_id", C.c_int64),
+                ("seed", C.c_uint32), ("reserved", C.c_uint32), ("p0", C.c_double),
+                ("p1", C.c_double), ("p2", C.c_double), ("a", _pd), ("b", _pd)]
+
+
+class GraphDesc(C.Structure):
+    _fields_ = [("n_sources", C.c_int32), ("sources", C.POINTER(SourceDesc)),
+                ("n_sinks", C.c_int32), ("sink_ids", _pi64), ("n_edges", C.c_int64),
+                ("edge_src", _pi64), ("edge_sink", _pi64), ("ctrl_src_id", C.c_int64),
+                ("start_time", C.c_double), ("end_time", C.c_double), ("ctrl_n_arr", C.c_int32),
+                ("ctrl_a", _pd), ("ctrl_b", _pd)]
+
+
+class BatchDesc(C.Structure):
+    _fields_ = [("ctrl_kind", C.c_int32), ("n_grid", C.c_int32), ("q", _pd), ("s", _pd),
+                ("n_rep", C.c_int64), ("ctrl_seed", _P), ("ctrl_seed0", C.c_uint32),
+                ("randomize_world", C.c_int32), ("world_seed", _P), ("world_seed0", C.c_uint32),
+                ("seed_mod", C.c_int64), ("ctrl_rate", _P), ("ctrl_rate_max", C.c_double),
+                ("Ks", _pi32), ("nK", C.c_int32), ("max_events", C.c_int64),
+                ("flags", C.c_int32), ("cap_scale", C.c_double), ("chunk", C.c_int64)]
+
+
+class Outputs(C.Structure):
+    _fields_ = [("metrics", _P), ("counts", _P), ("status", _P), ("ev_t", _P),
+                ("ev_src", _P), ("ev_cap", C.c_int64)]
+
+
+class RQError(RuntimeError):
+    def __init__(self, fn, code):
+        self.code = code
+        super().__init__("%s failed: %s (%d)" % (fn, strerror(code), code))
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(SO_PATH):
+        raise ImportError("redqueen_amd: %s is missing -- build it with "
+                          "`python -c 'import __graft_entry__ as g; g.build()'` "
+                          "(there is no CPU fallback)" % SO_PATH)
+    L = C.CDLL(SO_PATH)
+    L.rq_abi_version.restype = C.c_int
+    L.rq_strerror.restype = C.c_char_p
+    L.rq_strerror.argtypes = [C.c_int]
+    L.rq_graph_build.argtypes = [C.POINTER(GraphDesc), C.POINTER(_P)]
+    L.rq_graph_free.argtypes = [_P]
+    L.rq_graph_info.argtypes = [_P, _pi64]
+    L.rq_graph_source_ids.argtypes = [_P, _pi64]
+    L.rq_graph_followers.argtypes = [_P, _pi64]
+    L.rq_workspace_size.argtypes = [_P, C.POINTER(BatchDesc), C.POINTER(C.c_size_t)]
+    L.rq_event_capacity.argtypes = [_P, C.POINTER(BatchDesc), _pi64]
+    L.rq_run_batch.argtypes = [_P, C.POINTER(BatchDesc), C.POINTER(Outputs), _P, C.c_size_t, _P]
+    L.rq_replay_workspace_size.argtypes = [C.c_int64, C.c_int32, C.POINTER(C.c_size_t)]
+    L.rq_metrics_replay.argtypes = [_P, _P, _P, _P, C.c_int64, C.c_int32, C.c_int64, C.c_double,
+                                    _pi32, C.c_int32, _P, _P, _P, C.c_size_t, _P]
+    for fn in ("rq_graph_build", "rq_graph_free", "rq_graph_info", "rq_graph_source_ids",
+               "rq_graph_followers", "rq_workspace_size", "rq_event_capacity", "rq_run_batch",
+               "rq_replay_workspace_size", "rq_metrics_replay"):
+        getattr(L, fn).restype = C.c_int
+    if L.rq_abi_version() != 1:
+        raise ImportError("librq.so ABI version mismatch")
+    _lib = L
+    return L
+
+
+def strerror(code):
+    try:
+        return lib().rq_strerror(code).decode()
+    except Exception:  # pragma: no cover
+        return "error"
+
+
+def check(fn, code):
+    if code != RQ_OK:
+        raise RQError(fn, code)
+
+
+EXPORTED = ["rq_abi_version", "rq_strerror", "rq_graph_build", "rq_graph_free", "rq_graph_info",
+            "rq_graph_source_ids", "rq_graph_followers", "rq_workspace_size",
+            "rq_event_capacity", "rq_run_batch", "rq_replay_workspace_size",
+            "rq_metrics_replay"]

@@ -1,0 +1,563 @@
+// rq_api.cpp -- host side of the C ABI declared in include/rq.h.
+//
+// rq_graph_build does what SimOpts + Manager.__init__ + Broadcaster.init_state
+// do in the reference (opt_model.py:145-181, :340-344, :773-780): validate the
+// network, give every sink a dense column (sorted sink id order, the
+// pivot_table column order of utils.py:54-55), build the per-source sink lists
+// in edge_list order (the Event.sink_ids of opt_model.py:306-307) as CSR, and
+// upload everything once.  rq_run_batch only enqueues kernels.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <numeric>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/rq.h"
+#include "rq_internal.h"
+
+namespace {
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+    int upload(const std::vector<T>& v)
+    {
+        n = v.size();
+        if (hipMalloc(&p, std::max<size_t>(1, n) * sizeof(T)) != hipSuccess) return RQ_ENOMEM;
+        if (n && hipMemcpy(p, v.data(), n * sizeof(T), hipMemcpyHostToDevice) != hipSuccess)
+            return RQ_EHIP;
+        return RQ_OK;
+    }
+};
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+}  // namespace
+
+struct rq_graph {
+    int n_str = 0, ctrl_idx = -1, n_sinks = 0, n_fol = 0;
+    int64_t n_edges = 0, ctrl_src_id = 0;
+    double start = 0.0, end = 0.0;
+    // per stream (sorted by src_id); the controlled slot has kind RQ_SRC_NONE
+    std::vector<int64_t> src_id;
+    std::vector<int> kind, orig_idx, arr_off, arr_n;
+    std::vector<uint32_t> seed;
+    std::vector<double> p0, p1, p2, arr_a, arr_b;
+    std::vector<int> csr_ptr, csr_col, outdeg_f, fol;
+    std::vector<int64_t> fol_ids;
+    std::vector<int> col_to_fol;     // sink column -> follower position or -1
+    // controlled-slot arrays (PiecewiseConst / RealData controlled runs)
+    int ctrl_arr_off = 0, ctrl_arr_n = 0;
+    DevBuf<int64_t> d_src_id;
+    DevBuf<int> d_kind, d_orig, d_arr_off, d_arr_n, d_csr_ptr, d_csr_col, d_outdeg_f, d_fol;
+    DevBuf<uint32_t> d_seed;
+    DevBuf<double> d_p0, d_p1, d_p2, d_arr_a, d_arr_b;
+};
+
+namespace {
+
+struct Plan {
+    int nK = 1, spl = 1, wpb = 4, n_sinks_pad = 0;
+    int64_t R = 0, chunk = 0, capsum = 0, cap_rows = 0;
+    std::vector<int> cap;
+    std::vector<int64_t> st_off;
+    size_t off_invc = 0, off_streams = 0, off_slen = 0, off_rt = 0, off_rs = 0, off_rv = 0,
+           off_rc = 0, off_sall = 0, off_stoff = 0, off_cap = 0, total = 0;
+};
+
+double stream_mean_var(const rq_graph* g, int j, int kind, const rq_batch_desc* b, double* var)
+{
+    const double span = g->end - g->start;
+    double m = 0.0;
+    *var = 0.0;
+    switch (kind) {
+    case RQ_SRC_POISSON:
+    case RQ_SRC_POISSON2: {
+        const double rate = j == g->ctrl_idx ? b->ctrl_rate_max : g->p0[j];
+        m = std::max(0.0, rate) * span;
+        *var = m;
+        break;
+    }
+    case RQ_SRC_HAWKES: {
+        const double l0 = g->p0[j], al = g->p1[j], be = g->p2[j];
+        const double br = be > 0.0 ? al / be : 1.0;
+        if (br < 0.95) {
+            m = l0 * span / (1.0 - br);
+            *var = l0 * span / ((1.0 - br) * (1.0 - br) * (1.0 - br));
+        } else {
+            m = l0 * span * 40.0 + 1000.0;
+            *var = m * m;
+        }
+        break;
+    }
+    case RQ_SRC_PWCONST: {
+        const int off = g->arr_off[j], n = g->arr_n[j];
+        for (int k = 0; k < n; ++k) {
+            const double lo = std::max(g->arr_a[off + k], g->start);
+            const double hi = std::min(k + 1 < n ? g->arr_a[off + k + 1] : g->end, g->end);
+            if (hi > lo) m += std::max(0.0, g->arr_b[off + k]) * (hi - lo);
+        }
+        *var = m;
+        break;
+    }
+    case RQ_SRC_REALDATA:
+        m = g->arr_n[j];
+        *var = 0.0;
+        break;
+    default:
+        break;
+    }
+    return m;
+}
+
+int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
+{
+    if (!g || !b) return RQ_EINVAL;
+    if (b->nK < 1 || b->nK > RQ_MAX_K || !b->Ks) return RQ_EINVAL;
+    if (b->n_grid < 1 || b->n_rep < 1) return RQ_EINVAL;
+    const int ck = b->ctrl_kind;
+    if (ck != RQ_SRC_OPT && ck != RQ_SRC_POISSON2 && ck != RQ_SRC_PWCONST &&
+        ck != RQ_SRC_REALDATA && ck != RQ_SRC_NONE)
+        return RQ_EINVAL;
+    if (ck == RQ_SRC_OPT && (!b->q || (g->n_fol > 0 && !b->s))) return RQ_EINVAL;
+    if (ck == RQ_SRC_POISSON2 && !b->ctrl_rate) return RQ_EINVAL;
+    if ((ck == RQ_SRC_PWCONST) && g->ctrl_arr_n < 1) return RQ_EINVAL;
+    const double scale = b->cap_scale >= 1.0 ? b->cap_scale : 1.0;
+    p->nK = b->nK;
+    p->R = (int64_t)b->n_grid * b->n_rep;
+    p->chunk = b->chunk > 0 ? std::min<int64_t>(b->chunk, p->R) : std::min<int64_t>(p->R, 16384);
+    p->cap.assign(g->n_str, 0);
+    p->st_off.assign(g->n_str, 0);
+    double wall_caps = 0.0;
+    int64_t ctrl_cap = 0;
+    for (int j = 0; j < g->n_str; ++j) {
+        int kind = g->kind[j];
+        if (j == g->ctrl_idx) kind = (ck == RQ_SRC_OPT || ck == RQ_SRC_NONE) ? RQ_SRC_NONE : ck;
+        double var;
+        const double m = stream_mean_var(g, j, kind, b, &var);
+        int64_t c = 0;
+        if (kind != RQ_SRC_NONE)
+            c = kind == RQ_SRC_REALDATA ? (int64_t)m
+                                        : (int64_t)std::ceil((m + 8.0 * std::sqrt(var) + 32.0) * scale);
+        if (c > (int64_t)1 << 30) return RQ_EINVAL;
+        p->cap[j] = (int)c;
+        p->st_off[j] = p->capsum;
+        p->capsum += c;
+        if (j == g->ctrl_idx) ctrl_cap = c;
+        else wall_caps += (double)c;
+    }
+    double rows = wall_caps + (ck == RQ_SRC_OPT ? wall_caps + 1.0 : (double)ctrl_cap) + 8.0;
+    if (b->max_events >= 0) rows = std::min(rows, (double)b->max_events + 1.0);
+    p->cap_rows = std::max<int64_t>(64, (int64_t)rows);
+    p->spl = g->n_str <= 64 ? 1 : g->n_str <= 128 ? 2 : g->n_str <= 256 ? 4 : 8;
+    if (g->n_str > 512) return RQ_EUNSUPPORTED;
+    p->n_sinks_pad = (g->n_sinks + 1) | 1;   // odd stride: spreads replicas over LDS banks
+    const size_t per_wave = (size_t)p->n_sinks_pad * 4;
+    p->wpb = per_wave * 4 <= 64 * 1024 ? 4 : per_wave * 2 <= 80 * 1024 ? 2 : 1;
+    if (per_wave > 160 * 1024) return RQ_EUNSUPPORTED;
+
+    const size_t A = 256;
+    const int64_t C = p->chunk;
+    size_t o = 0;
+    p->off_invc = o;    o = align_up(o + sizeof(double) * (size_t)b->n_grid * g->n_str, A);
+    p->off_stoff = o;   o = align_up(o + sizeof(int64_t) * g->n_str, A);
+    p->off_cap = o;     o = align_up(o + sizeof(int) * g->n_str, A);
+    p->off_streams = o; o = align_up(o + sizeof(double) * (size_t)C * p->capsum, A);
+    p->off_slen = o;    o = align_up(o + sizeof(int) * (size_t)C * g->n_str, A);
+    p->off_rt = o;      o = align_up(o + sizeof(double) * (size_t)C * p->cap_rows, A);
+    p->off_rs = o;      o = align_up(o + sizeof(double) * (size_t)C * p->cap_rows, A);
+    p->off_rv = o;      o = align_up(o + sizeof(uint32_t) * (size_t)C * p->cap_rows, A);
+    p->off_rc = o;      o = align_up(o + sizeof(uint32_t) * (size_t)C * p->cap_rows * p->nK, A);
+    p->off_sall = o;    o = align_up(o + sizeof(int) * (size_t)C, A);
+    p->total = o;
+    return RQ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rq_abi_version(void) { return RQ_ABI_VERSION; }
+
+const char* rq_strerror(int code)
+{
+    switch (code) {
+    case RQ_OK: return "ok";
+    case RQ_EINVAL: return "invalid argument";
+    case RQ_EOVERFLOW: return "capacity overflow";
+    case RQ_EHIP: return "HIP runtime error";
+    case RQ_ENOMEM: return "out of memory";
+    case RQ_EUNSORTED: return "dataframe t column is not sorted";
+    case RQ_EUNSUPPORTED: return "unsupported by this engine";
+    default: return "unknown error";
+    }
+}
+
+int rq_graph_build(const rq_graph_desc* d, rq_graph_t* out)
+{
+    if (!d || !out) return RQ_EINVAL;
+    *out = nullptr;
+    if (d->n_sinks < 1 || !d->sink_ids) return RQ_EINVAL;              // "No sinks."
+    if (d->n_sources < 0 || (d->n_sources > 0 && !d->sources)) return RQ_EINVAL;
+    if (d->n_edges < 0 || (d->n_edges > 0 && (!d->edge_src || !d->edge_sink))) return RQ_EINVAL;
+    if (!(d->end_time >= d->start_time)) return RQ_EINVAL;
+    rq_graph* g = new (std::nothrow) rq_graph();
+    if (!g) return RQ_ENOMEM;
+    std::unique_ptr<rq_graph> guard(g);
+    g->start = d->start_time;
+    g->end = d->end_time;
+    g->ctrl_src_id = d->ctrl_src_id;
+
+    // sinks: dense columns in sorted id order; "Duplicates in sink_ids."
+    std::vector<int64_t> sinks(d->sink_ids, d->sink_ids + d->n_sinks);
+    std::sort(sinks.begin(), sinks.end());
+    if (std::adjacent_find(sinks.begin(), sinks.end()) != sinks.end()) return RQ_EINVAL;
+    g->n_sinks = d->n_sinks;
+    std::unordered_map<int64_t, int> col;
+    for (int c = 0; c < g->n_sinks; ++c) col[sinks[c]] = c;
+
+    // sources: other sources + the controlled slot, sorted by src_id
+    struct S { int64_t id; int orig; };
+    std::vector<S> order;
+    for (int k = 0; k < d->n_sources; ++k) {
+        const rq_source_desc& s = d->sources[k];
+        if (s.kind < RQ_SRC_POISSON || s.kind > RQ_SRC_REALDATA) return RQ_EUNSUPPORTED;
+        if (s.kind == RQ_SRC_PWCONST || s.kind == RQ_SRC_REALDATA) {
+            if (s.n_arr < (s.kind == RQ_SRC_PWCONST ? 1 : 0) || (s.n_arr > 0 && !s.a)) return RQ_EINVAL;
+            if (s.kind == RQ_SRC_PWCONST && !s.b) return RQ_EINVAL;
+        }
+        order.push_back({s.src_id, k});
+    }
+    order.push_back({d->ctrl_src_id, -1});
+    std::sort(order.begin(), order.end(), [](const S& x, const S& y) { return x.id < y.id; });
+    for (size_t k = 1; k < order.size(); ++k)
+        if (order[k].id == order[k - 1].id) return RQ_EINVAL;          // "Duplicates in sources."
+    g->n_str = (int)order.size();
+    std::unordered_map<int64_t, int> sidx;
+    for (int j = 0; j < g->n_str; ++j) {
+        const S& o = order[j];
+        sidx[o.id] = j;
+        g->src_id.push_back(o.id);
+        g->orig_idx.push_back(o.orig);
+        g->arr_off.push_back((int)g->arr_a.size());
+        if (o.orig < 0) {
+            g->ctrl_idx = j;
+            g->kind.push_back(RQ_SRC_NONE);
+            g->seed.push_back(0);
+            g->p0.push_back(0); g->p1.push_back(0); g->p2.push_back(0);
+            g->ctrl_arr_off = (int)g->arr_a.size();
+            int n = 0;
+            if (d->ctrl_n_arr > 0 && d->ctrl_a) {
+                std::vector<double> a(d->ctrl_a, d->ctrl_a + d->ctrl_n_arr);
+                if (d->ctrl_b) {   // piecewise: keep order (asserted sorted)
+                    if (!std::is_sorted(a.begin(), a.end())) return RQ_EINVAL;
+                    for (int q = 0; q < d->ctrl_n_arr; ++q) {
+                        g->arr_a.push_back(a[q]);
+                        g->arr_b.push_back(d->ctrl_b[q]);
+                    }
+                    n = d->ctrl_n_arr;
+                } else {           // real data: times in [start, end], sorted
+                    std::vector<double> keep;
+                    for (double t : a) if (t >= g->start && t <= g->end) keep.push_back(t);
+                    std::sort(keep.begin(), keep.end());
+                    for (double t : keep) { g->arr_a.push_back(t); g->arr_b.push_back(0.0); }
+                    n = (int)keep.size();
+                }
+            }
+            g->ctrl_arr_n = n;
+            g->arr_n.push_back(n);
+            continue;
+        }
+        const rq_source_desc& s = d->sources[o.orig];
+        g->kind.push_back(s.kind);
+        g->seed.push_back(s.seed);
+        g->p0.push_back(s.p0); g->p1.push_back(s.p1); g->p2.push_back(s.p2);
+        int n = 0;
+        if (s.kind == RQ_SRC_PWCONST) {
+            // PiecewiseConst asserts (opt_model.py:631, :644-645)
+            if (!std::is_sorted(s.a, s.a + s.n_arr)) return RQ_EINVAL;
+            if (s.a[0] != g->start || g->end < s.a[s.n_arr - 1]) return RQ_EINVAL;
+            for (int q = 0; q < s.n_arr; ++q) { g->arr_a.push_back(s.a[q]); g->arr_b.push_back(s.b[q]); }
+            n = s.n_arr;
+        } else if (s.kind == RQ_SRC_REALDATA) {
+            std::vector<double> keep;
+            for (int q = 0; q < s.n_arr; ++q)
+                if (s.a[q] >= g->start && s.a[q] <= g->end) keep.push_back(s.a[q]);
+            std::sort(keep.begin(), keep.end());
+            for (double t : keep) { g->arr_a.push_back(t); g->arr_b.push_back(0.0); }
+            n = (int)keep.size();
+        } else if (s.kind == RQ_SRC_HAWKES) {
+            if (!(s.p0 >= 0.0) || !(s.p1 >= 0.0) || !(s.p2 >= 0.0)) return RQ_EINVAL;
+        }
+        g->arr_n.push_back(n);
+    }
+
+    // edges: "Unknown sources/sinks in edge_list." ; CSR in edge-list order
+    std::vector<std::vector<int>> rows(g->n_str);
+    for (int64_t e = 0; e < d->n_edges; ++e) {
+        auto si = sidx.find(d->edge_src[e]);
+        auto ci = col.find(d->edge_sink[e]);
+        if (si == sidx.end() || ci == col.end()) return RQ_EINVAL;
+        rows[si->second].push_back(ci->second);
+    }
+    g->n_edges = d->n_edges;
+    for (int j = 0; j < g->n_str; ++j) {
+        std::vector<int> r = rows[j];
+        std::sort(r.begin(), r.end());
+        // duplicate (source, sink) edges make fractional pivot cells: replay handles them,
+        // the simulation engine does not
+        if (std::adjacent_find(r.begin(), r.end()) != r.end()) return RQ_EUNSUPPORTED;
+    }
+    // followers of the controlled source: sorted sink order (Opt.sink_ids, opt_model.py:341)
+    std::vector<int> fcols = rows[g->ctrl_idx];
+    std::sort(fcols.begin(), fcols.end());
+    g->n_fol = (int)fcols.size();
+    g->col_to_fol.assign(g->n_sinks, -1);
+    for (int f = 0; f < g->n_fol; ++f) {
+        g->col_to_fol[fcols[f]] = f;
+        g->fol_ids.push_back(sinks[fcols[f]]);
+    }
+    g->fol = fcols;
+    g->csr_ptr.push_back(0);
+    for (int j = 0; j < g->n_str; ++j) {
+        const std::vector<int>& r = j == g->ctrl_idx ? fcols : rows[j];
+        int of = 0;
+        for (int c : r) {
+            g->csr_col.push_back(c);
+            of += g->col_to_fol[c] >= 0;
+        }
+        g->outdeg_f.push_back(of);
+        g->csr_ptr.push_back((int)g->csr_col.size());
+    }
+
+    int rc;
+    if ((rc = g->d_src_id.upload(g->src_id)) || (rc = g->d_kind.upload(g->kind)) ||
+        (rc = g->d_orig.upload(g->orig_idx)) || (rc = g->d_arr_off.upload(g->arr_off)) ||
+        (rc = g->d_arr_n.upload(g->arr_n)) || (rc = g->d_csr_ptr.upload(g->csr_ptr)) ||
+        (rc = g->d_csr_col.upload(g->csr_col)) || (rc = g->d_outdeg_f.upload(g->outdeg_f)) ||
+        (rc = g->d_fol.upload(g->fol)) || (rc = g->d_seed.upload(g->seed)) ||
+        (rc = g->d_p0.upload(g->p0)) || (rc = g->d_p1.upload(g->p1)) ||
+        (rc = g->d_p2.upload(g->p2)) || (rc = g->d_arr_a.upload(g->arr_a)) ||
+        (rc = g->d_arr_b.upload(g->arr_b)))
+        return rc;
+    *out = guard.release();
+    return RQ_OK;
+}
+
+int rq_graph_free(rq_graph_t g)
+{
+    delete g;
+    return RQ_OK;
+}
+
+int rq_graph_info(rq_graph_t g, int64_t* info)
+{
+    if (!g || !info) return RQ_EINVAL;
+    info[0] = g->n_str;
+    info[1] = g->n_sinks;
+    info[2] = g->n_fol;
+    info[3] = g->n_edges;
+    info[4] = g->ctrl_idx;
+    return RQ_OK;
+}
+
+int rq_graph_source_ids(rq_graph_t g, int64_t* ids)
+{
+    if (!g || !ids) return RQ_EINVAL;
+    std::copy(g->src_id.begin(), g->src_id.end(), ids);
+    return RQ_OK;
+}
+
+int rq_graph_followers(rq_graph_t g, int64_t* ids)
+{
+    if (!g || !ids) return RQ_EINVAL;
+    std::copy(g->fol_ids.begin(), g->fol_ids.end(), ids);
+    return RQ_OK;
+}
+
+int rq_workspace_size(rq_graph_t g, const rq_batch_desc* b, size_t* bytes)
+{
+    if (!bytes) return RQ_EINVAL;
+    Plan p;
+    const int rc = make_plan(g, b, &p);
+    if (rc) return rc;
+    *bytes = p.total;
+    return RQ_OK;
+}
+
+int rq_event_capacity(rq_graph_t g, const rq_batch_desc* b, int64_t* cap)
+{
+    if (!cap) return RQ_EINVAL;
+    Plan p;
+    const int rc = make_plan(g, b, &p);
+    if (rc) return rc;
+    *cap = p.cap_rows;
+    return RQ_OK;
+}
+
+int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, void* workspace,
+                 size_t workspace_bytes, void* hip_stream)
+{
+    Plan p;
+    int rc = make_plan(g, b, &p);
+    if (rc) return rc;
+    if (!out || !out->metrics || !out->counts || !out->status || !workspace) return RQ_EINVAL;
+    if (workspace_bytes < p.total) return RQ_EINVAL;
+    if ((b->flags & RQ_RUN_EVENT_LOG) && (!out->ev_t || !out->ev_src || out->ev_cap < 1))
+        return RQ_EINVAL;
+    hipStream_t s = (hipStream_t)hip_stream;
+    char* ws = (char*)workspace;
+
+    // c_j = sum over edges (j, i), i a follower, of sqrt(s_i / q)  (opt_model.py:515, :536)
+    std::vector<double> invc((size_t)b->n_grid * g->n_str, 0.0);
+    if (b->ctrl_kind == RQ_SRC_OPT) {
+        std::vector<double> w(g->n_fol);
+        for (int gi = 0; gi < b->n_grid; ++gi) {
+            for (int f = 0; f < g->n_fol; ++f) w[f] = std::sqrt(b->s[(size_t)gi * g->n_fol + f] / b->q[gi]);
+            for (int j = 0; j < g->n_str; ++j) {
+                if (j == g->ctrl_idx) continue;
+                double c = 0.0;
+                for (int e = g->csr_ptr[j]; e < g->csr_ptr[j + 1]; ++e) {
+                    const int f = g->col_to_fol[g->csr_col[e]];
+                    if (f >= 0) c = c + w[f];
+                }
+                invc[(size_t)gi * g->n_str + j] = c > 0.0 ? 1.0 / c : 0.0;
+            }
+        }
+    }
+    if (hipMemcpyAsync(ws + p.off_invc, invc.data(), invc.size() * sizeof(double),
+                       hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(ws + p.off_stoff, p.st_off.data(), p.st_off.size() * sizeof(int64_t),
+                       hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(ws + p.off_cap, p.cap.data(), p.cap.size() * sizeof(int),
+                       hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemsetAsync(out->status, 0, sizeof(int32_t) * p.R, s) != hipSuccess)
+        return RQ_EHIP;
+
+    const int ctrl_stream_kind =
+        (b->ctrl_kind == RQ_SRC_OPT || b->ctrl_kind == RQ_SRC_NONE) ? RQ_SRC_NONE : b->ctrl_kind;
+    for (int64_t c0 = 0; c0 < p.R; c0 += p.chunk) {
+        const int64_t C = std::min(p.chunk, p.R - c0);
+        GenArgs ga{};
+        ga.n_chunk = C;
+        ga.chunk0 = c0;
+        ga.n_str = g->n_str;
+        ga.ctrl_idx = g->ctrl_idx;
+        ga.ctrl_stream_kind = ctrl_stream_kind;
+        ga.randomize = b->randomize_world;
+        ga.seed_mod = b->seed_mod;
+        ga.ctrl_seed = b->ctrl_seed;
+        ga.ctrl_seed0 = b->ctrl_seed0;
+        ga.world_seed = b->world_seed;
+        ga.world_seed0 = b->world_seed0;
+        ga.ctrl_rate = b->ctrl_rate;
+        ga.kind = g->d_kind.p;
+        ga.orig_idx = g->d_orig.p;
+        ga.seed = g->d_seed.p;
+        ga.p0 = g->d_p0.p;
+        ga.p1 = g->d_p1.p;
+        ga.p2 = g->d_p2.p;
+        ga.arr_off = g->d_arr_off.p;
+        ga.arr_n = g->d_arr_n.p;
+        ga.arr_a = g->d_arr_a.p;
+        ga.arr_b = g->d_arr_b.p;
+        ga.st_off = (const int64_t*)(ws + p.off_stoff);
+        ga.cap = (const int*)(ws + p.off_cap);
+        ga.capsum = p.capsum;
+        ga.start = g->start;
+        ga.end = g->end;
+        ga.streams = (double*)(ws + p.off_streams);
+        ga.slen = (int*)(ws + p.off_slen);
+        ga.status = out->status;
+        if (rq_launch_gen(ga, s) != hipSuccess) return RQ_EHIP;
+
+        SweepArgs sa{};
+        sa.n_chunk = C;
+        sa.chunk0 = c0;
+        sa.n_rep = b->n_rep;
+        sa.wpb = p.wpb;
+        sa.n_str = g->n_str;
+        sa.n_sinks = g->n_sinks;
+        sa.n_sinks_pad = p.n_sinks_pad;
+        sa.ctrl_idx = g->ctrl_idx;
+        sa.ctrl_kind = b->ctrl_kind;
+        sa.n_fol = b->ctrl_kind == RQ_SRC_NONE ? 0 : g->n_fol;
+        for (int q = 0; q < RQ_MAX_K; ++q) sa.Ks[q] = q < b->nK ? b->Ks[q] : 1;
+        sa.ctrl_src_id = g->ctrl_src_id;
+        sa.seed_mod = b->seed_mod;
+        sa.ctrl_seed = b->ctrl_seed;
+        sa.ctrl_seed0 = b->ctrl_seed0;
+        sa.src_id = g->d_src_id.p;
+        sa.inv_c = (const double*)(ws + p.off_invc);
+        sa.csr_ptr = g->d_csr_ptr.p;
+        sa.csr_col = g->d_csr_col.p;
+        sa.outdeg_f = g->d_outdeg_f.p;
+        sa.fol = g->d_fol.p;
+        sa.st_off = (const int64_t*)(ws + p.off_stoff);
+        sa.capsum = p.capsum;
+        sa.streams = (const double*)(ws + p.off_streams);
+        sa.slen = (const int*)(ws + p.off_slen);
+        sa.start = g->start;
+        sa.end = g->end;
+        sa.max_events = b->max_events;
+        sa.cap_rows = p.cap_rows;
+        sa.rows_t = (double*)(ws + p.off_rt);
+        sa.rows_sum = (double*)(ws + p.off_rs);
+        sa.rows_valid = (uint32_t*)(ws + p.off_rv);
+        sa.rows_cnt = (uint32_t*)(ws + p.off_rc);
+        sa.sall = (int*)(ws + p.off_sall);
+        sa.counts = out->counts;
+        sa.status = out->status;
+        if (b->flags & RQ_RUN_EVENT_LOG) {
+            sa.ev_t = out->ev_t;
+            sa.ev_src = out->ev_src;
+            sa.ev_cap = out->ev_cap;
+        }
+        if (rq_launch_sweep(sa, p.spl, p.nK, s) != hipSuccess) return RQ_EHIP;
+
+        ScanArgs sc{};
+        sc.n_chunk = C;
+        sc.chunk0 = c0;
+        sc.nrows_from_counts = 1;
+        sc.counts = out->counts;
+        sc.sall = (const int*)(ws + p.off_sall);
+        sc.row_stride = p.cap_rows;
+        sc.rows_t = sa.rows_t;
+        sc.rows_sum = sa.rows_sum;
+        sc.rows_valid = sa.rows_valid;
+        sc.rows_cnt = sa.rows_cnt;
+        sc.end = g->end;
+        sc.metrics = out->metrics;
+        if (rq_launch_scan(sc, p.nK, s) != hipSuccess) return RQ_EHIP;
+    }
+    return RQ_OK;
+}
+
+int rq_replay_workspace_size(int64_t n_rows, int32_t n_cols, size_t* bytes)
+{
+    (void)n_rows;
+    (void)n_cols;
+    if (!bytes) return RQ_EINVAL;
+    *bytes = 0;
+    return RQ_EUNSUPPORTED;
+}
+
+int rq_metrics_replay(const double* t, const int64_t* src, const int32_t* sink_col,
+                      const int64_t* event_id, int64_t n_rows, int32_t n_cols, int64_t src_id,
+                      double end_time, const int32_t* Ks, int32_t nK, double* out, int64_t* counts,
+                      void* workspace, size_t workspace_bytes, void* hip_stream)
+{
+    (void)t; (void)src; (void)sink_col; (void)event_id; (void)n_rows; (void)n_cols;
+    (void)src_id; (void)end_time; (void)Ks; (void)nK; (void)out; (void)counts;
+    (void)workspace; (void)workspace_bytes; (void)hip_stream;
+    return RQ_EUNSUPPORTED;
+}
+
+}  // extern "C"

@@ -1,0 +1,252 @@
+// rq_device.h -- gfx950 device helpers shared by the engine kernels.
+//
+//   * Philox4x32-10 (Salmon et al. SC'11) -- the engine's counter-based RNG:
+//     stream (seed, salt), draw d -> call d>>1, uniform from words (0,1) or
+//     (2,3).  The CPU oracle has its own implementation pinned by Random123's
+//     known-answer vectors; GPU == oracle is checked by the parity tests.
+//   * wave64 helpers (min / ballot / broadcast).
+//   * wave_npsum: numpy's float64 np.sum order (8192-element chunks, pairwise
+//     tree with 8-accumulator leaves <= 128) evaluated by one wavefront: the
+//     leaves run 8 lanes x 8 leaves at a time, the tree above them is walked
+//     by the (uniform) wave with an LDS stack.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rq_spec.h"
+
+#pragma clang fp contract(off)
+
+#define RQ_INF __builtin_huge_val()
+
+namespace rq {
+
+__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1)
+{
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t lo0 = 0xD2511F53u * c[0];
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c[0]);
+        const uint32_t lo1 = 0xCD9E8D57u * c[2];
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c[2]);
+        const uint32_t n0 = hi1 ^ c[1] ^ k0;
+        const uint32_t n2 = hi0 ^ c[3] ^ k1;
+        c[0] = n0;
+        c[1] = lo1;
+        c[2] = n2;
+        c[3] = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+
+__host__ __device__ __forceinline__ uint32_t kind_salt(int kind, bool ctrl)
+{
+    return 0x52510000u | (uint32_t)kind | (ctrl ? 0x100u : 0u);
+}
+
+// Sequential reader of one Philox stream (one lane, one source).
+struct PhiloxStream {
+    uint32_t key0, key1;
+    uint64_t d;        // next draw index
+    uint32_t w2, w3;   // second half of the last call
+    __device__ __forceinline__ PhiloxStream(uint32_t seed, uint32_t salt)
+        : key0(seed), key1(salt), d(0), w2(0), w3(0) {}
+    __device__ __forceinline__ double next()
+    {
+        double u;
+        if ((d & 1) == 0) {
+            const uint64_t call = d >> 1;
+            uint32_t c[4] = {(uint32_t)call, (uint32_t)(call >> 32), 0u, 0u};
+            philox4x32_10(c, key0, key1);
+            w2 = c[2];
+            w3 = c[3];
+            u = rq_uniform53(c[0], c[1]);
+        } else {
+            u = rq_uniform53(w2, w3);
+        }
+        ++d;
+        return u;
+    }
+};
+
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+
+__device__ __forceinline__ double wave_min(double v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+__device__ __forceinline__ double bcast_d(double v, int src_lane)
+{
+    const uint64_t b = rq_dbl_bits(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, src_lane);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), src_lane);
+    return rq_bits_dbl(((uint64_t)hi << 32) | lo);
+}
+
+__device__ __forceinline__ int bcast_i(int v, int src_lane)
+{
+    return __builtin_amdgcn_readlane(v, src_lane);
+}
+
+__device__ __forceinline__ int popc(uint64_t m) { return __popcll(m); }
+
+// ---------------------------------------------------------------------------
+// numpy-order float64 sum of NV sequences of length n, by ONE wavefront.
+// VAL(k, v) fills v[0..NV) with element k of each sequence.
+// lds: >= rq_npsum_lds_doubles<NV>() doubles, private to this wave.
+// ---------------------------------------------------------------------------
+template <int NV>
+__host__ __device__ constexpr int npsum_lds_doubles()
+{
+    // leaf values [NV][128] + leaf (off,len) [128][2 ints = 1 double] + stack [24][NV+1]
+    return NV * 128 + 128 + 24 * (NV + 1);
+}
+
+template <int NV, class VAL>
+__device__ void wave_npsum(int64_t n, VAL&& val, double* lds, double out[NV])
+{
+    const int lane = lane_id();
+    const int grp = lane >> 3, jj = lane & 7;
+    double* leafv = lds;                                   // [NV][128]
+    int* leaf = reinterpret_cast<int*>(lds + NV * 128);    // [128][2]
+    double* stk = lds + NV * 128 + 128;                    // [24][NV+1]
+
+    double res[NV];
+#pragma unroll
+    for (int s = 0; s < NV; ++s) res[s] = 0.0;
+
+    for (int64_t c0 = 0; c0 < n; c0 += 8192) {
+        const int m = (int)((n - c0) < 8192 ? (n - c0) : 8192);
+        // ---- enumerate the leaves of pairwise(m), left to right (uniform) ----
+        int nleaf = 0;
+        {
+            int so[16], sn[16], sp = 0;
+            so[0] = 0;
+            sn[0] = m;
+            sp = 1;
+            while (sp > 0) {
+                --sp;
+                const int o = so[sp], len = sn[sp];
+                if (len <= 128) {
+                    if (lane == 0) {
+                        leaf[2 * nleaf] = o;
+                        leaf[2 * nleaf + 1] = len;
+                    }
+                    ++nleaf;
+                } else {
+                    int n2 = len / 2;
+                    n2 -= n2 % 8;
+                    so[sp] = o + n2;
+                    sn[sp] = len - n2;   // right pushed first
+                    so[sp + 1] = o;
+                    sn[sp + 1] = n2;     // left on top
+                    sp += 2;
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // ---- leaf values: 8 leaves per round, lane jj = accumulator jj ----
+        for (int L0 = 0; L0 < nleaf; L0 += 8) {
+            const int L = L0 + grp;
+            const bool act = L < nleaf;
+            const int off = act ? leaf[2 * L] : 0;
+            const int len = act ? leaf[2 * L + 1] : 0;
+            double r[NV];
+#pragma unroll
+            for (int s = 0; s < NV; ++s) r[s] = 0.0;
+            const int lim = len - (len % 8);
+            if (len >= 8) {
+                val(c0 + off + jj, r);
+                for (int i = 8; i < lim; i += 8) {
+                    double v[NV];
+                    val(c0 + off + i + jj, v);
+#pragma unroll
+                    for (int s = 0; s < NV; ++s) r[s] += v[s];
+                }
+            }
+#pragma unroll
+            for (int s = 0; s < NV; ++s) {
+                double x = r[s];
+                x = x + __shfl_xor(x, 1, 64);   // (r0+r1), (r2+r3), ...
+                x = x + __shfl_xor(x, 2, 64);   // ((r0+r1)+(r2+r3)), ...
+                x = x + __shfl_xor(x, 4, 64);   // (...)+((r4+r5)+(r6+r7))
+                r[s] = x;
+            }
+            if (act && jj == 0) {
+                double v[NV];
+                if (len < 8) {
+#pragma unroll
+                    for (int s = 0; s < NV; ++s) r[s] = -0.0;
+                }
+                for (int i = (len >= 8 ? lim : 0); i < len; ++i) {
+                    val(c0 + off + i, v);
+#pragma unroll
+                    for (int s = 0; s < NV; ++s) r[s] += v[s];
+                }
+#pragma unroll
+                for (int s = 0; s < NV; ++s) leafv[s * 128 + L] = r[s];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // ---- post-order walk of the tree; leaves consumed left to right ----
+        double cv[NV];
+        {
+            int sn[16], st[16], sp = 0, li = 0;
+            sn[0] = m;
+            st[0] = 0;
+            sp = 1;
+            bool have = false;
+            while (sp > 0) {
+                const int top = sp - 1;
+                const int len = sn[top];
+                if (len <= 128) {
+#pragma unroll
+                    for (int s = 0; s < NV; ++s) cv[s] = leafv[s * 128 + li];
+                    ++li;
+                    --sp;
+                    have = true;
+                } else if (st[top] == 0) {
+                    int n2 = len / 2;
+                    n2 -= n2 % 8;
+                    st[top] = 1;
+                    sn[sp] = n2;
+                    st[sp] = 0;
+                    ++sp;
+                    have = false;
+                } else if (st[top] == 1) {
+                    // left value arrived in cv: park it, descend right
+#pragma unroll
+                    for (int s = 0; s < NV; ++s) stk[top * (NV + 1) + s] = cv[s];
+                    int n2 = len / 2;
+                    n2 -= n2 % 8;
+                    st[top] = 2;
+                    sn[sp] = len - n2;
+                    st[sp] = 0;
+                    ++sp;
+                    have = false;
+                } else {
+#pragma unroll
+                    for (int s = 0; s < NV; ++s) cv[s] = stk[top * (NV + 1) + s] + cv[s];
+                    --sp;
+                    have = true;
+                }
+                (void)have;
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < NV; ++s) res[s] = res[s] + cv[s];
+        __builtin_amdgcn_wave_barrier();
+    }
+#pragma unroll
+    for (int s = 0; s < NV; ++s) out[s] = res[s];
+}
+
+}  // namespace rq

@@ -1,0 +1,83 @@
+// rq_internal.h -- kernel argument blocks shared by rq_kernels.hip and rq_api.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/rq.h"
+
+struct GenArgs {
+    int64_t n_chunk, chunk0;
+    int n_str, ctrl_idx, ctrl_stream_kind, randomize;
+    int64_t seed_mod;
+    const uint32_t* ctrl_seed;
+    uint32_t ctrl_seed0;
+    const uint32_t* world_seed;
+    uint32_t world_seed0;
+    const double* ctrl_rate;
+    const int* kind;
+    const int* orig_idx;
+    const uint32_t* seed;
+    const double *p0, *p1, *p2;
+    const int *arr_off, *arr_n;
+    const double *arr_a, *arr_b;
+    const int64_t* st_off;
+    const int* cap;
+    int64_t capsum;
+    double start, end;
+    double* streams;
+    int* slen;
+    int32_t* status;
+};
+
+struct SweepArgs {
+    int64_t n_chunk, chunk0, n_rep;
+    int wpb, n_str, n_sinks, n_sinks_pad, ctrl_idx, ctrl_kind, n_fol;
+    int Ks[RQ_MAX_K];
+    int64_t ctrl_src_id;
+    int64_t seed_mod;
+    const uint32_t* ctrl_seed;
+    uint32_t ctrl_seed0;
+    const int64_t* src_id;     // [n_str]
+    const double* inv_c;       // [n_grid][n_str]
+    const int* csr_ptr;        // [n_str + 1]
+    const int* csr_col;        // sink columns, edge-list order per source
+    const int* outdeg_f;       // [n_str] edges into the controlled source's followers
+    const int* fol;            // [n_fol] follower columns
+    const int64_t* st_off;
+    int64_t capsum;
+    const double* streams;
+    const int* slen;
+    double start, end;
+    int64_t max_events;
+    int64_t cap_rows;
+    double* rows_t;
+    double* rows_sum;
+    uint32_t* rows_valid;
+    uint32_t* rows_cnt;
+    int* sall;
+    int64_t* counts;
+    int32_t* status;
+    double* ev_t;
+    int32_t* ev_src;
+    int64_t ev_cap;
+};
+
+struct ScanArgs {
+    int64_t n_chunk, chunk0;
+    int nrows_from_counts;
+    int64_t nrows;          // used when !nrows_from_counts (replay)
+    int ncols;              // used when sall == nullptr (replay)
+    const int64_t* counts;
+    const int* sall;
+    int64_t row_stride;
+    const double* rows_t;
+    const double* rows_sum;
+    const uint32_t* rows_valid;
+    const uint32_t* rows_cnt;
+    double end;
+    double* metrics;
+};
+
+hipError_t rq_launch_gen(const GenArgs& a, hipStream_t s);
+hipError_t rq_launch_sweep(const SweepArgs& a, int spl, int nK, hipStream_t s);
+hipError_t rq_launch_scan(const ScanArgs& a, int nK, hipStream_t s);

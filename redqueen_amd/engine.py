@@ -1,0 +1,280 @@
+"""Engine front-end: a device-resident graph + batched runs through librq.so.
+
+``Graph`` is the compiled form of a SimOpts (opt_model.py:755-967): other
+sources, sinks and edge list are validated like ``Manager.__init__``
+(opt_model.py:145-181) and uploaded once.  ``Graph.run`` enqueues one batch
+(seeds x grid points) on the current torch stream and returns torch tensors;
+torch is only the device-memory / stream plumbing.
+"""
+import ctypes as C
+import math
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+KIND_BY_NAME = {"Poisson": L.SRC_POISSON, "Poisson2": L.SRC_POISSON2, "Hawkes": L.SRC_HAWKES,
+                "PiecewiseConst": L.SRC_PWCONST, "RealData": L.SRC_REALDATA, "Opt": L.SRC_OPT}
+CTRL_BY_NAME = {"opt": L.SRC_OPT, "poisson": L.SRC_POISSON2, "pwconst": L.SRC_PWCONST,
+                "times": L.SRC_REALDATA, "wall": L.SRC_NONE}
+
+
+def _arr(x, dt):
+    return np.ascontiguousarray(np.asarray(x, dtype=dt))
+
+
+def _source_kind(name):
+    if isinstance(name, str):
+        if name not in KIND_BY_NAME:
+            raise ValueError("Unknown type of broadcaster: {}".format(name))
+        return KIND_BY_NAME[name]
+    kind = getattr(name, "_rq_kind", None)
+    if kind is None:
+        raise NotImplementedError("broadcaster %r has no engine kernel" % (name,))
+    return kind
+
+
+class Graph:
+    """Compiled network.  ``other_sources``: list of (name-or-class, kwargs)."""
+
+    def __init__(self, src_id, other_sources, sink_ids, edge_list, end_time, start_time=0.0,
+                 ctrl_a=None, ctrl_b=None):
+        self._keep = []
+        srcs = []
+        for name, kw in other_sources:
+            kind = _source_kind(name)
+            if kind == L.SRC_OPT:
+                raise NotImplementedError("an Opt broadcaster among the other sources")
+            d = L.SourceDesc()
+            d.kind = kind
+            d.src_id = int(kw["src_id"])
+            d.seed = int(kw.get("seed", 0)) & 0xFFFFFFFF
+            if kind in (L.SRC_POISSON, L.SRC_POISSON2):
+                d.p0 = float(kw.get("rate", 1.0))
+            elif kind == L.SRC_HAWKES:
+                d.p0 = float(kw.get("l_0", 1.0))
+                d.p1 = float(kw.get("alpha", 1.0))
+                d.p2 = float(kw.get("beta", 10.0))
+            elif kind == L.SRC_PWCONST:
+                a = _arr(kw["change_times"], np.float64)
+                b = _arr(kw["rates"], np.float64)
+                if a.size != b.size:
+                    raise ValueError("change_times and rates differ in length")
+                self._keep += [a, b]
+                d.n_arr = a.size
+                d.a = a.ctypes.data_as(L._pd)
+                d.b = b.ctypes.data_as(L._pd)
+            elif kind == L.SRC_REALDATA:
+                a = _arr(kw["times"], np.float64)
+                self._keep.append(a)
+                d.n_arr = a.size
+                d.a = a.ctypes.data_as(L._pd)
+            srcs.append(d)
+        self.src_id = int(src_id)
+        self.end_time = float(end_time)
+        self.start_time = float(start_time)
+        self.sink_ids = _arr(sink_ids, np.int64)
+        edges = list(edge_list)
+        self.edge_src = _arr([e[0] for e in edges], np.int64)
+        self.edge_sink = _arr([e[1] for e in edges], np.int64)
+        arr = (L.SourceDesc * max(1, len(srcs)))(*srcs)
+        gd = L.GraphDesc()
+        gd.n_sources = len(srcs)
+        gd.sources = arr
+        gd.n_sinks = self.sink_ids.size
+        gd.sink_ids = self.sink_ids.ctypes.data_as(L._pi64)
+        gd.n_edges = len(edges)
+        gd.edge_src = self.edge_src.ctypes.data_as(L._pi64)
+        gd.edge_sink = self.edge_sink.ctypes.data_as(L._pi64)
+        gd.ctrl_src_id = self.src_id
+        gd.start_time = self.start_time
+        gd.end_time = self.end_time
+        if ctrl_a is not None:
+            ca = _arr(ctrl_a, np.float64)
+            self._keep.append(ca)
+            gd.ctrl_n_arr = ca.size
+            gd.ctrl_a = ca.ctypes.data_as(L._pd)
+            if ctrl_b is not None:
+                cb = _arr(ctrl_b, np.float64)
+                self._keep.append(cb)
+                gd.ctrl_b = cb.ctypes.data_as(L._pd)
+        h = C.c_void_p()
+        L.check("rq_graph_build", L.lib().rq_graph_build(C.byref(gd), C.byref(h)))
+        self._h = h
+        info = np.zeros(8, dtype=np.int64)
+        L.lib().rq_graph_info(h, info.ctypes.data_as(L._pi64))
+        self.n_streams, self.n_sinks, self.n_followers, self.n_edges, self.ctrl_idx = (
+            int(v) for v in info[:5])
+        self.stream_src_ids = np.zeros(self.n_streams, dtype=np.int64)
+        L.lib().rq_graph_source_ids(h, self.stream_src_ids.ctypes.data_as(L._pi64))
+        self.followers = np.zeros(max(1, self.n_followers), dtype=np.int64)[:self.n_followers]
+        if self.n_followers:
+            L.lib().rq_graph_followers(h, self.followers.ctypes.data_as(L._pi64))
+        self._ws = None
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                L.lib().rq_graph_free(h)
+            except Exception:
+                pass
+
+    # ------------------------------------------------------------------
+    def s_matrix(self, s, n_grid=1):
+        """s as in SimOpts (scalar, vector over sorted followers, or dict sink->s)."""
+        F = self.n_followers
+        if isinstance(s, dict):
+            row = np.asarray([s[int(x)] for x in self.followers], dtype=np.float64)
+        else:
+            row = np.ones(F, dtype=np.float64) * np.asarray(s, dtype=np.float64)
+        return np.ascontiguousarray(np.tile(row, (n_grid, 1)))
+
+    def run(self, ctrl="opt", q=1.0, s=None, n_rep=1, ctrl_seed=0, world_seed=0,
+            randomize=False, seed_mod=0, ctrl_rate=None, Ks=(1,), max_events=None,
+            event_log=False, cap_scale=1.0, chunk=0, stream=None, check=True):
+        """Enqueue one batch.  ``q``: scalar or [n_grid]; ``s``: per grid point
+        row(s) over the sorted followers ([n_grid, F]) or anything ``s_matrix``
+        takes.  Seeds: int base (seed + replica id) or a device uint32 tensor."""
+        dev = torch.device("cuda", torch.cuda.current_device())
+        ck = CTRL_BY_NAME[ctrl] if isinstance(ctrl, str) else int(ctrl)
+        qv = _arr(np.atleast_1d(q), np.float64)
+        n_grid = qv.size
+        if ck == L.SRC_OPT:
+            if s is None:
+                raise ValueError("s required for the RedQueen broadcaster")
+            sm = np.asarray(s, dtype=np.float64) if (isinstance(s, np.ndarray) and s.ndim == 2) \
+                else self.s_matrix(s, n_grid)
+            sm = np.ascontiguousarray(sm, dtype=np.float64)
+            if sm.shape != (n_grid, self.n_followers):
+                raise ValueError("s must be [n_grid, n_followers]")
+        else:
+            sm = np.zeros((n_grid, max(1, self.n_followers)))
+        R = n_grid * int(n_rep)
+        Ks = _arr(Ks, np.int32)
+        if not 1 <= Ks.size <= L.MAX_K:
+            raise ValueError("1..%d K values per run" % L.MAX_K)
+        b = L.BatchDesc()
+        b.ctrl_kind = ck
+        b.n_grid = n_grid
+        b.q = qv.ctypes.data_as(L._pd)
+        b.s = sm.ctypes.data_as(L._pd)
+        b.n_rep = int(n_rep)
+        keep = []
+        if torch.is_tensor(ctrl_seed):
+            cs = ctrl_seed.to(device=dev, dtype=torch.int32).contiguous()
+            keep.append(cs)
+            b.ctrl_seed = cs.data_ptr()
+        else:
+            b.ctrl_seed0 = int(ctrl_seed) & 0xFFFFFFFF
+        b.randomize_world = int(bool(randomize))
+        if torch.is_tensor(world_seed):
+            ws_ = world_seed.to(device=dev, dtype=torch.int32).contiguous()
+            keep.append(ws_)
+            b.world_seed = ws_.data_ptr()
+        else:
+            b.world_seed0 = int(world_seed) & 0xFFFFFFFF
+        b.seed_mod = int(seed_mod)
+        if ck == L.SRC_POISSON2:
+            if ctrl_rate is None:
+                raise ValueError("ctrl_rate required for a Poisson controlled source")
+            cr = torch.as_tensor(ctrl_rate, dtype=torch.float64, device=dev).reshape(-1)
+            if cr.numel() == 1:
+                cr = cr.expand(R)
+            cr = cr.contiguous()
+            keep.append(cr)
+            b.ctrl_rate = cr.data_ptr()
+            b.ctrl_rate_max = float(cr.max().item()) if cr.numel() else 0.0
+        b.Ks = Ks.ctypes.data_as(L._pi32)
+        b.nK = Ks.size
+        b.max_events = -1 if max_events is None or max_events == float("inf") else int(max_events)
+        b.flags = L.RUN_EVENT_LOG if event_log else 0
+        b.cap_scale = float(cap_scale)
+        b.chunk = int(chunk)
+        lib = L.lib()
+        while True:
+            nbytes = C.c_size_t()
+            L.check("rq_workspace_size", lib.rq_workspace_size(self._h, C.byref(b), C.byref(nbytes)))
+            if self._ws is None or self._ws.numel() < nbytes.value:
+                self._ws = None
+                self._ws = torch.empty(max(256, nbytes.value), dtype=torch.uint8, device=dev)
+            metrics = torch.empty((R, Ks.size + 2), dtype=torch.float64, device=dev)
+            counts = torch.empty((R, 4), dtype=torch.int64, device=dev)
+            status = torch.empty(R, dtype=torch.int32, device=dev)
+            out = L.Outputs()
+            out.metrics, out.counts, out.status = metrics.data_ptr(), counts.data_ptr(), status.data_ptr()
+            ev_t = ev_src = None
+            if event_log:
+                cap = C.c_int64()
+                L.check("rq_event_capacity", lib.rq_event_capacity(self._h, C.byref(b), C.byref(cap)))
+                ev_t = torch.empty((R, cap.value), dtype=torch.float64, device=dev)
+                ev_src = torch.empty((R, cap.value), dtype=torch.int32, device=dev)
+                out.ev_t, out.ev_src, out.ev_cap = ev_t.data_ptr(), ev_src.data_ptr(), cap.value
+            st = (stream or torch.cuda.current_stream()).cuda_stream
+            L.check("rq_run_batch", lib.rq_run_batch(self._h, C.byref(b), C.byref(out),
+                                                     self._ws.data_ptr(), self._ws.numel(), st))
+            res = BatchResult(self, metrics, counts, status, ev_t, ev_src, Ks, n_grid, int(n_rep))
+            if not check:
+                return res
+            torch.cuda.current_stream().synchronize()
+            ovf = int((status & (L.ST_ROWS_OVERFLOW | L.ST_STREAM_OVERFLOW)).any().item())
+            if not ovf:
+                return res
+            if b.cap_scale > 64:
+                raise L.RQError("rq_run_batch", L.RQ_EOVERFLOW)
+            b.cap_scale = b.cap_scale * 2.0
+
+
+class BatchResult:
+    """Per-replica outputs (torch tensors on the device), replica i = g * n_rep + r."""
+
+    def __init__(self, graph, metrics, counts, status, ev_t, ev_src, Ks, n_grid, n_rep):
+        self.graph = graph
+        self.metrics, self.counts, self.status = metrics, counts, status
+        self.ev_t, self.ev_src = ev_t, ev_src
+        self.Ks = list(int(k) for k in Ks)
+        self.n_grid, self.n_rep = n_grid, n_rep
+
+    def top_k(self, k):
+        return self.metrics[:, self.Ks.index(k)]
+
+    @property
+    def avg_rank(self):
+        return self.metrics[:, len(self.Ks)]
+
+    @property
+    def r_2(self):
+        return self.metrics[:, len(self.Ks) + 1]
+
+    @property
+    def num_events(self):
+        return self.counts[:, 0]
+
+    @property
+    def world_events(self):
+        return self.counts[:, 1]
+
+    @property
+    def n_events(self):
+        return self.counts[:, 2]
+
+    def events(self, i):
+        """(t, src_id) numpy arrays of replica i (needs event_log=True)."""
+        n = int(self.counts[i, 2].item())
+        t = self.ev_t[i, :n].cpu().numpy()
+        s = self.graph.stream_src_ids[self.ev_src[i, :n].cpu().numpy()]
+        return t, s
+
+
+def expected_events(graph_kw):
+    """Rough expected event count of a world (for sizing benchmarks)."""
+    span = graph_kw["end_time"] - graph_kw.get("start_time", 0.0)
+    tot = 0.0
+    for name, kw in graph_kw["other_sources"]:
+        if name in ("Poisson", "Poisson2"):
+            tot += kw.get("rate", 1.0) * span
+        elif name == "Hawkes":
+            br = kw.get("alpha", 1.0) / kw.get("beta", 10.0)
+            tot += kw.get("l_0", 1.0) * span / max(1e-9, 1 - br)
+    return tot if math.isfinite(tot) else 0.0

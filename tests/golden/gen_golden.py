@@ -1,0 +1,315 @@
+#!/usr/bin/env python
+"""Generate the golden fixtures under tests/golden/ from the REFERENCE itself.
+
+Run in the build container only (the reference never travels to the GPU box):
+
+    MPLBACKEND=Agg python tests/golden/gen_golden.py [--dist N]
+
+It imports MPI-SWS/RedQueen from /root/reference with the local
+``_shim/decorated_options.py`` stand-in on sys.path (the real package is not
+installed and there is no network) and records, as plain data:
+
+  npsum.npz        arrays and np.sum() of them (numpy's pairwise float64 sum)
+  mt_draws.npz     numpy legacy RandomState draws (random_sample, exponential,
+                   poisson, uniform) -- pins the oracle's MT19937 restatement
+  readme_runs.npz  README graph (README.md:60-81) runs create_manager_with_opt
+                   for several seeds: event arrays + metrics from utils.py
+  kat_runs.npz     notebook KATs K1-K6
+  adversarial.npz  hand-made tie-heavy / duplicate (t, sink) / many-sink dfs
+                   with the reference's time_in_top_k / average_rank / int_r_2
+  dist_c2.npz      (--dist N) N-replica C2 ensemble: RedQueen vs Poisson stats
+  dist_world.npz   (--dist N) wall-only ensembles for Hawkes / PiecewiseConst /
+                   Poisson sources (event counts and metrics)
+"""
+import argparse
+import json
+import multiprocessing as mp
+import os
+import sys
+import warnings
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "_shim"))
+sys.path.insert(0, "/root/reference")
+warnings.filterwarnings("ignore")
+os.environ.setdefault("MPLBACKEND", "Agg")
+
+from redqueen.opt_model import SimOpts  # noqa: E402
+import redqueen.utils as U  # noqa: E402
+import pandas as pd  # noqa: E402
+
+README = dict(src_id=1, end_time=100.0, s={1: 1.0, 3: 1.0}, q=1.0, sink_ids=[1, 2, 3],
+              other_sources=[("Poisson2", {"src_id": 2, "seed": 42, "rate": 10}),
+                             ("Hawkes", {"src_id": 3, "seed": 43, "l_0": 10, "alpha": 1.0,
+                                         "beta": 10.0})],
+              edge_list=[(1, 1), (1, 3), (2, 1), (2, 2), (2, 3), (3, 3)])
+
+KAT_BASE = dict(src_id=1, end_time=100.0, q=1.0, sink_ids=[5001, 5002],
+                other_sources=[("Poisson2", {"src_id": 1000, "seed": 42, "rate": 10.0}),
+                               ("Poisson2", {"src_id": 1001, "seed": 43, "rate": 10.0})],
+                edge_list=[(1000, 5001), (1001, 5002), (1, 5001), (1, 5002)])
+
+KS = [1, 2, 5, 10]
+
+
+def metrics(df, so):
+    top = [U.time_in_top_k(df=df, K=k, sim_opts=so) for k in KS]
+    avg = U.average_rank(df, sim_opts=so)
+    r2 = U.int_r_2(df, so)
+    own = len(df.event_id[df.src_id == so.src_id].unique())
+    world = len(df.event_id[df.src_id != so.src_id].unique())
+    return np.asarray(top + [avg, r2], dtype=np.float64), own, world
+
+
+def events_of(df):
+    g = df.groupby("event_id", sort=True).first()
+    return g.t.values, g.time_delta.values, g.src_id.values.astype(np.int64)
+
+
+def gen_npsum():
+    # the inputs are regenerated from (seed, n) by the tests: legacy RandomState
+    # streams are frozen by numpy's compatibility policy, so only sums are stored
+    sizes = list(range(0, 140)) + [255, 256, 257, 1000, 4095, 8191, 8192, 8193, 12345,
+                                   16384, 16385, 50000, 131073]
+    sums = [np.sum(npsum_input(n)) for n in sizes]
+    np.savez_compressed(os.path.join(HERE, "npsum.npz"), sizes=np.asarray(sizes),
+                        sums=np.asarray(sums))
+
+
+def npsum_input(n):
+    rs = np.random.RandomState(1000003 + n)
+    return rs.standard_normal(n) * np.exp(rs.uniform(-30, 30, n))
+
+
+def gen_draws():
+    out = {}
+    for seed in [0, 1, 42, 43, 101, 2**31 + 7, 2**32 - 1]:
+        r = np.random.RandomState(seed)
+        out["rs_%d" % seed] = r.random_sample(256)
+        out["exp_%d" % seed] = np.random.RandomState(seed).exponential(0.37, 256)
+        out["uni_%d" % seed] = np.random.RandomState(seed).uniform(3.0, 100.0, 256)
+        for lam in [0.5, 3.0, 9.99, 10.0, 37.5, 1000.0]:
+            r = np.random.RandomState(seed)
+            out["poi_%d_%g" % (seed, lam)] = np.asarray([r.poisson(lam) for _ in range(64)],
+                                                        dtype=np.float64)
+    np.savez_compressed(os.path.join(HERE, "mt_draws.npz"), **out)
+
+
+def gen_readme():
+    so = SimOpts(**README)
+    rec = {}
+    seeds = [101, 1, 2, 3, 5, 7, 11, 13]
+    for seed in seeds:
+        m = so.create_manager_with_opt(seed=seed)
+        m.run_dynamic()
+        df = m.state.get_dataframe()
+        t, dt, s = events_of(df)
+        met, own, world = metrics(df, so)
+        rec["t_%d" % seed], rec["dt_%d" % seed], rec["src_%d" % seed] = t, dt, s
+        rec["met_%d" % seed] = met
+        rec["cnt_%d" % seed] = np.asarray([own, world, len(df)])
+    # wall-only and Poisson-controlled variants of the same world
+    m = so.create_manager_for_wall()
+    m.run_dynamic()
+    df = m.state.get_dataframe()
+    rec["t_wall"], rec["dt_wall"], rec["src_wall"] = events_of(df)
+    rec["met_wall"], own, world = metrics(df, so)
+    rec["cnt_wall"] = np.asarray([own, world, len(df)])
+    m = so.create_manager_with_poisson(seed=7, capacity=400)
+    m.run_dynamic()
+    df = m.state.get_dataframe()
+    rec["t_pois"], rec["dt_pois"], rec["src_pois"] = events_of(df)
+    rec["met_pois"], own, world = metrics(df, so)
+    rec["cnt_pois"] = np.asarray([own, world, len(df)])
+    # a long horizon: > 8192 pivot rows, exercises the chunked np.sum
+    so_long = so.update({"end_time": 400.0})
+    m = so_long.create_manager_with_opt(seed=3)
+    m.run_dynamic()
+    df = m.state.get_dataframe()
+    rec["t_long"], rec["dt_long"], rec["src_long"] = events_of(df)
+    rec["met_long"], own, world = metrics(df, so_long)
+    rec["cnt_long"] = np.asarray([own, world, len(df)])
+    # max_events truncation
+    m = so.create_manager_with_opt(seed=101)
+    m.run_dynamic(max_events=500)
+    df = m.state.get_dataframe()
+    rec["t_max"], rec["dt_max"], rec["src_max"] = events_of(df)
+    rec["met_max"], own, world = metrics(df, so)
+    rec["cnt_max"] = np.asarray([own, world, len(df)])
+    np.savez_compressed(os.path.join(HERE, "readme_runs.npz"), seeds=np.asarray(seeds), **rec)
+    # a PiecewiseConst + Poisson(dynamic) + RealData world, all kinds in one run
+    so2 = SimOpts(src_id=1, end_time=50.0, s=np.asarray([1.0, 2.0, 0.5]), q=2.0,
+                  sink_ids=[10, 11, 12, 13],
+                  other_sources=[("PiecewiseConst", {"src_id": 4, "seed": 9,
+                                                     "change_times": [0.0, 10.0, 30.0],
+                                                     "rates": [2.0, 8.0, 1.0]}),
+                                 ("Poisson", {"src_id": 5, "seed": 10, "rate": 3.0}),
+                                 ("RealData", {"src_id": 6, "times": [0.5, 7.25, 7.5, 33.0, 49.0, 60.0]}),
+                                 ("Hawkes", {"src_id": 7, "seed": 11, "l_0": 1.5, "alpha": 0.5,
+                                             "beta": 2.0})],
+                  edge_list=[(1, 10), (1, 11), (1, 12), (4, 10), (4, 13), (5, 11), (5, 12),
+                             (6, 10), (6, 11), (6, 12), (6, 13), (7, 12), (7, 13)])
+    rec2 = {}
+    for seed in [3, 4]:
+        m = so2.create_manager_with_opt(seed=seed)
+        m.run_dynamic()
+        df = m.state.get_dataframe()
+        rec2["t_%d" % seed], rec2["dt_%d" % seed], rec2["src_%d" % seed] = events_of(df)
+        rec2["met_%d" % seed], own, world = metrics(df, so2)
+        rec2["cnt_%d" % seed] = np.asarray([own, world, len(df)])
+    np.savez_compressed(os.path.join(HERE, "mixed_runs.npz"), **rec2)
+
+
+def gen_kats():
+    rec = {}
+    # K1/K2: std_poisson(world_seed=42, world_rate=1000.0), Opt seed 1, run()
+    so = SimOpts.std_poisson(world_seed=42, world_rate=1000.0)
+    m = so.create_manager_with_opt(1)
+    m.run()
+    df = m.state.get_dataframe()
+    rec["k1_t"], rec["k1_dt"], rec["k1_src"] = events_of(df)
+    rec["k1_uint"] = np.asarray([U.u_int_opt(df, sim_opts=so)])
+    rec["k2_top10"] = np.asarray([U.time_in_top_k(df, src_id=x, K=10, end_time=1.0)
+                                  for x in (1, 2)])
+    # K3..K6 (opt_broadcast.ipynb:5443-5615)
+    so3 = SimOpts(s=np.asarray([1.0, 1.0]), **KAT_BASE)
+    so5 = SimOpts(s=np.asarray([0.5, 1.5]), **KAT_BASE)
+    for name, so_, kind, seed, cap in [("k3", so3, "opt", 1, None), ("k4", so3, "poisson", 45, 324),
+                                       ("k5", so5, "opt", 1, None), ("k6", so5, "poisson", 4, 325)]:
+        if kind == "opt":
+            m = so_.create_manager_with_opt(seed)
+        else:
+            m = so_.create_manager_with_poisson(seed, capacity=cap)
+        m.run_dynamic()
+        df = m.state.get_dataframe()
+        rec[name + "_t"], rec[name + "_dt"], rec[name + "_src"] = events_of(df)
+        met, own, world = metrics(df, so3)  # notebook evaluates with sim_opts_1's src/end
+        rec[name + "_met"] = met
+        rec[name + "_cnt"] = np.asarray([own, world, len(df), df.shape[1]])
+    np.savez_compressed(os.path.join(HERE, "kat_runs.npz"), **rec)
+
+
+def adversarial_df(rs, n_events, sinks, src_id, tie_p, dup_p, n_sources=4):
+    rows = []
+    t = 0.0
+    for e in range(n_events):
+        if rs.rand() > tie_p:
+            t = t + float(rs.exponential(0.5))
+        src = src_id if rs.rand() < 0.2 else int(rs.randint(2, 2 + n_sources))
+        k = rs.randint(1, min(len(sinks), 6) + 1)
+        ss = list(rs.choice(sinks, k, replace=False))
+        if rs.rand() < dup_p:
+            ss.append(ss[0])
+        for y in ss:
+            rows.append((100 + e, 0.0, src, t, int(y)))
+    return pd.DataFrame.from_records(rows, columns=["event_id", "time_delta", "src_id", "t",
+                                                    "sink_id"])
+
+
+def gen_adversarial():
+    rs = np.random.RandomState(777)
+    rec = {}
+    cases = []
+    specs = [(40, [1, 2, 3], 0.0, 0.0), (40, [1, 2, 3], 0.5, 0.0), (60, [1, 2, 3], 0.4, 0.3),
+             (200, list(range(50, 62)), 0.3, 0.3), (200, list(range(50, 62)), 0.6, 0.5),
+             (300, list(range(1000, 1040)), 0.2, 0.2), (30, [7], 0.5, 0.5),
+             (500, list(range(10, 30)), 0.5, 0.4)]
+    for ci, (ne, sinks, tie_p, dup_p) in enumerate(specs):
+        for rep in range(4):
+            df = adversarial_df(rs, ne, sinks, 1, tie_p, dup_p)
+            end = float(df.t.max()) + 1.0
+            top = [U.time_in_top_k(df=df, K=k, src_id=1, end_time=end) for k in KS]
+            avg = U.average_rank(df, src_id=1, end_time=end)
+            r2 = np.sum(U.rank_of_src_in_df(df, 1).mean(1) ** 2 *
+                        np.diff(np.concatenate([U.rank_of_src_in_df(df, 1).index.values, [end]])))
+            key = "c%d_%d" % (ci, rep)
+            rec[key + "_eid"] = df.event_id.values
+            rec[key + "_src"] = df.src_id.values
+            rec[key + "_t"] = df.t.values
+            rec[key + "_sink"] = df.sink_id.values
+            rec[key + "_end"] = np.asarray([end])
+            rec[key + "_met"] = np.asarray(top + [avg, r2])
+            cases.append(key)
+    np.savez_compressed(os.path.join(HERE, "adversarial.npz"), cases=np.asarray(cases), **rec)
+
+
+# ---------------------------------------------------------------- ensembles
+def _c2_worker(r):
+    so = SimOpts(**README)
+    w = so.randomize_other_sources(r)
+    m = w.create_manager_with_opt(seed=r)
+    m.run_dynamic()
+    df = m.state.get_dataframe()
+    met, own, world = metrics(df, so)
+    n_ev = m.state.get_num_events()
+    m2 = w.create_manager_with_poisson(seed=r, capacity=float(own))
+    m2.run_dynamic()
+    df2 = m2.state.get_dataframe()
+    met2, own2, world2 = metrics(df2, so)
+    return np.concatenate([[own, world, n_ev], met, [own2, world2, m2.state.get_num_events()],
+                           met2])
+
+
+def _world_worker(args):
+    name, r = args
+    so = WORLDS[name]
+    w = so.randomize_other_sources(r)
+    m = w.create_manager_for_wall()
+    m.run_dynamic()
+    df = m.state.get_dataframe()
+    counts = [int(np.sum(df.groupby("event_id").first().src_id.values == x["src_id"]))
+              for _, x in so.other_sources]
+    met, own, world = metrics(df, so)
+    return np.concatenate([counts, met])
+
+
+WORLDS = {
+    "hawkes": SimOpts(src_id=1, end_time=50.0, s=1.0, q=1.0, sink_ids=[1, 2],
+                      other_sources=[("Hawkes", {"src_id": 2, "seed": 0, "l_0": 2.0,
+                                                 "alpha": 1.0, "beta": 2.0}),
+                                     ("Hawkes", {"src_id": 3, "seed": 0, "l_0": 5.0,
+                                                 "alpha": 2.0, "beta": 10.0})],
+                      edge_list=[(2, 1), (3, 1), (3, 2)]),
+    "pwconst": SimOpts(src_id=1, end_time=60.0, s=1.0, q=1.0, sink_ids=[1, 2],
+                       other_sources=[("PiecewiseConst", {"src_id": 2, "seed": 0,
+                                                          "change_times": [0.0, 20.0, 45.0],
+                                                          "rates": [3.0, 0.5, 6.0]}),
+                                      ("Poisson", {"src_id": 3, "seed": 0, "rate": 4.0}),
+                                      ("Poisson2", {"src_id": 4, "seed": 0, "rate": 2.5})],
+                       edge_list=[(2, 1), (3, 2), (4, 1), (4, 2)]),
+}
+
+
+def gen_dist(n):
+    with mp.Pool(os.cpu_count()) as pool:
+        res = np.asarray(pool.map(_c2_worker, range(n), chunksize=16))
+    cols = (["opt_posts", "opt_world", "opt_events"] + ["opt_top%d" % k for k in KS] +
+            ["opt_avg", "opt_r2", "poi_posts", "poi_world", "poi_events"] +
+            ["poi_top%d" % k for k in KS] + ["poi_avg", "poi_r2"])
+    np.savez_compressed(os.path.join(HERE, "dist_c2.npz"), data=res, cols=np.asarray(cols))
+    rec = {}
+    for name in WORLDS:
+        with mp.Pool(os.cpu_count()) as pool:
+            rec[name] = np.asarray(pool.map(_world_worker, [(name, r) for r in range(n)],
+                                            chunksize=16))
+    np.savez_compressed(os.path.join(HERE, "dist_world.npz"), **rec)
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--dist", type=int, default=0)
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    steps = {"npsum": gen_npsum, "draws": gen_draws, "readme": gen_readme, "kats": gen_kats,
+             "adv": gen_adversarial}
+    for k, f in steps.items():
+        if not a.only or k in a.only.split(","):
+            f()
+            print("done", k, flush=True)
+    if a.dist:
+        gen_dist(a.dist)
+        print("done dist", flush=True)
+    with open(os.path.join(HERE, "README.md"), "w") as fh:
+        fh.write(__doc__)
