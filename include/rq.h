@@ -131,6 +131,8 @@ typedef struct rq_batch_desc {
     int32_t flags;               /* RQ_RUN_EVENT_LOG                                              */
     double cap_scale;            /* >= 1: multiplies every auto-sized capacity                   */
     int64_t chunk;               /* replicas in flight per launch wave (0 = library default)     */
+    int32_t sweep_mode;          /* 0 auto, 1 general wave-min sweep, 2 merge (LDS sort) + sorted  */
+                                 /* sweep; both are bit-identical, auto picks the faster one    */
 } rq_batch_desc;
 
 typedef struct rq_outputs {
@@ -177,6 +179,14 @@ int rq_metrics_replay(const double* t, const int64_t* src, const int32_t* sink_c
                       int64_t src_id, double end_time, const int32_t* Ks, int32_t nK,
                       double* out, int64_t* counts, void* workspace, size_t workspace_bytes,
                       void* hip_stream);
+
+/* Per-kernel timing for benchmarks: rq_timing(1) starts recording HIP events
+ * around every kernel this library launches (on the caller's stream);
+ * rq_timing_read() waits for them and returns, per kernel class
+ * [0 stream generation, 1 sweep, 2 scan, 3 replay, 4 merge], the summed milliseconds
+ * and the number of launches, then clears the record.  rq_timing(0) stops. */
+int rq_timing(int enable);
+int rq_timing_read(double* ms, int64_t* launches);
 
 #ifdef __cplusplus
 }

@@ -46,7 +46,8 @@ class BatchDesc(C.Structure):
                 ("randomize_world", C.c_int32), ("world_seed", _P), ("world_seed0", C.c_uint32),
                 ("seed_mod", C.c_int64), ("ctrl_rate", _P), ("ctrl_rate_max", C.c_double),
                 ("Ks", _pi32), ("nK", C.c_int32), ("max_events", C.c_int64),
-                ("flags", C.c_int32), ("cap_scale", C.c_double), ("chunk", C.c_int64)]
+                ("flags", C.c_int32), ("cap_scale", C.c_double), ("chunk", C.c_int64),
+                ("sweep_mode", C.c_int32)]
 
 
 class Outputs(C.Structure):
@@ -86,7 +87,9 @@ def lib():
     L.rq_replay_workspace_size.argtypes = [C.c_int64, C.c_int32, C.POINTER(C.c_size_t)]
     L.rq_metrics_replay.argtypes = [_P, _P, _P, _P, C.c_int64, C.c_int32, C.c_int64, C.c_double,
                                     _pi32, C.c_int32, _P, _P, _P, C.c_size_t, _P]
-    for fn in ("rq_graph_build", "rq_graph_free", "rq_graph_info", "rq_graph_source_ids",
+    L.rq_timing.argtypes = [C.c_int]
+    L.rq_timing_read.argtypes = [_pd, _pi64]
+    for fn in ("rq_timing", "rq_timing_read", "rq_graph_build", "rq_graph_free", "rq_graph_info", "rq_graph_source_ids",
                "rq_graph_followers", "rq_workspace_size", "rq_event_capacity", "rq_run_batch",
                "rq_replay_workspace_size", "rq_metrics_replay"):
         getattr(L, fn).restype = C.c_int
@@ -111,4 +114,4 @@ def check(fn, code):
 EXPORTED = ["rq_abi_version", "rq_strerror", "rq_graph_build", "rq_graph_free", "rq_graph_info",
             "rq_graph_source_ids", "rq_graph_followers", "rq_workspace_size",
             "rq_event_capacity", "rq_run_batch", "rq_replay_workspace_size",
-            "rq_metrics_replay"]
+            "rq_metrics_replay", "rq_timing", "rq_timing_read"]

@@ -27,6 +27,7 @@
 
 #include "rq_device.h"
 #include "rq_internal.h"
+#include "rq_sweep_core.h"
 
 #pragma clang fp contract(off)
 
@@ -148,7 +149,8 @@ __global__ __launch_bounds__(256) void rq_gen_streams(GenArgs a)
 }
 
 // ============================================================================
-// 2. sweep: one wavefront per replica
+// 2a. general sweep: one wavefront per replica, lanes own arrival heads and
+//     pick the next event with a wave-wide min (any number of sources <= 512)
 // ============================================================================
 template <int SPL, int NK>
 __global__ __launch_bounds__(256) void rq_sweep(SweepArgs a)
@@ -172,17 +174,10 @@ __global__ __launch_bounds__(256) void rq_sweep(SweepArgs a)
 #pragma unroll
     for (int q = 0; q < SPL; ++q) {
         const int j = lane * SPL + q;
-        if (j < a.n_str) {
-            off[q] = a.st_off[j];
-            len[q] = slen[j];
-            pos[q] = 0;
-            head[q] = len[q] > 0 ? st[off[q]] : RQ_INF;
-        } else {
-            off[q] = 0;
-            len[q] = 0;
-            pos[q] = 0;
-            head[q] = RQ_INF;
-        }
+        off[q] = j < a.n_str ? (int)a.st_off[j] : 0;
+        len[q] = j < a.n_str ? slen[j] : 0;
+        pos[q] = 0;
+        head[q] = len[q] > 0 ? st[off[q]] : RQ_INF;
     }
     double lmin = RQ_INF;
     int larg = 0;
@@ -193,56 +188,27 @@ __global__ __launch_bounds__(256) void rq_sweep(SweepArgs a)
             larg = q;
         }
 
-    // ---- controlled broadcaster ----
     const bool opt = a.ctrl_kind == RQ_SRC_OPT;
     double opt_next = opt ? a.start : RQ_INF;
     const int64_t k = a.seed_mod > 0 ? i % a.seed_mod : i;
-    const uint32_t oseed = a.ctrl_seed ? a.ctrl_seed[i] : a.ctrl_seed0 + (uint32_t)k;
-    const uint32_t osalt = kind_salt(RQ_SRC_OPT, true);
-    uint64_t obatch = 0;
-    int okk = 128;          // index inside the current batch of 128 exponentials
-    double ox0 = 0.0, ox1 = 0.0;
+    OptDraws od;
+    od.init(a.ctrl_seed ? a.ctrl_seed[i] : a.ctrl_seed0 + (uint32_t)k);
     const double* invc = a.inv_c + (int64_t)g * a.n_str;
 
-    // ---- pivot-row aggregates (Appendix B of SURVEY.md) ----
-    int64_t sumR = 0, sumF = 0;
-    int nvalid = 0;
-    int cnt[NK];
-    int Km1[NK];
-#pragma unroll
-    for (int q = 0; q < NK; ++q) {
-        cnt[q] = 0;
-        Km1[q] = a.Ks[q] - 1;
-    }
-
-    // row staging: lane (row & 63) holds a row until its tile is flushed
-    double r_t = 0.0, r_sum = 0.0;
-    int r_valid = 0;
-    int r_cnt[NK];
-#pragma unroll
-    for (int q = 0; q < NK; ++q) r_cnt[q] = 0;
+    Agg<NK> ag;
+    ag.init(a.Ks);
+    RowStage<NK> rs;
     const int64_t rbase = rl * a.cap_rows;
-    double* Rt = a.rows_t + rbase;
-    double* Rs = a.rows_sum + rbase;
-    uint32_t* Rv = a.rows_valid + rbase;
-    uint32_t* Rc = a.rows_cnt + rbase * NK;   // [row][NK]
-    int64_t nrow = 0;
-    double last_t = -RQ_INF;
-
-    // event log staging
+    rs.init(a.rows_t + rbase, a.rows_sum + rbase, a.rows_valid + rbase, a.rows_cnt + rbase * NK,
+            a.cap_rows);
     const bool evlog = a.ev_t != nullptr;
-    double e_t = 0.0;
-    int e_src = 0;
-    double* Et = evlog ? a.ev_t + i * a.ev_cap : nullptr;
-    int32_t* Es = evlog ? a.ev_src + i * a.ev_cap : nullptr;
+    EvStage es;
+    if (evlog) es.init(a.ev_t + i * a.ev_cap, a.ev_src + i * a.ev_cap, a.ev_cap);
 
     int64_t n_events = 0, posts = 0, world = 0;
     int status = 0;
-    const int64_t maxev = a.max_events;
-
     for (;;) {
-        if (maxev >= 0 && n_events >= maxev) break;
-        // -------- next event: min over lanes, ties -> lowest lane/source --------
+        if (a.max_events >= 0 && n_events >= a.max_events) break;
         const double tw = wave_min(lmin);
         const uint64_t cand = __ballot(lmin == tw);
         const int wl = cand ? (__ffsll((unsigned long long)cand) - 1) : 0;
@@ -258,87 +224,38 @@ __global__ __launch_bounds__(256) void rq_sweep(SweepArgs a)
             tev = tw;
         }
         if (!(tev <= a.end)) break;
-
-        // event log
-        if (evlog) {
-            if (n_events < a.ev_cap) {
-                const int slot = (int)(n_events & 63);
-                if (lane == slot) {
-                    e_t = tev;
-                    e_src = own ? a.ctrl_idx : jw;
-                }
-                if (slot == 63) {
-                    Et[n_events - 63 + lane] = e_t;
-                    Es[n_events - 63 + lane] = e_src;
-                }
-            } else {
-                status |= RQ_ST_ROWS_OVERFLOW;
-            }
-        }
+        if (evlog) es.push(tev, own ? a.ctrl_idx : jw, lane, status);
         ++n_events;
 
         int nsinks;
-        if (own) {
-            // -------- own post: every follower's rank -> 0 (opt_model.py:71-72) --------
-            const int F = a.n_fol;
-            nsinks = F;
-            int dvalid = 0;
-            int dle[NK];
-#pragma unroll
-            for (int q = 0; q < NK; ++q) dle[q] = 0;
-            for (int f0 = 0; f0 < F; f0 += 64) {
-                const int f = f0 + lane;
-                const bool act = f < F;
-                int r = 0;
-                int c = 0;
-                if (act) {
-                    c = a.fol[f];
-                    r = rank[c];
-                }
-                const bool inv = act && r < 0;
-                dvalid += popc(__ballot(inv));
-#pragma unroll
-                for (int q = 0; q < NK; ++q) dle[q] -= popc(__ballot(act && r >= 0 && r <= Km1[q]));
-                if (act) rank[c] = 0;
-            }
-#pragma unroll
-            for (int q = 0; q < NK; ++q) cnt[q] += dle[q] + (0 <= Km1[q] ? F : 0);
-            nvalid += dvalid;
-            sumR -= sumF;
-            sumF = 0;
-            if (opt) {
-                opt_next = RQ_INF;
-            } else {
-                // controlled stream (Poisson2 / PiecewiseConst / RealData): advance its head
-#pragma unroll
-                for (int q = 0; q < SPL; ++q)
-                    if (lane == wl && q == wq) {
-                        ++pos[q];
-                        head[q] = pos[q] < len[q] ? st[off[q] + pos[q]] : RQ_INF;
-                    }
-            }
-            if (F > 0) ++posts;
-        } else {
-            // -------- other source jw --------
+        if (!own || !opt) {
+            // advance the winning head
 #pragma unroll
             for (int q = 0; q < SPL; ++q)
                 if (lane == wl && q == wq) {
                     ++pos[q];
                     head[q] = pos[q] < len[q] ? st[off[q] + pos[q]] : RQ_INF;
                 }
+            if (lane == wl) {
+                lmin = RQ_INF;
+                larg = 0;
+#pragma unroll
+                for (int q = 0; q < SPL; ++q)
+                    if (head[q] < lmin) {
+                        lmin = head[q];
+                        larg = q;
+                    }
+            }
+        }
+        if (own) {
+            nsinks = a.n_fol;
+            ag.own(rank, a.fol, a.n_fol, lane);
+            if (opt) opt_next = RQ_INF;
+            if (nsinks > 0) ++posts;
+        } else {
             if (opt) {
                 // one Exp(c_j) draw per non-own event (opt_model.py:536-544)
-                if (okk == 128) {
-                    const uint64_t call = obatch * 64 + lane;
-                    uint32_t c[4] = {(uint32_t)call, (uint32_t)(call >> 32), 0u, 0u};
-                    philox4x32_10(c, oseed, osalt);
-                    ox0 = rq_std_exponential(rq_uniform53(c[0], c[1]));
-                    ox1 = rq_std_exponential(rq_uniform53(c[2], c[3]));
-                    ++obatch;
-                    okk = 0;
-                }
-                const double x = bcast_d((okk & 1) ? ox1 : ox0, okk >> 1);
-                ++okk;
+                const double x = od.next(lane);
                 const double ic = invc[jw];
                 const double e = ic > 0.0 ? x * ic : RQ_INF;
                 const double c2 = tev + e;
@@ -346,120 +263,219 @@ __global__ __launch_bounds__(256) void rq_sweep(SweepArgs a)
             }
             const int e0 = a.csr_ptr[jw], e1 = a.csr_ptr[jw + 1];
             nsinks = e1 - e0;
-            int dvalid = 0;
-            int dle[NK];
-#pragma unroll
-            for (int q = 0; q < NK; ++q) dle[q] = 0;
-            for (int e = e0; e < e1; e += 64) {
-                const int ee = e + lane;
-                const bool act = ee < e1;
-                int r = 0, c = 0;
-                if (act) {
-                    c = a.csr_col[ee];
-                    r = rank[c];
-                    rank[c] = r < 0 ? 1 : r + 1;
-                }
-                const bool inv = act && r < 0;
-                dvalid += popc(__ballot(inv));
-#pragma unroll
-                for (int q = 0; q < NK; ++q) {
-                    dle[q] += popc(__ballot(inv && 1 <= Km1[q]));
-                    dle[q] -= popc(__ballot(act && r >= 0 && r == Km1[q]));
-                }
-            }
-            nvalid += dvalid;
-#pragma unroll
-            for (int q = 0; q < NK; ++q) cnt[q] += dle[q];
-            sumR += nsinks;
-            sumF += a.outdeg_f[jw];
+            ag.wall(rank, a.csr_col, e0, e1, a.outdeg_f[jw], lane);
             if (nsinks > 0) ++world;
         }
-
-        // lane-local min refresh for the lane whose head moved
-        if (lane == wl) {
-            lmin = RQ_INF;
-            larg = 0;
-#pragma unroll
-            for (int q = 0; q < SPL; ++q)
-                if (head[q] < lmin) {
-                    lmin = head[q];
-                    larg = q;
-                }
-        }
-
-        // -------- pivot row --------
-        if (nsinks > 0) {
-            if (nrow > 0 && tev == last_t) {
-                // same timestamp as the previous row: pivot_table merges them
-                status |= RQ_ST_TIE;
-                const int64_t rr = nrow - 1;
-                if ((nrow & 63) != 0) {
-                    if (lane == (int)(rr & 63)) {
-                        r_sum = (double)sumR;
-                        r_valid = nvalid;
-#pragma unroll
-                        for (int q = 0; q < NK; ++q) r_cnt[q] = cnt[q];
-                    }
-                } else if (lane == 0 && rr < a.cap_rows) {
-                    Rs[rr] = (double)sumR;
-                    Rv[rr] = (uint32_t)nvalid;
-#pragma unroll
-                    for (int q = 0; q < NK; ++q) Rc[rr * NK + q] = (uint32_t)cnt[q];
-                }
-            } else {
-                if (nrow >= a.cap_rows) {
-                    status |= RQ_ST_ROWS_OVERFLOW;
-                    break;
-                }
-                const int slot = (int)(nrow & 63);
-                if (lane == slot) {
-                    r_t = tev;
-                    r_sum = (double)sumR;
-                    r_valid = nvalid;
-#pragma unroll
-                    for (int q = 0; q < NK; ++q) r_cnt[q] = cnt[q];
-                }
-                ++nrow;
-                last_t = tev;
-                if (slot == 63) {
-                    const int64_t rr = nrow - 64 + lane;
-                    Rt[rr] = r_t;
-                    Rs[rr] = r_sum;
-                    Rv[rr] = (uint32_t)r_valid;
-#pragma unroll
-                    for (int q = 0; q < NK; ++q) Rc[rr * NK + q] = (uint32_t)r_cnt[q];
-                }
-            }
-        }
+        if (nsinks > 0 && !rs.emit(tev, ag, lane, status)) break;
     }
-
-    // flush the partial tiles
-    {
-        const int rem = (int)(nrow & 63);
-        if (lane < rem) {
-            const int64_t rr = nrow - rem + lane;
-            Rt[rr] = r_t;
-            Rs[rr] = r_sum;
-            Rv[rr] = (uint32_t)r_valid;
-#pragma unroll
-            for (int q = 0; q < NK; ++q) Rc[rr * NK + q] = (uint32_t)r_cnt[q];
-        }
-        if (evlog && n_events <= a.ev_cap) {
-            const int erem = (int)(n_events & 63);
-            if (lane < erem) {
-                Et[n_events - erem + lane] = e_t;
-                Es[n_events - erem + lane] = e_src;
-            }
-        }
-    }
+    rs.flush(lane);
+    if (evlog) es.flush(lane);
     if (lane == 0) {
         int64_t* cnto = a.counts + i * 4;
         cnto[0] = posts;
         cnto[1] = world;
         cnto[2] = n_events;
-        cnto[3] = nrow;
-        a.sall[rl] = nvalid;
-        if (nrow == 0) status |= RQ_ST_EMPTY;
+        cnto[3] = rs.nrow;
+        a.sall[rl] = ag.nvalid;
+        if (rs.nrow == 0) status |= RQ_ST_EMPTY;
+        if (status) atomicOr(&a.status[i], status);
+    }
+}
+
+// ============================================================================
+// 2b. merge: one workgroup per replica sorts all arrivals of its streams by
+//     (t, source index) with a bitonic network in LDS, in place.
+// ============================================================================
+__global__ __launch_bounds__(256) void rq_merge(MergeArgs a)
+{
+    extern __shared__ double lds_key[];
+    const int64_t rl = blockIdx.x;
+    if (rl >= a.n_chunk) return;
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const int* slen = a.slen + rl * a.n_str;
+    __shared__ int pref[RQ_MAX_STREAMS + 1];
+    if (tid == 0) {
+        int acc = 0;
+        for (int j = 0; j < a.n_str; ++j) {
+            pref[j] = acc;
+            acc += slen[j];
+        }
+        pref[a.n_str] = acc;
+    }
+    __syncthreads();
+    const int n = pref[a.n_str];
+    if (n > a.n2max) {
+        if (tid == 0) {
+            a.mcount[rl] = -1;
+            atomicOr(&a.status[a.chunk0 + rl], RQ_ST_STREAM_OVERFLOW);
+        }
+        return;
+    }
+    int n2 = 64;
+    while (n2 < n) n2 <<= 1;
+    double* key = lds_key;
+    uint16_t* val = reinterpret_cast<uint16_t*>(lds_key + n2);
+    double* st = a.streams + rl * a.capsum;
+    for (int j = 0; j < a.n_str; ++j) {
+        const int o = (int)a.st_off[j], b = pref[j], L = pref[j + 1] - b;
+        for (int q = tid; q < L; q += nt) {
+            key[b + q] = st[o + q];
+            val[b + q] = (uint16_t)j;
+        }
+    }
+    for (int q = n + tid; q < n2; q += nt) {
+        key[q] = RQ_INF;
+        val[q] = 0xFFFF;
+    }
+    __syncthreads();
+    for (int kk = 2; kk <= n2; kk <<= 1) {
+        for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+            for (int q = tid; q < n2; q += nt) {
+                const int p = q ^ jj;
+                if (p > q) {
+                    const double x = key[q], y = key[p];
+                    const uint16_t u = val[q], v = val[p];
+                    const bool gt = x > y || (x == y && u > v);
+                    if (gt == ((q & kk) == 0)) {
+                        key[q] = y;
+                        key[p] = x;
+                        val[q] = v;
+                        val[p] = u;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    uint16_t* ms = a.msrc + rl * a.capsum;
+    for (int q = tid; q < n; q += nt) {
+        st[q] = key[q];
+        ms[q] = val[q];
+    }
+    if (tid == 0) a.mcount[rl] = n;
+}
+
+// ============================================================================
+// 2c. sorted sweep: one wavefront per replica walks the merged arrivals in
+//     64-event tiles (next tile prefetched); graph tables live in LDS.
+// ============================================================================
+template <int NK, class COL>
+__global__ __launch_bounds__(256) void rq_sweep_sorted(SweepArgs a)
+{
+    extern __shared__ double lds_sw[];
+    const int lane = lane_id();
+    const int w = threadIdx.x >> 6;
+    char* base = reinterpret_cast<char*>(lds_sw);
+    COL* col = reinterpret_cast<COL*>(base + a.lds_col);
+    int* cptr = reinterpret_cast<int*>(base + a.lds_ptr);
+    int* odf = reinterpret_cast<int*>(base + a.lds_odf);
+    int* cbf = reinterpret_cast<int*>(base + a.lds_cbf);
+    // block-shared graph tables
+    for (int e = threadIdx.x; e < a.n_csr; e += blockDim.x) col[e] = (COL)a.csr_col[e];
+    for (int j = threadIdx.x; j <= a.n_str; j += blockDim.x) cptr[j] = a.csr_ptr[j];
+    for (int j = threadIdx.x; j < a.n_str; j += blockDim.x) {
+        odf[j] = a.outdeg_f[j];
+        cbf[j] = a.ctrl_src_id < a.src_id[j];
+    }
+    const int64_t rl = (int64_t)blockIdx.x * a.wpb + w;
+    const bool live = rl < a.n_chunk;
+    const int64_t i = a.chunk0 + (live ? rl : 0);
+    const int g = (int)(i / a.n_rep);
+    double* invc = reinterpret_cast<double*>(base + a.lds_wave + (size_t)w * a.lds_wave_stride);
+    int* rank = reinterpret_cast<int*>(base + a.lds_wave + (size_t)w * a.lds_wave_stride +
+                                       a.lds_rank_off);
+    for (int j = lane; j < a.n_str; j += 64) invc[j] = a.inv_c[(int64_t)g * a.n_str + j];
+    for (int c = lane; c < a.n_sinks; c += 64) rank[c] = -1;
+    __syncthreads();
+    if (!live) return;
+
+    const int nm = a.mcount[rl];
+    const double* Mt = a.streams + rl * a.capsum;
+    const uint16_t* Ms = a.msrc + rl * a.capsum;
+    int tb = 0;    // tile base
+    double ct = lane < nm ? Mt[lane] : RQ_INF;
+    int cs = lane < nm ? (int)Ms[lane] : 0;
+    double nt = 64 + lane < nm ? Mt[64 + lane] : RQ_INF;
+    int ns = 64 + lane < nm ? (int)Ms[64 + lane] : 0;
+    int kk = 0;
+
+    const bool opt = a.ctrl_kind == RQ_SRC_OPT;
+    double opt_next = opt ? a.start : RQ_INF;
+    const int64_t k = a.seed_mod > 0 ? i % a.seed_mod : i;
+    OptDraws od;
+    od.init(a.ctrl_seed ? a.ctrl_seed[i] : a.ctrl_seed0 + (uint32_t)k);
+
+    Agg<NK> ag;
+    ag.init(a.Ks);
+    RowStage<NK> rs;
+    const int64_t rbase = rl * a.cap_rows;
+    rs.init(a.rows_t + rbase, a.rows_sum + rbase, a.rows_valid + rbase, a.rows_cnt + rbase * NK,
+            a.cap_rows);
+    const bool evlog = a.ev_t != nullptr;
+    EvStage es;
+    if (evlog) es.init(a.ev_t + i * a.ev_cap, a.ev_src + i * a.ev_cap, a.ev_cap);
+    const COL* fol = col + cptr[a.ctrl_idx];
+
+    int64_t n_events = 0, posts = 0, world = 0;
+    int status = 0;
+    for (;;) {
+        if (a.max_events >= 0 && n_events >= a.max_events) break;
+        if (kk == 64) {
+            tb += 64;
+            ct = nt;
+            cs = ns;
+            const int q = tb + 64 + lane;
+            nt = q < nm ? Mt[q] : RQ_INF;
+            ns = q < nm ? (int)Ms[q] : 0;
+            kk = 0;
+        }
+        const double tw = bcast_d(ct, kk);
+        const int jw = bcast_i(cs, kk);
+        bool own;
+        double tev;
+        if (opt) {
+            own = opt_next < tw || (opt_next == tw && (tw == RQ_INF || cbf[jw]));
+            tev = own ? opt_next : tw;
+        } else {
+            own = jw == a.ctrl_idx;
+            tev = tw;
+        }
+        if (!(tev <= a.end)) break;
+        if (evlog) es.push(tev, own ? a.ctrl_idx : jw, lane, status);
+        ++n_events;
+        if (!own || !opt) ++kk;
+
+        int nsinks;
+        if (own) {
+            nsinks = a.n_fol;
+            ag.own(rank, fol, a.n_fol, lane);
+            if (opt) opt_next = RQ_INF;
+            if (nsinks > 0) ++posts;
+        } else {
+            if (opt) {
+                const double x = od.next(lane);
+                const double ic = invc[jw];
+                const double e = ic > 0.0 ? x * ic : RQ_INF;
+                const double c2 = tev + e;
+                if (c2 < opt_next) opt_next = c2;
+            }
+            const int e0 = cptr[jw], e1 = cptr[jw + 1];
+            nsinks = e1 - e0;
+            ag.wall(rank, col, e0, e1, odf[jw], lane);
+            if (nsinks > 0) ++world;
+        }
+        if (nsinks > 0 && !rs.emit(tev, ag, lane, status)) break;
+    }
+    rs.flush(lane);
+    if (evlog) es.flush(lane);
+    if (lane == 0) {
+        int64_t* cnto = a.counts + i * 4;
+        cnto[0] = posts;
+        cnto[1] = world;
+        cnto[2] = n_events;
+        cnto[3] = rs.nrow;
+        a.sall[rl] = ag.nvalid;
+        if (rs.nrow == 0) status |= RQ_ST_EMPTY;
         if (status) atomicOr(&a.status[i], status);
     }
 }
@@ -539,6 +555,39 @@ hipError_t rq_launch_gen(const GenArgs& a, hipStream_t s)
     dim3 grid((unsigned)((a.n_chunk + 255) / 256), (unsigned)a.n_str);
     hipLaunchKernelGGL(rq_gen_streams, grid, dim3(256), 0, s, a);
     return hipGetLastError();
+}
+
+hipError_t rq_launch_merge(const MergeArgs& a, hipStream_t s)
+{
+    if (a.n_chunk <= 0) return hipSuccess;
+    const size_t lds = (size_t)a.n2max * (sizeof(double) + sizeof(uint16_t));
+    hipLaunchKernelGGL(rq_merge, dim3((unsigned)a.n_chunk), dim3(256), lds, s, a);
+    return hipGetLastError();
+}
+
+template <int NK, class COL>
+static hipError_t launch_sorted_t(const SweepArgs& a, hipStream_t s)
+{
+    const unsigned blocks = (unsigned)((a.n_chunk + a.wpb - 1) / a.wpb);
+    hipLaunchKernelGGL((rq_sweep_sorted<NK, COL>), dim3(blocks), dim3(64 * a.wpb), a.lds_total, s, a);
+    return hipGetLastError();
+}
+
+template <class COL>
+static hipError_t launch_sorted_k(const SweepArgs& a, int nK, hipStream_t s)
+{
+    switch (nK) {
+    case 1: return launch_sorted_t<1, COL>(a, s);
+    case 2: return launch_sorted_t<2, COL>(a, s);
+    case 3: return launch_sorted_t<3, COL>(a, s);
+    default: return launch_sorted_t<4, COL>(a, s);
+    }
+}
+
+hipError_t rq_launch_sweep_sorted(const SweepArgs& a, int nK, int col16, hipStream_t s)
+{
+    if (a.n_chunk <= 0) return hipSuccess;
+    return col16 ? launch_sorted_k<uint16_t>(a, nK, s) : launch_sorted_k<int>(a, nK, s);
 }
 
 hipError_t rq_launch_sweep(const SweepArgs& a, int spl, int nK, hipStream_t s)

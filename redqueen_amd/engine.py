@@ -133,7 +133,7 @@ class Graph:
 
     def run(self, ctrl="opt", q=1.0, s=None, n_rep=1, ctrl_seed=0, world_seed=0,
             randomize=False, seed_mod=0, ctrl_rate=None, Ks=(1,), max_events=None,
-            event_log=False, cap_scale=1.0, chunk=0, stream=None, check=True):
+            event_log=False, cap_scale=1.0, chunk=0, stream=None, check=True, sweep_mode=0):
         """Enqueue one batch.  ``q``: scalar or [n_grid]; ``s``: per grid point
         row(s) over the sorted followers ([n_grid, F]) or anything ``s_matrix``
         takes.  Seeds: int base (seed + replica id) or a device uint32 tensor."""
@@ -192,6 +192,7 @@ class Graph:
         b.flags = L.RUN_EVENT_LOG if event_log else 0
         b.cap_scale = float(cap_scale)
         b.chunk = int(chunk)
+        b.sweep_mode = int(sweep_mode)
         lib = L.lib()
         while True:
             nbytes = C.c_size_t()

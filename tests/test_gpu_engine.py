@@ -56,13 +56,15 @@ def _cmp_replica(res, i, met_o, t_o, s_o, Ks):
     assert c[2] == len(t_o)
 
 
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("seed", [101, 5, 7])
-def test_readme_single(seed):
+def test_readme_single(seed, mode):
     torch, engine, graphs, O = _ctx()
     so = graphs.readme()
     g = _graph(engine, so)
     Ks = (1, 2, 5)
-    res = g.run("opt", q=so["q"], s=so["s"], n_rep=1, ctrl_seed=seed, Ks=Ks, event_log=True)
+    res = g.run("opt", q=so["q"], s=so["s"], n_rep=1, ctrl_seed=seed, Ks=Ks, event_log=True,
+                sweep_mode=mode)
     met_o, t_o, s_o = _oracle(O, so, ("opt", seed), Ks)
     _cmp_replica(res, 0, met_o, t_o, s_o, Ks)
     assert int(res.status[0].item()) == 0
@@ -81,13 +83,15 @@ def test_readme_batch_randomized():
         _cmp_replica(res, r, met_o, t_o, s_o, (1,))
 
 
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("seed", [3, 4, 17])
-def test_mixed_kinds(seed):
+def test_mixed_kinds(seed, mode):
     torch, engine, graphs, O = _ctx()
     so = graphs.mixed()
     g = _graph(engine, so)
     Ks = (1, 2, 5, 10)
-    res = g.run("opt", q=so["q"], s=so["s"], n_rep=1, ctrl_seed=seed, Ks=Ks, event_log=True)
+    res = g.run("opt", q=so["q"], s=so["s"], n_rep=1, ctrl_seed=seed, Ks=Ks, event_log=True,
+                sweep_mode=mode)
     met_o, t_o, s_o = _oracle(O, so, ("opt", seed), Ks)
     _cmp_replica(res, 0, met_o, t_o, s_o, Ks)
 
@@ -106,26 +110,29 @@ def test_kat_weights_and_grid():
             _cmp_replica(res, gi * 3 + r, met_o, t_o, s_o, (1, 2))
 
 
-def test_poisson_controlled_and_wall():
+@pytest.mark.parametrize("mode", [1, 2])
+def test_poisson_controlled_and_wall(mode):
     torch, engine, graphs, O = _ctx()
     so = graphs.readme()
     g = _graph(engine, so)
     rates = torch.tensor([4.0, 0.0, 9.5, 1.25], dtype=torch.float64)
-    res = g.run("poisson", n_rep=4, ctrl_seed=7, ctrl_rate=rates, Ks=(1,), event_log=True)
+    res = g.run("poisson", n_rep=4, ctrl_seed=7, ctrl_rate=rates, Ks=(1,), event_log=True,
+                sweep_mode=mode)
     for r in range(4):
         met_o, t_o, s_o = _oracle(O, so, ("poisson", 7 + r, float(rates[r])), (1,))
         _cmp_replica(res, r, met_o, t_o, s_o, (1,))
-    res = g.run("wall", n_rep=1, Ks=(1, 3), event_log=True)
+    res = g.run("wall", n_rep=1, Ks=(1, 3), event_log=True, sweep_mode=mode)
     met_o, t_o, s_o = _oracle(O, so, ("wall",), (1, 3))
     _cmp_replica(res, 0, met_o, t_o, s_o, (1, 3))
 
 
-def test_max_events():
+@pytest.mark.parametrize("mode", [1, 2])
+def test_max_events(mode):
     torch, engine, graphs, O = _ctx()
     so = graphs.readme()
     g = _graph(engine, so)
     res = g.run("opt", q=1.0, s=so["s"], n_rep=1, ctrl_seed=101, max_events=500, Ks=(1,),
-                event_log=True)
+                event_log=True, sweep_mode=mode)
     met_o, t_o, s_o = _oracle(O, so, ("opt", 101), (1,), max_events=500)
     assert len(t_o) == 500
     _cmp_replica(res, 0, met_o, t_o, s_o, (1,))
@@ -153,7 +160,11 @@ def test_large_batch_no_overflow_and_determinism():
               randomize=True, Ks=(1,))
     b = g.run("opt", q=so["q"], s=so["s"], n_rep=2048, ctrl_seed=0, world_seed=0,
               randomize=True, Ks=(1,), chunk=300)
+    c = g.run("opt", q=so["q"], s=so["s"], n_rep=2048, ctrl_seed=0, world_seed=0,
+              randomize=True, Ks=(1,), sweep_mode=2)
     assert torch.equal(a.metrics, b.metrics) and torch.equal(a.counts, b.counts)
+    # the merge+sorted sweep and the general wave-min sweep are the same machine
+    assert torch.equal(a.metrics, c.metrics) and torch.equal(a.counts, c.counts)
     assert int(a.status.sum().item()) == 0
     ev = a.n_events.double().mean().item()
     assert 4800 < ev < 6200, ev
