@@ -131,12 +131,15 @@ typedef struct rq_batch_desc {
     int32_t flags;               /* RQ_RUN_EVENT_LOG                                              */
     double cap_scale;            /* >= 1: multiplies every auto-sized capacity                   */
     int64_t chunk;               /* replicas in flight per launch wave (0 = library default)     */
+    int64_t replica0;            /* this call runs global replicas [replica0, replica0+n_local):  */
+    int64_t n_local;             /* a shard of the grid (0 = all n_grid*n_rep); outputs are      */
+                                 /* indexed locally, seeds and grid point use the global id     */
     int32_t sweep_mode;          /* 0 auto, 1 general wave-min sweep, 2 merge (LDS sort) + sorted  */
                                  /* sweep; both are bit-identical, auto picks the faster one    */
 } rq_batch_desc;
 
 typedef struct rq_outputs {
-    double* metrics;   /* device [R][nK + 2]: top_K..., avg_rank, r_2     (R = n_grid*n_rep) */
+    double* metrics;   /* device [R][nK + 2]: top_K..., avg_rank, r_2  (R = n_local or n_grid*n_rep) */
     int64_t* counts;   /* device [R][4]: num_events (own posts that reached a sink = the   */
                        /* reference 'capacity'), world_events, n_events (all), pivot rows   */
     int32_t* status;   /* device [R]: RQ_ST_* bits                                            */

@@ -77,7 +77,11 @@ def lib():
         L.rqo_engine_run.argtypes = [C.POINTER(_Scenario), C.POINTER(_Events)]
         L.rqo_engine_batch.restype = C.c_int64
         L.rqo_engine_batch.argtypes = [C.POINTER(_Scenario), C.c_int64, C.c_uint32, C.c_int32,
-                                       i32, C.c_int32, C.c_int32, d, i64]
+                                       i32, C.c_int32, C.c_int32, d, C.c_uint32, d, i64]
+        L.rqo_spec_log.restype = C.c_double
+        L.rqo_spec_log.argtypes = [C.c_double]
+        L.rqo_spec_exp.restype = C.c_double
+        L.rqo_spec_exp.argtypes = [C.c_double]
         _lib = L
     return _lib
 
@@ -264,12 +268,21 @@ def engine_metrics(sc, Ks=(1,)):
                       sc.end_time, Ks), (t, dt, s)
 
 
-def engine_batch(sc, n_rep, seed0=0, randomize=True, Ks=(1,), n_threads=1):
+def engine_batch(sc, n_rep, seed0=0, randomize=True, Ks=(1,), n_threads=1, ctrl_rates=None,
+                 ctrl_seed_offset=0):
+    """n_rep replicas: replica r uses seed u + ctrl_seed_offset (u = seed0 + r) for the
+    controlled source and,
+    with randomize, u + 99*idx for other source idx.  Returns (metrics [n_rep, nK+2],
+    counts [n_rep, 3] = posts, world, events, total events)."""
     Ks = np.ascontiguousarray(Ks, dtype=np.int32)
     out = np.zeros((n_rep, len(Ks) + 2))
     cnt = np.zeros((n_rep, 3), dtype=np.int64)
+    rp = None
+    if ctrl_rates is not None:
+        rates = np.ascontiguousarray(ctrl_rates, dtype=np.float64)
+        rp = _p(rates, C.c_double)
     tot = lib().rqo_engine_batch(C.byref(sc.c), n_rep, seed0, int(randomize),
-                                 _p(Ks, C.c_int32), len(Ks), n_threads,
+                                 _p(Ks, C.c_int32), len(Ks), n_threads, rp, ctrl_seed_offset,
                                  _p(out, C.c_double), _p(cnt, C.c_int64))
     if tot < 0:
         raise RuntimeError("rqo_engine_batch failed: %d" % tot)

@@ -838,8 +838,12 @@ done:
 /* ------------------------------------------------------------------------ */
 /* Batched CPU baseline (engine model + Appendix-B metrics, pthreads)         */
 /* ------------------------------------------------------------------------ */
+double rqo_spec_log(double x) { return rq_log(x); }
+double rqo_spec_exp(double x) { return rq_exp(x); }
+
 typedef struct {
-    const rqo_scenario* sc; int64_t r0, r1; uint32_t seed0; int randomize;
+    const rqo_scenario* sc; int64_t r0, r1; uint32_t seed0; int randomize; const double* rates;
+    uint32_t ctrl_off;
     const int32_t* Ks; int32_t nK; double* out; int64_t* counts; int64_t events; int rc;
 } batch_job;
 
@@ -866,7 +870,8 @@ static void* batch_worker(void* arg)
     for (int64_t r = j->r0; r < j->r1; r++) {
         uint32_t u = j->seed0 + (uint32_t)r;
         memcpy(srcs, sc->sources, sizeof(rqo_source) * ns);
-        srcs[0].seed = u;
+        srcs[0].seed = u + j->ctrl_off;
+        if (j->rates) srcs[0].p0 = j->rates[r];
         if (j->randomize)
             for (int i = 1; i < ns; i++) srcs[i].seed = u + 99u * (uint32_t)(i - 1);
         rqo_scenario s2 = *sc;
@@ -929,7 +934,8 @@ out:
 
 int64_t rqo_engine_batch(const rqo_scenario* sc, int64_t n_rep, uint32_t seed0,
                          int32_t randomize, const int32_t* Ks, int32_t nK,
-                         int32_t n_threads, double* out, int64_t* counts)
+                         int32_t n_threads, const double* ctrl_rates, uint32_t ctrl_seed_offset,
+                         double* out, int64_t* counts)
 {
     if (n_threads < 1) n_threads = 1;
     pthread_t* th = malloc(sizeof(pthread_t) * n_threads);
@@ -938,6 +944,8 @@ int64_t rqo_engine_batch(const rqo_scenario* sc, int64_t n_rep, uint32_t seed0,
     for (int i = 0; i < n_threads; i++) {
         jobs[i].sc = sc; jobs[i].seed0 = seed0; jobs[i].randomize = randomize;
         jobs[i].Ks = Ks; jobs[i].nK = nK; jobs[i].out = out; jobs[i].counts = counts;
+        jobs[i].rates = ctrl_rates;
+        jobs[i].ctrl_off = ctrl_seed_offset;
         jobs[i].r0 = n_rep * i / n_threads;
         jobs[i].r1 = n_rep * (i + 1) / n_threads;
         pthread_create(&th[i], NULL, batch_worker, &jobs[i]);

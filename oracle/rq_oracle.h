@@ -115,10 +115,17 @@ uint32_t rqo_kind_salt(int32_t kind);
 /* Batched CPU baseline: n_rep replicas of the engine model, replica r uses
  * world seeds (u_r + 99*idx) and controlled seed u_r where u_r = seed0 + r,
  * metrics with Appendix-B semantics.  out: [n_rep][nK+2], counts [n_rep][3]
- * (posts, world, events).  n_threads pthreads.  Returns total events. */
+ * (posts, world, events).  n_threads pthreads.  ctrl_rates (may be NULL):
+ * per-replica rate of a Poisson2 controlled source (sources[0] must be
+ * POISSON2).  Returns total events. */
 int64_t rqo_engine_batch(const rqo_scenario* sc, int64_t n_rep, uint32_t seed0,
                          int32_t randomize, const int32_t* Ks, int32_t nK,
-                         int32_t n_threads, double* out, int64_t* counts);
+                         int32_t n_threads, const double* ctrl_rates, uint32_t ctrl_seed_offset,
+                         double* out, int64_t* counts);
+
+/* the engine's arithmetic spec (redqueen_amd/csrc/rq_spec.h), exported for tests */
+double rqo_spec_log(double x);
+double rqo_spec_exp(double x);
 
 #ifdef __cplusplus
 }

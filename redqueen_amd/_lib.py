@@ -47,7 +47,7 @@ class BatchDesc(C.Structure):
                 ("seed_mod", C.c_int64), ("ctrl_rate", _P), ("ctrl_rate_max", C.c_double),
                 ("Ks", _pi32), ("nK", C.c_int32), ("max_events", C.c_int64),
                 ("flags", C.c_int32), ("cap_scale", C.c_double), ("chunk", C.c_int64),
-                ("sweep_mode", C.c_int32)]
+                ("replica0", C.c_int64), ("n_local", C.c_int64), ("sweep_mode", C.c_int32)]
 
 
 class Outputs(C.Structure):

@@ -44,8 +44,7 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // stream around every kernel, summed by rq_timing_read.  Off by default.
 enum { K_GEN = 0, K_SWEEP = 1, K_SCAN = 2, K_REPLAY = 3, K_MERGE = 4, K_N = 5 };
 bool g_timing = false;
-std::mutex g_tab_mu;
-std::unordered_map<void*, std::vector<char>> g_tab_cache;
+
 std::vector<std::pair<hipEvent_t, hipEvent_t>> g_ev[K_N];
 
 struct TimedLaunch {
@@ -68,7 +67,30 @@ struct TimedLaunch {
 
 }  // namespace
 
+namespace {
+constexpr int kStages = 4;
+struct Stage {
+    void* buf = nullptr;
+    size_t bytes = 0;
+    hipEvent_t done = nullptr;
+};
+}  // namespace
+
 struct rq_graph {
+    // pinned staging ring for the per-run parameter tables
+    std::mutex stage_mu;
+    Stage stage[kStages];
+    int stage_next = 0;
+    ~rq_graph()
+    {
+        for (Stage& st : stage) {
+            if (st.done) {
+                (void)hipEventSynchronize(st.done);
+                (void)hipEventDestroy(st.done);
+            }
+            if (st.buf) (void)hipHostFree(st.buf);
+        }
+    }
     int n_str = 0, ctrl_idx = -1, n_sinks = 0, n_fol = 0;
     int64_t n_edges = 0, ctrl_src_id = 0;
     double start = 0.0, end = 0.0;
@@ -167,7 +189,10 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     if ((ck == RQ_SRC_PWCONST) && g->ctrl_arr_n < 1) return RQ_EINVAL;
     const double scale = b->cap_scale >= 1.0 ? b->cap_scale : 1.0;
     p->nK = b->nK;
-    p->R = (int64_t)b->n_grid * b->n_rep;
+    const int64_t Rall = (int64_t)b->n_grid * b->n_rep;
+    if (b->replica0 < 0 || b->n_local < 0 || b->replica0 + b->n_local > Rall) return RQ_EINVAL;
+    p->R = b->n_local > 0 ? b->n_local : Rall - b->replica0;
+    if (p->R < 1) return RQ_EINVAL;
     p->chunk = b->chunk > 0 ? std::min<int64_t>(b->chunk, p->R) : std::min<int64_t>(p->R, 16384);
     p->cap.assign(g->n_str, 0);
     p->st_off.assign(g->n_str, 0);
@@ -502,20 +527,30 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             }
         }
     }
-    // parameter tables [inv_c | st_off | cap]: uploaded only when this workspace does not
-    // already hold exactly these bytes (a pageable copy would stall the host on the stream)
+    // parameter tables [inv_c | st_off | cap]: staged in one of the graph's pinned host
+    // buffers so the copy is truly asynchronous (a pageable copy would stall the host)
     {
-        std::vector<char> tab(p.tables_bytes);
-        std::memcpy(tab.data() + p.off_invc, invc.data(), invc.size() * sizeof(double));
-        std::memcpy(tab.data() + p.off_stoff, p.st_off.data(), p.st_off.size() * sizeof(int64_t));
-        std::memcpy(tab.data() + p.off_cap, p.cap.data(), p.cap.size() * sizeof(int));
-        std::lock_guard<std::mutex> lk(g_tab_mu);
-        auto it = g_tab_cache.find(workspace);
-        if (it == g_tab_cache.end() || it->second != tab) {
-            if (hipMemcpyAsync(ws, tab.data(), tab.size(), hipMemcpyHostToDevice, s) != hipSuccess)
-                return RQ_EHIP;
-            g_tab_cache[workspace] = std::move(tab);
+        std::lock_guard<std::mutex> lk(g->stage_mu);
+        Stage& st = g->stage[g->stage_next];
+        g->stage_next = (g->stage_next + 1) % kStages;
+        if (st.done && hipEventSynchronize(st.done) != hipSuccess) return RQ_EHIP;
+        if (st.bytes < p.tables_bytes) {
+            if (st.buf) (void)hipHostFree(st.buf);
+            st.buf = nullptr;
+            st.bytes = 0;
+            if (hipHostMalloc(&st.buf, p.tables_bytes, hipHostMallocDefault) != hipSuccess)
+                return RQ_ENOMEM;
+            st.bytes = p.tables_bytes;
         }
+        if (!st.done && hipEventCreateWithFlags(&st.done, hipEventDisableTiming) != hipSuccess)
+            return RQ_EHIP;
+        char* tab = (char*)st.buf;
+        std::memcpy(tab + p.off_invc, invc.data(), invc.size() * sizeof(double));
+        std::memcpy(tab + p.off_stoff, p.st_off.data(), p.st_off.size() * sizeof(int64_t));
+        std::memcpy(tab + p.off_cap, p.cap.data(), p.cap.size() * sizeof(int));
+        if (hipMemcpyAsync(ws, tab, p.tables_bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipEventRecord(st.done, s) != hipSuccess)
+            return RQ_EHIP;
     }
     if (hipMemsetAsync(out->status, 0, sizeof(int32_t) * p.R, s) != hipSuccess) return RQ_EHIP;
 
@@ -526,6 +561,7 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
         GenArgs ga{};
         ga.n_chunk = C;
         ga.chunk0 = c0;
+        ga.rep0 = b->replica0;
         ga.n_str = g->n_str;
         ga.ctrl_idx = g->ctrl_idx;
         ga.ctrl_stream_kind = ctrl_stream_kind;
@@ -563,6 +599,7 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
         sa.n_chunk = C;
         sa.chunk0 = c0;
         sa.n_rep = b->n_rep;
+        sa.rep0 = b->replica0;
         sa.wpb = p.wpb;
         sa.n_str = g->n_str;
         sa.n_sinks = g->n_sinks;
@@ -640,8 +677,8 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
         ScanArgs sc{};
         sc.n_chunk = C;
         sc.chunk0 = c0;
-        sc.nrows_from_counts = 1;
-        sc.counts = out->counts;
+        sc.nrows = out->counts + 3;
+        sc.nrows_stride = 4;
         sc.sall = (const int*)(ws + p.off_sall);
         sc.row_stride = p.cap_rows;
         sc.rows_t = sa.rows_t;
@@ -688,13 +725,33 @@ int rq_timing_read(double* ms, int64_t* launches)
     return rq_timing(g_timing ? 1 : 0);
 }
 
+namespace {
+struct ReplayPlan {
+    size_t off_rt, off_rs, off_rv, off_rc, off_state, off_nrows, off_sall, off_err, total;
+};
+ReplayPlan replay_plan(int64_t n_rows, int32_t n_cols)
+{
+    ReplayPlan p{};
+    const size_t A = 256;
+    size_t o = 0;
+    p.off_rt = o;    o = align_up(o + 8 * (size_t)n_rows, A);
+    p.off_rs = o;    o = align_up(o + 8 * (size_t)n_rows, A);
+    p.off_rv = o;    o = align_up(o + 4 * (size_t)n_rows, A);
+    p.off_rc = o;    o = align_up(o + 4 * (size_t)n_rows * RQ_MAX_K, A);
+    p.off_state = o; o = align_up(o + 40 * (size_t)n_cols, A);
+    p.off_nrows = o; o = align_up(o + 8, A);
+    p.off_sall = o;  o = align_up(o + 4, A);
+    p.off_err = o;   o = align_up(o + 4, A);
+    p.total = o;
+    return p;
+}
+}  // namespace
+
 int rq_replay_workspace_size(int64_t n_rows, int32_t n_cols, size_t* bytes)
 {
-    (void)n_rows;
-    (void)n_cols;
-    if (!bytes) return RQ_EINVAL;
-    *bytes = 0;
-    return RQ_EUNSUPPORTED;
+    if (!bytes || n_rows < 1 || n_cols < 1) return RQ_EINVAL;
+    *bytes = replay_plan(n_rows, n_cols).total;
+    return RQ_OK;
 }
 
 int rq_metrics_replay(const double* t, const int64_t* src, const int32_t* sink_col,
@@ -702,10 +759,64 @@ int rq_metrics_replay(const double* t, const int64_t* src, const int32_t* sink_c
                       double end_time, const int32_t* Ks, int32_t nK, double* out, int64_t* counts,
                       void* workspace, size_t workspace_bytes, void* hip_stream)
 {
-    (void)t; (void)src; (void)sink_col; (void)event_id; (void)n_rows; (void)n_cols;
-    (void)src_id; (void)end_time; (void)Ks; (void)nK; (void)out; (void)counts;
-    (void)workspace; (void)workspace_bytes; (void)hip_stream;
-    return RQ_EUNSUPPORTED;
+    if (!t || !src || !sink_col || !out || !counts || !workspace || !Ks) return RQ_EINVAL;
+    if (n_rows < 1 || n_cols < 1 || nK < 1 || nK > RQ_MAX_K) return RQ_EINVAL;
+    const ReplayPlan p = replay_plan(n_rows, n_cols);
+    if (workspace_bytes < p.total) return RQ_EINVAL;
+    hipStream_t s = (hipStream_t)hip_stream;
+    char* ws = (char*)workspace;
+    ReplayArgs ra{};
+    ra.t = t;
+    ra.src = src;
+    ra.col = sink_col;
+    ra.eid = event_id;
+    ra.n_rows = n_rows;
+    ra.n_cols = n_cols;
+    ra.src_id = src_id;
+    for (int q = 0; q < RQ_MAX_K; ++q) ra.Ks[q] = q < nK ? Ks[q] : 1;
+    ra.lds_state = (size_t)n_cols * 40 <= 120 * 1024;
+    double* cell = (double*)(ws + p.off_state);
+    ra.cell = cell;
+    ra.gsum = cell + n_cols;
+    int* q = (int*)(ra.gsum + n_cols);
+    ra.pos = q;
+    ra.last = q + n_cols;
+    ra.gtag = q + 2 * n_cols;
+    ra.gcnt = q + 3 * n_cols;
+    ra.ctag = q + 4 * n_cols;
+    ra.touched = q + 5 * n_cols;
+    ra.cap_rows = n_rows;
+    ra.rows_t = (double*)(ws + p.off_rt);
+    ra.rows_sum = (double*)(ws + p.off_rs);
+    ra.rows_valid = (uint32_t*)(ws + p.off_rv);
+    ra.rows_cnt = (uint32_t*)(ws + p.off_rc);
+    ra.nrows = (int64_t*)(ws + p.off_nrows);
+    ra.sall = (int*)(ws + p.off_sall);
+    ra.counts = counts;
+    ra.metrics = out;
+    ra.err = (int32_t*)(ws + p.off_err);
+    {
+        TimedLaunch tl(K_REPLAY, s);
+        if (rq_launch_replay(ra, nK, s) != hipSuccess) return RQ_EHIP;
+    }
+    ScanArgs sc{};
+    sc.n_chunk = 1;
+    sc.chunk0 = 0;
+    sc.nrows = ra.nrows;
+    sc.nrows_stride = 1;
+    sc.sall = ra.sall;
+    sc.row_stride = n_rows;
+    sc.rows_t = ra.rows_t;
+    sc.rows_sum = ra.rows_sum;
+    sc.rows_valid = ra.rows_valid;
+    sc.rows_cnt = ra.rows_cnt;
+    sc.end = end_time;
+    sc.metrics = out;
+    {
+        TimedLaunch tl(K_SCAN, s);
+        if (rq_launch_scan(sc, nK, s) != hipSuccess) return RQ_EHIP;
+    }
+    return RQ_OK;
 }
 
 }  // extern "C"

@@ -6,7 +6,7 @@
 #include "../../include/rq.h"
 
 struct GenArgs {
-    int64_t n_chunk, chunk0;
+    int64_t n_chunk, chunk0, rep0;   // local replica = chunk0 + rl, global = rep0 + local
     int n_str, ctrl_idx, ctrl_stream_kind, randomize;
     int64_t seed_mod;
     const uint32_t* ctrl_seed;
@@ -32,7 +32,7 @@ struct GenArgs {
 #define RQ_MAX_STREAMS 512
 
 struct MergeArgs {
-    int64_t n_chunk, chunk0;
+    int64_t n_chunk, chunk0;         // local indices
     int n_str, n2max;
     const int64_t* st_off;
     int64_t capsum;
@@ -44,7 +44,7 @@ struct MergeArgs {
 };
 
 struct SweepArgs {
-    int64_t n_chunk, chunk0, n_rep;
+    int64_t n_chunk, chunk0, n_rep, rep0;
     int wpb, n_str, n_sinks, n_sinks_pad, ctrl_idx, ctrl_kind, n_fol;
     int Ks[RQ_MAX_K];
     int64_t ctrl_src_id;
@@ -83,11 +83,9 @@ struct SweepArgs {
 
 struct ScanArgs {
     int64_t n_chunk, chunk0;
-    int nrows_from_counts;
-    int64_t nrows;          // used when !nrows_from_counts (replay)
-    int ncols;              // used when sall == nullptr (replay)
-    const int64_t* counts;
-    const int* sall;
+    const int64_t* nrows;   // number of pivot rows of replica rl at nrows[(chunk0+rl)*nrows_stride]
+    int64_t nrows_stride;
+    const int* sall;        // sink columns S of replica rl (chunk-relative)
     int64_t row_stride;
     const double* rows_t;
     const double* rows_sum;
@@ -102,3 +100,36 @@ hipError_t rq_launch_sweep(const SweepArgs& a, int spl, int nK, hipStream_t s);
 hipError_t rq_launch_scan(const ScanArgs& a, int nK, hipStream_t s);
 hipError_t rq_launch_merge(const MergeArgs& a, hipStream_t s);
 hipError_t rq_launch_sweep_sorted(const SweepArgs& a, int nK, int col16, hipStream_t s);
+
+struct ReplayArgs {
+    const double* t;
+    const int64_t* src;
+    const int32_t* col;
+    const int64_t* eid;     // may be null
+    int64_t n_rows;
+    int n_cols;
+    int64_t src_id;
+    int Ks[RQ_MAX_K];
+    int lds_state;          // 1: per-sink state lives in LDS (n_cols * 40 B fits)
+    // per-sink state (global workspace) [n_cols] each
+    int* pos;
+    int* last;
+    int* gtag;
+    int* gcnt;
+    int* ctag;
+    double* cell;
+    double* gsum;
+    int* touched;           // [n_cols]
+    // pivot-row log
+    int64_t cap_rows;
+    double* rows_t;
+    double* rows_sum;
+    uint32_t* rows_valid;
+    uint32_t* rows_cnt;
+    int64_t* nrows;         // out [1]
+    int* sall;              // out [1]
+    int64_t* counts;        // out [4] (caller buffer)
+    double* metrics;        // caller buffer (NaN-filled on error)
+    int32_t* err;           // out [1]: 0 ok, 1 unsorted t
+};
+hipError_t rq_launch_replay(const ReplayArgs& a, int nK, hipStream_t s);

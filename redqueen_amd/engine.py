@@ -133,7 +133,7 @@ class Graph:
 
     def run(self, ctrl="opt", q=1.0, s=None, n_rep=1, ctrl_seed=0, world_seed=0,
             randomize=False, seed_mod=0, ctrl_rate=None, Ks=(1,), max_events=None,
-            event_log=False, cap_scale=1.0, chunk=0, stream=None, check=True, sweep_mode=0):
+            event_log=False, cap_scale=1.0, chunk=0, stream=None, check=True, sweep_mode=0, replica0=0, n_local=0):
         """Enqueue one batch.  ``q``: scalar or [n_grid]; ``s``: per grid point
         row(s) over the sorted followers ([n_grid, F]) or anything ``s_matrix``
         takes.  Seeds: int base (seed + replica id) or a device uint32 tensor."""
@@ -151,7 +151,8 @@ class Graph:
                 raise ValueError("s must be [n_grid, n_followers]")
         else:
             sm = np.zeros((n_grid, max(1, self.n_followers)))
-        R = n_grid * int(n_rep)
+        R_all = n_grid * int(n_rep)
+        R = int(n_local) if n_local else R_all - int(replica0)
         Ks = _arr(Ks, np.int32)
         if not 1 <= Ks.size <= L.MAX_K:
             raise ValueError("1..%d K values per run" % L.MAX_K)
@@ -181,7 +182,7 @@ class Graph:
                 raise ValueError("ctrl_rate required for a Poisson controlled source")
             cr = torch.as_tensor(ctrl_rate, dtype=torch.float64, device=dev).reshape(-1)
             if cr.numel() == 1:
-                cr = cr.expand(R)
+                cr = cr.expand(R_all)
             cr = cr.contiguous()
             keep.append(cr)
             b.ctrl_rate = cr.data_ptr()
@@ -193,6 +194,8 @@ class Graph:
         b.cap_scale = float(cap_scale)
         b.chunk = int(chunk)
         b.sweep_mode = int(sweep_mode)
+        b.replica0 = int(replica0)
+        b.n_local = int(n_local)
         lib = L.lib()
         while True:
             nbytes = C.c_size_t()
@@ -216,6 +219,7 @@ class Graph:
             L.check("rq_run_batch", lib.rq_run_batch(self._h, C.byref(b), C.byref(out),
                                                      self._ws.data_ptr(), self._ws.numel(), st))
             res = BatchResult(self, metrics, counts, status, ev_t, ev_src, Ks, n_grid, int(n_rep))
+            res.replica0 = int(replica0)
             if not check:
                 return res
             torch.cuda.current_stream().synchronize()

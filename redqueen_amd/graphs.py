@@ -75,15 +75,16 @@ def mixed():
 
 def followers_graph(num_followers=1000, num_sources=50, degree=5, end_time=100.0,
                     kinds=("Poisson2", "Hawkes"), world_rate=1.0, alpha=1.0, beta=10.0,
-                    seed=42, network_seed=1024):
+                    seed=42, network_seed=1024, max_num_followers=None):
     """C3 ("syn1k") and C5: the construction of
     opt_runs.prepare_multiple_followers_sim_opts (opt_runs.py:726-795) with the
     broadcaster kinds interleaved in contiguous blocks (first half kinds[0], ...).
     Followers 1000.., broadcasters 5000.., the controlled source 1 follows all."""
     rs = np.random.RandomState(seed)
-    fol_ids = 1000 + np.arange(num_followers)
+    nmax = num_followers if max_num_followers is None else max_num_followers
+    fol_ids = 1000 + np.arange(nmax)
     b_ids = 5000 + np.arange(num_sources)
-    edges = make_edge_list(num_followers, num_sources, degree, network_seed,
+    edges = make_edge_list(nmax, num_sources, degree, network_seed,
                            follower_id_offset=1000, broadcaster_id_offset=5000)
     others = []
     per = int(np.ceil(num_sources / len(kinds)))

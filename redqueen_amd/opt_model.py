@@ -1,0 +1,450 @@
+"""Drop-in surface of the reference's ``redqueen/opt_model.py``.
+
+Same class names, constructor arguments, factories, validation and errors as
+the reference (file:line below); the simulation itself runs in librq.so on
+the GPU.  Broadcaster objects here are parameter holders: their arrival
+processes are implemented by the gfx950 kernels (engine semantics),
+so ``get_next_interval`` is not called from Python.
+
+    SimOpts            opt_model.py:755-967
+    Manager            opt_model.py:144-314
+    State / Event      opt_model.py:20-141
+    Poisson, Poisson2, Hawkes, PiecewiseConst, RealData, Opt   :381-750
+"""
+import logging
+import warnings
+
+import numpy as np
+import pandas as pd
+
+from . import _lib as L
+from .utils import is_sorted, mb
+
+
+class Event:
+    def __init__(self, event_id, time_delta, cur_time, src_id, sink_ids, metadata=None):
+        self.event_id = event_id
+        self.time_delta = time_delta
+        self.cur_time = cur_time
+        self.src_id = src_id
+        self.sink_ids = sink_ids
+        self.metadata = metadata
+
+    def __repr__(self):
+        return ('[ Event_id: {}, time_delta: {}, cur_time: {}, src_id: {} ]'
+                .format(self.event_id, self.time_delta, self.cur_time, self.src_id))
+
+
+class State:
+    """Event log of one run (opt_model.py:35-141), filled from the engine's SoA log."""
+
+    def __init__(self, cur_time, sink_ids):
+        self.num_sinks = len(sink_ids)
+        self.time = cur_time
+        self.sink_ids = list(sink_ids)
+        self._start = cur_time
+        self._t = np.zeros(0)
+        self._src = np.zeros(0, dtype=np.int64)
+        self._edges = []
+        self._events = None
+
+    def _set_log(self, t, src, edge_list):
+        self._t = np.asarray(t, dtype=np.float64)
+        self._src = np.asarray(src, dtype=np.int64)
+        self._edges = list(edge_list)
+        self._events = None
+        if self._t.size:
+            self.time = float(self._t[-1])
+
+    def _time_delta(self):
+        prev = np.concatenate([[self._start], self._t[:-1]]) if self._t.size else self._t
+        return self._t - prev
+
+    @property
+    def events(self):
+        if self._events is None:
+            sinks = {}
+            for s, d in self._edges:
+                sinks.setdefault(s, []).append(d)
+            td = self._time_delta()
+            self._events = [Event(100 + k, float(td[k]), float(self._t[k]), int(self._src[k]),
+                                  list(sinks.get(int(self._src[k]), [])))
+                            for k in range(self._t.size)]
+        return self._events
+
+    def get_num_events(self):
+        return int(self._t.size)
+
+    def get_dataframe(self):
+        """One row per (event, sink) in event order then edge-list order, columns
+        event_id, time_delta, src_id, t, sink_id (State.get_dataframe, :85-97)."""
+        n = self._t.size
+        srcs = np.asarray([e[0] for e in self._edges], dtype=np.int64)
+        dsts = np.asarray([e[1] for e in self._edges], dtype=np.int64)
+        order = np.argsort(srcs, kind="stable")
+        srcs_sorted, dsts_sorted = srcs[order], dsts[order]
+        uniq, start = np.unique(srcs_sorted, return_index=True)
+        cnt = np.diff(np.concatenate([start, [srcs_sorted.size]]))
+        if n == 0 or uniq.size == 0:
+            return pd.DataFrame.from_records([])
+        pos = np.searchsorted(uniq, self._src)
+        hit = (pos < uniq.size) & (uniq[np.minimum(pos, uniq.size - 1)] == self._src)
+        k_cnt = np.where(hit, cnt[np.minimum(pos, uniq.size - 1)], 0)
+        k_start = np.where(hit, start[np.minimum(pos, uniq.size - 1)], 0)
+        ev = np.repeat(np.arange(n), k_cnt)
+        if ev.size == 0:
+            return pd.DataFrame.from_records([])
+        first = np.repeat(np.cumsum(k_cnt) - k_cnt, k_cnt)
+        within = np.arange(ev.size) - first
+        sink = dsts_sorted[np.repeat(k_start, k_cnt) + within]
+        td = self._time_delta()
+        return pd.DataFrame({"event_id": (100 + ev).astype(np.int64),
+                             "time_delta": td[ev],
+                             "src_id": self._src[ev],
+                             "t": self._t[ev],
+                             "sink_id": sink.astype(np.int64)})
+
+
+# ----------------------------------------------------------------- broadcasters
+class Broadcaster:
+    """Parameter holder; the arrival process runs in the engine kernels."""
+    _rq_kind = None
+
+    def __init__(self, src_id, seed):
+        self.src_id = src_id
+        self.seed = seed
+        self.used = False
+        self.is_dynamic = True
+
+    def is_fresh(self):
+        return not self.used
+
+    def get_next_interval(self, event):  # pragma: no cover - engine-side
+        raise NotImplementedError("arrival processes run in librq.so (gfx950)")
+
+    def _kwargs(self):
+        return {"src_id": self.src_id, "seed": self.seed}
+
+
+class Poisson(Broadcaster):
+    _rq_kind = L.SRC_POISSON
+
+    def __init__(self, src_id, seed, rate=1.0):
+        super().__init__(src_id, seed)
+        self.rate = rate
+
+    def _kwargs(self):
+        return dict(super()._kwargs(), rate=self.rate)
+
+
+class Poisson2(Broadcaster):
+    _rq_kind = L.SRC_POISSON2
+
+    def __init__(self, src_id, seed, rate=1.0):
+        super().__init__(src_id, seed)
+        self.rate = rate
+        self.is_dynamic = False
+
+    def _kwargs(self):
+        return dict(super()._kwargs(), rate=self.rate)
+
+
+class SmartPoisson(Broadcaster):
+    """Present for name parity (opt_model.py:436-455); not registered, no kernel."""
+
+    def __init__(self, src_id, seed, rate=1.0):
+        super().__init__(src_id, seed)
+        self.rate = rate
+
+
+class Hawkes(Broadcaster):
+    _rq_kind = L.SRC_HAWKES
+
+    def __init__(self, src_id, seed, l_0=1.0, alpha=1.0, beta=10.0):
+        super().__init__(src_id, seed)
+        self.l_0, self.alpha, self.beta = l_0, alpha, beta
+
+    def _kwargs(self):
+        return dict(super()._kwargs(), l_0=self.l_0, alpha=self.alpha, beta=self.beta)
+
+
+class PiecewiseConst(Broadcaster):
+    _rq_kind = L.SRC_PWCONST
+
+    def __init__(self, src_id, seed, change_times, rates):
+        super().__init__(src_id, seed)
+        assert is_sorted(change_times)
+        self.change_times = change_times
+        self.rates = rates
+        self.is_dynamic = False
+
+    def _kwargs(self):
+        return dict(super()._kwargs(), change_times=self.change_times, rates=self.rates)
+
+
+class RealData(Broadcaster):
+    _rq_kind = L.SRC_REALDATA
+
+    def __init__(self, src_id, times):
+        super().__init__(src_id, 0)
+        self.times = np.asarray(times)
+        self.is_dynamic = False
+
+    def get_num_events(self):
+        return len(self.times)
+
+    def _kwargs(self):
+        return {"src_id": self.src_id, "times": self.times}
+
+
+class Opt(Broadcaster):
+    """RedQueen (opt_model.py:493-544)."""
+    _rq_kind = L.SRC_OPT
+
+    def __init__(self, src_id, seed, q=1.0, s=1.0):
+        super().__init__(src_id, seed)
+        self.q = q
+        self.s = s
+
+
+class OptPWSignificance(Broadcaster):
+    """opt_model.py:547-623 -- SURVEY 8(f) 'next'; no kernel in this round."""
+
+    def __init__(self, src_id, seed, s_vec, time_period, q=1.0):
+        super().__init__(src_id, seed)
+        self.s_pw = np.asarray(s_vec)
+        self.q = q
+        self.time_period = time_period
+
+
+# ----------------------------------------------------------------------- Manager
+class Manager:
+    def __init__(self, sources, sink_ids=None, end_time=None, edge_list=None, sim_opts=None,
+                 start_time=0):
+        if sim_opts is not None:
+            edge_list = mb(edge_list, sim_opts.edge_list)
+            sink_ids = mb(sink_ids, sim_opts.sink_ids)
+            end_time = mb(end_time, sim_opts.end_time)
+        assert len(sources) > 0, "No sources."
+        assert len(sink_ids) > 0, "No sinks."
+        assert len(set(x.src_id for x in sources)) == len(sources), "Duplicates in sources."
+        assert len(set(sink_ids)) == len(sink_ids), "Duplicates in sink_ids."
+        if edge_list is None:
+            edge_list = [(src.src_id, dst) for src in sources for dst in sink_ids]
+        else:
+            known = set(src.src_id for src in sources)
+            assert set(x[0] for x in edge_list).issubset(known), "Unknown sources in edge_list."
+            assert set(x[1] for x in edge_list).issubset(set(sink_ids)), \
+                "Unknown sinks in edge_list."
+        self.end_time = end_time
+        self.edge_list = edge_list
+        self.sink_ids = sink_ids
+        self.state = State(start_time, sink_ids)
+        self.sources = sources
+        self.sim_opts = sim_opts
+        self.start_time = start_time
+
+    def get_state(self):
+        return self.state
+
+    def run(self):
+        warnings.warn('Consider using `run_dynamic` instead of `run`.')
+        return self.run_till()
+
+    def run_till(self, end_time=None):
+        if end_time is not None:
+            logging.warning('Warning: deprecation warning: end_time should not be set.')
+            self.end_time = end_time
+        return self.run_dynamic()
+
+    def _controlled(self):
+        ctrl = None
+        if self.sim_opts is not None:
+            for s in self.sources:
+                if s.src_id == self.sim_opts.src_id and isinstance(s, (Opt, Poisson2,
+                                                                       PiecewiseConst, RealData)):
+                    ctrl = s
+        if ctrl is None:
+            opts = [s for s in self.sources if isinstance(s, Opt)]
+            if len(opts) > 1:
+                raise NotImplementedError("more than one Opt broadcaster in one run")
+            ctrl = opts[0] if opts else None
+        return ctrl
+
+    def run_dynamic(self, max_events=float('inf')):
+        from .engine import Graph
+        if max_events is None:
+            max_events = float('inf')
+        for src in self.sources:
+            if not src.is_fresh():
+                raise ValueError('Source with id: {} is not fresh.'.format(src.src_id))
+        ctrl = self._controlled()
+        others = [s for s in self.sources if s is not ctrl]
+        for s in others:
+            if s._rq_kind is None or s._rq_kind == L.SRC_OPT:
+                raise NotImplementedError("broadcaster %s has no engine kernel" %
+                                          type(s).__name__)
+        if ctrl is None:
+            ids = [s.src_id for s in self.sources] + [e[0] for e in self.edge_list]
+            ctrl_id = min(ids) - 1
+        else:
+            ctrl_id = ctrl.src_id
+        other_desc = [(type(s).__name__, s._kwargs()) for s in others]
+        ctrl_a = ctrl_b = None
+        if isinstance(ctrl, PiecewiseConst):
+            ctrl_a, ctrl_b = ctrl.change_times, ctrl.rates
+        elif isinstance(ctrl, RealData):
+            ctrl_a = ctrl.times
+        g = Graph(ctrl_id, other_desc, self.sink_ids, self.edge_list, self.end_time,
+                  start_time=self.start_time, ctrl_a=ctrl_a, ctrl_b=ctrl_b)
+        maxev = None if max_events == float('inf') else int(max_events)
+        seed = 0 if ctrl is None else int(ctrl.seed) & 0xFFFFFFFF
+        if isinstance(ctrl, Opt):
+            if isinstance(ctrl.s, dict):
+                s = ctrl.s
+            else:
+                s = np.ones(g.n_followers) * np.asarray(ctrl.s, dtype=float)
+            res = g.run("opt", q=ctrl.q, s=s, ctrl_seed=seed, max_events=maxev, event_log=True)
+        elif isinstance(ctrl, Poisson2):
+            res = g.run("poisson", ctrl_seed=seed, ctrl_rate=[float(ctrl.rate)], max_events=maxev,
+                        event_log=True)
+        elif isinstance(ctrl, PiecewiseConst):
+            res = g.run("pwconst", ctrl_seed=seed, max_events=maxev, event_log=True)
+        elif isinstance(ctrl, RealData):
+            res = g.run("times", max_events=maxev, event_log=True)
+        else:
+            res = g.run("wall", max_events=maxev, event_log=True)
+        for s in self.sources:
+            s.used = True
+        t, src = res.events(0)
+        self.state._set_log(t, src, self.edge_list)
+        self.result = res
+        return self
+
+
+# ----------------------------------------------------------------------- SimOpts
+class SimOpts:
+    """Holds the options; its methods return managers (opt_model.py:755-967)."""
+
+    broadcasters = {
+        'Hawkes': Hawkes,
+        'RealData': RealData,
+        'Opt': Opt,
+        'PiecewiseConst': PiecewiseConst,
+        'Poisson': Poisson,
+        'Poisson2': Poisson2,
+        'OptPWSignificance': OptPWSignificance,
+    }
+
+    @classmethod
+    def registerSource(cls, sourceName, sourceConstructor):
+        cls.broadcasters[sourceName] = sourceConstructor
+
+    def __init__(self, **kwargs):
+        self.src_id = kwargs['src_id']
+        self.s = kwargs['s']
+        self.q = kwargs['q']
+        self.other_sources = kwargs['other_sources']
+        self.sink_ids = kwargs['sink_ids']
+        self.edge_list = kwargs['edge_list']
+        self.end_time = kwargs['end_time']
+
+    def create_other_sources(self):
+        others = []
+        for x in self.other_sources:
+            if callable(x[0]):
+                others.append(x[0](**x[1]))
+            elif x[0] in self.broadcasters:
+                others.append(self.broadcasters[x[0]](**x[1]))
+            else:
+                raise ValueError('Unknown type of broadcaster: {}'.format(x[0]))
+        return others
+
+    def randomize_other_sources(self, using_seed):
+        other_sources = []
+        for idx, (x, y) in enumerate(self.other_sources):
+            assert 'seed' in y, 'Do not know how to randomize {}.'.format(x)
+            y_new = y.copy()
+            y_new['seed'] = using_seed + 99 * idx
+            other_sources.append((x, y_new))
+        return self.update({'other_sources': other_sources})
+
+    def create_manager_with_opt(self, seed):
+        opt = Opt(src_id=self.src_id, seed=seed, s=self.s, q=self.q)
+        return Manager(sim_opts=self, sources=[opt] + self.create_other_sources())
+
+    def create_manager_with_broadcaster(self, broadcaster):
+        assert broadcaster.src_id == self.src_id, \
+            "Broadcaster has src_id = {}; expected = {}".format(broadcaster.src_id, self.src_id)
+        return Manager(sim_opts=self, sources=[broadcaster] + self.create_other_sources())
+
+    def create_manager_with_poisson(self, seed, rate=None, capacity=None):
+        if rate is None and capacity is None:
+            raise ValueError('One of rate or capacity must be specified.')
+        elif rate is None:
+            rate = capacity / self.end_time
+        elif capacity is None:
+            pass
+        else:
+            raise ValueError('Only one of rate or capacity must be specified.')
+        poisson = Poisson2(src_id=self.src_id, seed=seed, rate=rate)
+        return Manager(sim_opts=self, sources=[poisson] + self.create_other_sources())
+
+    def create_manager_with_piecewise_const(self, seed, change_times, rates):
+        assert len(change_times) == len(rates)
+        piecewise = PiecewiseConst(src_id=self.src_id, seed=seed, change_times=change_times,
+                                   rates=rates)
+        return Manager(sim_opts=self, sources=[piecewise] + self.create_other_sources())
+
+    def create_manager_with_significance(self, seed, time_period, significance=None,
+                                         num_segments=None):
+        raise NotImplementedError("OptPWSignificance is SURVEY 8(f) 'next' -- not in this round")
+
+    def create_manager_for_wall(self):
+        edge_list = [x for x in self.edge_list if x[0] != self.src_id]
+        return Manager(sim_opts=self.update({'edge_list': edge_list}),
+                       sources=self.create_other_sources())
+
+    def create_manager_with_times(self, event_times):
+        deterministic = RealData(self.src_id, event_times)
+        return Manager(sim_opts=self, sources=[deterministic] + self.create_other_sources())
+
+    def get_dict(self):
+        return {'src_id': self.src_id, 'q': self.q, 's': self.s,
+                'other_sources': self.other_sources, 'sink_ids': self.sink_ids,
+                'edge_list': self.edge_list, 'end_time': self.end_time}
+
+    def copy(self):
+        return self.update({})
+
+    def update(self, changes):
+        new_opts = self.get_dict()
+        new_opts.update(changes)
+        return SimOpts(**new_opts)
+
+    @staticmethod
+    def std_poisson(world_seed, world_rate):
+        return SimOpts(src_id=1,
+                       other_sources=[('Poisson2', {'src_id': 2, 'seed': world_seed,
+                                                    'rate': world_rate})],
+                       end_time=1.0, sink_ids=[1001], s=np.asarray([1.0]), q=1.0,
+                       edge_list=[(1, 1001), (2, 1001)])
+
+    @staticmethod
+    def std_hawkes(world_seed, world_lambda_0, world_alpha, world_beta):
+        assert world_alpha / world_beta <= 1.0, "The Hawkes wall will explode."
+        return SimOpts(src_id=1,
+                       other_sources=[('Hawkes', {'src_id': 2, 'seed': world_seed,
+                                                  'l_0': world_lambda_0, 'alpha': world_alpha,
+                                                  'beta': world_beta})],
+                       end_time=1.0, sink_ids=[1001], s=np.asarray([1.0]), q=1.0,
+                       edge_list=[(1, 1001), (2, 1001)])
+
+    @staticmethod
+    def std_piecewise_const(world_seed, world_change_times, world_rates):
+        return SimOpts(src_id=1,
+                       other_sources=[('PiecewiseConst', {'src_id': 2, 'seed': world_seed,
+                                                          'change_times': world_change_times,
+                                                          'rates': world_rates})],
+                       end_time=1.0, sink_ids=[1001], s=np.asarray([1.0]), q=1.0,
+                       edge_list=[(1, 1001), (2, 1001)])

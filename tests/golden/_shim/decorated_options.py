@@ -36,6 +36,8 @@ def optioned(option_arg="opts"):
         @functools.wraps(fn)
         def wrapper(*args, **kwargs):
             opts = kwargs.get(option_arg)
+            if option_arg not in sig.parameters:
+                kwargs.pop(option_arg, None)
             if opts is not None:
                 bound = sig.bind_partial(*args, **kwargs)
                 for name in sig.parameters:
@@ -43,8 +45,6 @@ def optioned(option_arg="opts"):
                         continue
                     if hasattr(opts, name):
                         kwargs[name] = getattr(opts, name)
-            if option_arg not in sig.parameters:
-                kwargs.pop(option_arg, None)
             return fn(*args, **kwargs)
 
         return wrapper

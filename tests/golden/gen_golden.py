@@ -17,6 +17,9 @@ installed and there is no network) and records, as plain data:
   kat_runs.npz     notebook KATs K1-K6
   adversarial.npz  hand-made tie-heavy / duplicate (t, sink) / many-sink dfs
                    with the reference's time_in_top_k / average_rank / int_r_2
+  frac.npz         dfs whose pivot has fractional (k/3) cells on 8-130 columns
+  graphs.npz       opt_runs.make_edge_list networks (C3 parameters) and a
+                   prepare_multiple_followers_sim_opts network
   dist_c2.npz      (--dist N) N-replica C2 ensemble: RedQueen vs Poisson stats
   dist_world.npz   (--dist N) wall-only ensembles for Hawkes / PiecewiseConst /
                    Poisson sources (event counts and metrics)
@@ -52,6 +55,7 @@ KAT_BASE = dict(src_id=1, end_time=100.0, q=1.0, sink_ids=[5001, 5002],
                 edge_list=[(1000, 5001), (1001, 5002), (1, 5001), (1, 5002)])
 
 KS = [1, 2, 5, 10]
+POISSON_SEED_OFFSET = 10 ** 6
 
 
 def metrics(df, so):
@@ -235,6 +239,60 @@ def gen_adversarial():
     np.savez_compressed(os.path.join(HERE, "adversarial.npz"), cases=np.asarray(cases), **rec)
 
 
+def gen_graphs():
+    """opt_runs.make_edge_list for the C3/C5 networks (the host-side generator is
+    pinned against it) and prepare_multiple_followers_sim_opts' Opt edge order."""
+    import redqueen.opt_runs as R
+    rec = {}
+    for name, (nf, nb, deg, seed) in {"c3": (1000, 50, 5, 1024), "small": (20, 7, 3, 5)}.items():
+        e = R.make_edge_list(num_followers=nf, num_broadcasters=nb, degree=deg, seed=seed,
+                             follower_id_offset=1000, broadcaster_id_offset=5000,
+                             opts=R.mk_edge_list_opts)
+        rec[name] = np.asarray(e, dtype=np.int64)
+    so = R.prepare_multiple_followers_sim_opts(num_followers=50, opts=R.multiple_follower_opts.set_new(
+        kind="Hawkes", num_other_broadcasters=20, max_num_followers=80))
+    rec["mf_edges"] = np.asarray(so.edge_list, dtype=np.int64)
+    rec["mf_sinks"] = np.asarray(so.sink_ids, dtype=np.int64)
+    rec["mf_q"] = np.asarray([so.q])
+    rec["mf_src"] = np.asarray([x[1]["src_id"] for x in so.other_sources], dtype=np.int64)
+    np.savez_compressed(os.path.join(HERE, "graphs.npz"), **rec)
+
+
+def gen_frac():
+    """dfs whose pivot has fractional cells (3 rows of one sink at one t with an own
+    row among them) on >= 8 sink columns: pins the pairwise row sum of df.mean(1)."""
+    rs = np.random.RandomState(4242)
+    rec, cases = {}, []
+    for ci in range(6):
+        S = [8, 12, 20, 33, 64, 130][ci]
+        sinks = list(range(200, 200 + S))
+        rows, t, eid = [], 0.0, 100
+        for e in range(120):
+            t += float(rs.exponential(0.3))
+            for rep in range(rs.randint(1, 4)):        # 1-3 events at the same t
+                src = 1 if rs.rand() < 0.3 else int(rs.randint(2, 6))
+                ss = list(rs.choice(sinks, rs.randint(1, min(S, 9) + 1), replace=False))
+                if rs.rand() < 0.5:
+                    ss += [ss[0], ss[-1]]
+                for y in ss:
+                    rows.append((eid, 0.0, src, t, int(y)))
+                eid += 1
+        df = pd.DataFrame.from_records(rows, columns=["event_id", "time_delta", "src_id", "t",
+                                                      "sink_id"])
+        end = float(df.t.max()) + 0.5
+        top = [U.time_in_top_k(df=df, K=k, src_id=1, end_time=end) for k in KS]
+        avg = U.average_rank(df, src_id=1, end_time=end)
+        r_t = U.rank_of_src_in_df(df, 1).mean(1)
+        r2 = np.sum(r_t ** 2 * np.diff(np.concatenate([r_t.index.values, [end]])))
+        key = "f%d" % ci
+        for col in ["event_id", "src_id", "t", "sink_id"]:
+            rec[key + "_" + col] = df[col].values
+        rec[key + "_end"] = np.asarray([end])
+        rec[key + "_met"] = np.asarray(top + [avg, r2])
+        cases.append(key)
+    np.savez_compressed(os.path.join(HERE, "frac.npz"), cases=np.asarray(cases), **rec)
+
+
 # ---------------------------------------------------------------- ensembles
 def _c2_worker(r):
     so = SimOpts(**README)
@@ -244,7 +302,10 @@ def _c2_worker(r):
     df = m.state.get_dataframe()
     met, own, world = metrics(df, so)
     n_ev = m.state.get_num_events()
-    m2 = w.create_manager_with_poisson(seed=r, capacity=float(own))
+    # comparator seed r + 10**6: with seed r the controlled Poisson2 would share
+    # RandomState(r) with world source 0 (randomize_other_sources gives idx 0 seed r) and
+    # draw the same uniforms -- its posts would coincide with that source's posts
+    m2 = w.create_manager_with_poisson(seed=r + POISSON_SEED_OFFSET, capacity=float(own))
     m2.run_dynamic()
     df2 = m2.state.get_dataframe()
     met2, own2, world2 = metrics(df2, so)
@@ -282,13 +343,16 @@ WORLDS = {
 }
 
 
-def gen_dist(n):
+def gen_dist(n, worlds=True):
     with mp.Pool(os.cpu_count()) as pool:
         res = np.asarray(pool.map(_c2_worker, range(n), chunksize=16))
     cols = (["opt_posts", "opt_world", "opt_events"] + ["opt_top%d" % k for k in KS] +
             ["opt_avg", "opt_r2", "poi_posts", "poi_world", "poi_events"] +
             ["poi_top%d" % k for k in KS] + ["poi_avg", "poi_r2"])
-    np.savez_compressed(os.path.join(HERE, "dist_c2.npz"), data=res, cols=np.asarray(cols))
+    np.savez_compressed(os.path.join(HERE, "dist_c2.npz"), data=res, cols=np.asarray(cols),
+                        poisson_seed_offset=np.asarray([POISSON_SEED_OFFSET]))
+    if not worlds:
+        return
     rec = {}
     for name in WORLDS:
         with mp.Pool(os.cpu_count()) as pool:
@@ -301,15 +365,16 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--dist", type=int, default=0)
     ap.add_argument("--only", default="")
+    ap.add_argument("--no-worlds", action="store_true")
     a = ap.parse_args()
     steps = {"npsum": gen_npsum, "draws": gen_draws, "readme": gen_readme, "kats": gen_kats,
-             "adv": gen_adversarial}
+             "adv": gen_adversarial, "graphs": gen_graphs, "frac": gen_frac}
     for k, f in steps.items():
         if not a.only or k in a.only.split(","):
             f()
             print("done", k, flush=True)
     if a.dist:
-        gen_dist(a.dist)
+        gen_dist(a.dist, worlds=not a.no_worlds)
         print("done dist", flush=True)
     with open(os.path.join(HERE, "README.md"), "w") as fh:
         fh.write(__doc__)

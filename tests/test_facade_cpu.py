@@ -1,0 +1,97 @@
+"""Host-side logic of the drop-in surface (no GPU): SimOpts / Manager API parity
+with the reference (opt_model.py:755-1013), the df row layout, the graph
+generators against the reference's networks."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from redqueen_amd import graphs
+from redqueen_amd.opt_model import (Hawkes, Manager, Opt, PiecewiseConst, Poisson, Poisson2,
+                                    RealData, SimOpts, State)
+
+
+def test_simopts_roundtrip_and_registry():
+    """The reference's own self-test, test_simOpts (opt_model.py:970-1013)."""
+    init_opts = {'src_id': 1, 'end_time': 100.0, 's': np.array([1, 2]), 'q': 1.0,
+                 'other_sources': [(Poisson, {'src_id': 2, 'seed': 1}),
+                                   (Poisson, {'src_id': 3, 'seed': 1})],
+                 'sink_ids': [1001, 1000],
+                 'edge_list': [(1, 1001), (1, 1000), (2, 1000), (3, 1001)]}
+    s = SimOpts(**init_opts)
+    assert s.get_dict() == init_opts
+    assert s.update({'src_id': 2}).src_id == 2
+    assert s.create_other_sources()[0].src_id == 2
+    init2 = dict(init_opts, other_sources=[
+        ('Poisson', {'src_id': 2, 'seed': 1, 'rate': 1000.0}),
+        ('Poisson2', {'src_id': 3, 'seed': 1, 'rate': 1000.0}),
+        ('Hawkes', {'src_id': 4, 'seed': 1, 'l_0': 1.0, 'alpha': 1.0, 'beta': 10.0}),
+        ('PiecewiseConst', {'src_id': 5, 'seed': 1, 'rates': [0.0, 0.5, 1.0],
+                            'change_times': [0, 50, 75]}),
+        ('Opt', {'src_id': 6, 'seed': 1, 's': np.array([1.0]), 'q': 1.0}),
+        ('RealData', {'src_id': 7, 'times': [0, 50, 75]})])
+    s = SimOpts(**init2)
+    kinds = [type(x) for x in s.create_other_sources()]
+    assert kinds == [Poisson, Poisson2, Hawkes, PiecewiseConst, Opt, RealData]
+    with pytest.raises(KeyError):
+        SimOpts(src_id=1)
+    with pytest.raises(ValueError):
+        SimOpts(**dict(init_opts, other_sources=[('Nope', {})])).create_other_sources()
+
+
+def test_factories_and_validation():
+    so = SimOpts(**graphs.readme())
+    with pytest.raises(ValueError):
+        so.create_manager_with_poisson(seed=1)
+    with pytest.raises(ValueError):
+        so.create_manager_with_poisson(seed=1, rate=1.0, capacity=3)
+    m = so.create_manager_with_poisson(seed=1, capacity=250)
+    assert isinstance(m.sources[0], Poisson2) and m.sources[0].rate == 2.5
+    w = so.create_manager_for_wall()
+    assert all(e[0] != so.src_id for e in w.edge_list) and w.sink_ids == so.sink_ids
+    r = so.randomize_other_sources(7)
+    assert [kw["seed"] for _, kw in r.other_sources] == [7, 106]
+    with pytest.raises(AssertionError):
+        Manager([Opt(1, 0), Opt(1, 1)], sink_ids=[1], end_time=1.0, edge_list=[])
+    with pytest.raises(AssertionError):
+        Manager([Opt(1, 0)], sink_ids=[1, 1], end_time=1.0, edge_list=[])
+    with pytest.raises(AssertionError):
+        Manager([Opt(1, 0)], sink_ids=[1], end_time=1.0, edge_list=[(2, 1)])
+    with pytest.raises(AssertionError):
+        Manager([Opt(1, 0)], sink_ids=[1], end_time=1.0, edge_list=[(1, 5)])
+    with pytest.raises(AssertionError):
+        PiecewiseConst(2, 0, change_times=[0, 5, 3], rates=[1, 2, 3])
+    m = Manager([Opt(1, 0), Poisson(2, 0)], sink_ids=[1, 2], end_time=1.0)
+    assert m.edge_list == [(1, 1), (1, 2), (2, 1), (2, 2)]
+    with pytest.raises(NotImplementedError):
+        so.create_manager_with_significance(1, 10.0)
+
+
+def test_dataframe_layout_matches_reference_expansion():
+    so = graphs.readme()
+    sc = O.Scenario(so, ("opt", 101))
+    t, dt, s = O.engine_run(sc)
+    st = State(0.0, so["sink_ids"])
+    st._set_log(t, s, so["edge_list"])
+    df = st.get_dataframe()
+    ref = sc.expand(t, dt, s)
+    assert list(df.columns) == ["event_id", "time_delta", "src_id", "t", "sink_id"]
+    for c in df.columns:
+        assert np.array_equal(df[c].values, ref[c]), c
+    assert str(df.event_id.dtype) == "int64" and str(df.sink_id.dtype) == "int64"
+    assert st.get_num_events() == len(t)
+    ev = st.events[3]
+    assert ev.event_id == 103 and ev.src_id == s[3] and ev.cur_time == t[3]
+
+
+def test_graph_generators_reproduce_reference_networks(golden):
+    g = golden("graphs.npz")
+    assert np.array_equal(np.asarray(graphs.make_edge_list(1000, 50, 5, 1024, 1000, 5000)), g["c3"])
+    assert np.array_equal(np.asarray(graphs.make_edge_list(20, 7, 3, 5, 1000, 5000)), g["small"])
+    so = graphs.followers_graph(num_followers=50, num_sources=20, degree=1, kinds=("Hawkes",),
+                                world_rate=100.0, max_num_followers=80)
+    assert np.array_equal(np.asarray(so["edge_list"]), g["mf_edges"])
+    assert np.array_equal(np.asarray(so["sink_ids"]), g["mf_sinks"])
+    assert so["q"] == g["mf_q"][0]
+    c3 = graphs.c3()
+    assert len(c3["sink_ids"]) == 1000 and len(c3["other_sources"]) == 50
+    assert len(c3["edge_list"]) == 6000
