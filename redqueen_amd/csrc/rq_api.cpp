@@ -120,6 +120,10 @@ struct Plan {
     // sorted path (merge + rq_sweep_sorted) when a replica's arrivals fit one LDS sort
     bool sorted = false;
     int n2max = 0, col16 = 0, swpb = 4;
+    // general sweep LDS layout
+    int gwpb = 4, gwin = 16, gcol_lds = 1, gcol16 = 0;
+    size_t g_col = 0, g_ptr = 0, g_odf = 0, g_cbf = 0, g_wave = 0, g_wave_stride = 0, g_rank_off = 0,
+           g_win_off = 0, g_total = 0;
     size_t lds_col = 0, lds_ptr = 0, lds_odf = 0, lds_cbf = 0, lds_wave = 0, lds_wave_stride = 0,
            lds_rank_off = 0, lds_total = 0;
     size_t tables_bytes = 0;
@@ -224,7 +228,7 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     p->n_sinks_pad = (g->n_sinks + 1) | 1;   // odd stride: spreads replicas over LDS banks
     const size_t per_wave = (size_t)p->n_sinks_pad * 4;
     p->wpb = per_wave * 4 <= 64 * 1024 ? 4 : per_wave * 2 <= 80 * 1024 ? 2 : 1;
-    if (per_wave > 160 * 1024) return RQ_EUNSUPPORTED;
+    if (per_wave > 150 * 1024) return RQ_EUNSUPPORTED;
 
     // sorted path: expected arrivals + 8 sd must fit a 16K-key bitonic sort in LDS
     {
@@ -252,6 +256,41 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
         // measured on MI355X (C3, 10k replicas): general sweep 23.6 ms vs merge 17.1 + sorted
         // sweep 17.6 ms, so auto (0) takes the general path; 2 forces the sorted one
         p->sorted = n2 <= 16384 && g->n_str <= 65535 && p->swpb > 0 && b->sweep_mode == 2;
+    }
+
+    // general sweep: pick (ring depth W, waves per block) for the most waves per CU
+    {
+        int best = -1;
+        for (int col_lds = 1; col_lds >= 0 && best < 0; --col_lds) {
+            const int c16 = col_lds && g->n_sinks <= 65535;
+            const size_t colb = col_lds ? (c16 ? 2 : 4) * g->csr_col.size() : 0;
+            size_t sh = 0;
+            const size_t o_col = sh;  sh = align_up(sh + colb, 16);
+            const size_t o_ptr = sh;  sh = align_up(sh + 4 * (g->n_str + 1), 16);
+            const size_t o_odf = sh;  sh = align_up(sh + 4 * g->n_str, 16);
+            const size_t o_cbf = sh;  sh = align_up(sh + 4 * g->n_str, 16);
+            const int spl = p->spl;
+            for (int W : {16, 8}) {
+                const size_t r_off = align_up(8 * (size_t)g->n_str, 16);
+                const size_t w_off = align_up(r_off + 4 * (size_t)p->n_sinks_pad, 16);
+                const size_t stride = align_up(w_off + 8 * (size_t)64 * spl * W, 16);
+                for (int wpb : {8, 4, 2, 1}) {
+                    const size_t tot = sh + wpb * stride;
+                    if (tot > kLdsMax) continue;
+                    const int blocks = (int)std::min<size_t>(kLdsMax / tot, 16);
+                    const int waves = std::min(blocks * wpb, 16);   // VGPR-limited beyond
+                    const int score = waves * 4 + (W == 16 ? 1 : 0);
+                    if (score > best) {
+                        best = score;
+                        p->gwin = W; p->gwpb = wpb; p->gcol_lds = col_lds; p->gcol16 = c16;
+                        p->g_col = o_col; p->g_ptr = o_ptr; p->g_odf = o_odf; p->g_cbf = o_cbf;
+                        p->g_wave = sh; p->g_wave_stride = stride; p->g_rank_off = r_off;
+                        p->g_win_off = w_off; p->g_total = tot;
+                    }
+                }
+            }
+        }
+        if (best < 0 && !p->sorted) return RQ_EUNSUPPORTED;
     }
 
     const size_t A = 256;
@@ -670,8 +709,21 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             TimedLaunch tl(K_SWEEP, s);
             if (rq_launch_sweep_sorted(sa, p.nK, p.col16, s) != hipSuccess) return RQ_EHIP;
         } else {
+            sa.n_csr = (int)g->csr_col.size();
+            sa.wpb = p.gwpb;
+            sa.win = p.gwin;
+            sa.col_in_lds = p.gcol_lds;
+            sa.lds_col = p.g_col;
+            sa.lds_ptr = p.g_ptr;
+            sa.lds_odf = p.g_odf;
+            sa.lds_cbf = p.g_cbf;
+            sa.lds_wave = p.g_wave;
+            sa.lds_wave_stride = p.g_wave_stride;
+            sa.lds_rank_off = p.g_rank_off;
+            sa.lds_win_off = p.g_win_off;
+            sa.lds_total = p.g_total;
             TimedLaunch tl(K_SWEEP, s);
-            if (rq_launch_sweep(sa, p.spl, p.nK, s) != hipSuccess) return RQ_EHIP;
+            if (rq_launch_sweep(sa, p.spl, p.nK, p.gcol16, s) != hipSuccess) return RQ_EHIP;
         }
 
         ScanArgs sc{};

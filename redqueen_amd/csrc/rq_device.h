@@ -94,6 +94,33 @@ __device__ __forceinline__ int bcast_i(int v, int src_lane)
 
 __device__ __forceinline__ int popc(uint64_t m) { return __popcll(m); }
 
+// ---- DPP wave reductions (result in lane 63, returned through v_readlane) ----
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)v, CTRL, ROWMASK, 0xF, false);
+}
+__device__ __forceinline__ uint32_t umin32(uint32_t a, uint32_t b) { return a < b ? a : b; }
+
+// min over the 64 lanes: quad swaps, half-row / row mirrors, then row broadcasts 15, 31
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
+{
+    v = umin32(v, dpp_u32<0xB1, 0xF>(v));    // quad_perm [1,0,3,2]
+    v = umin32(v, dpp_u32<0x4E, 0xF>(v));    // quad_perm [2,3,0,1]
+    v = umin32(v, dpp_u32<0x141, 0xF>(v));   // row_half_mirror
+    v = umin32(v, dpp_u32<0x140, 0xF>(v));   // row_mirror
+    v = umin32(v, dpp_u32<0x142, 0xA>(v));   // row_bcast:15 -> rows 1, 3
+    v = umin32(v, dpp_u32<0x143, 0xC>(v));   // row_bcast:31 -> rows 2, 3
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+// order-preserving map of a double onto uint64 (negative values reversed)
+__device__ __forceinline__ uint64_t order_key(double t)
+{
+    const uint64_t b = rq_dbl_bits(t);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
 // ---------------------------------------------------------------------------
 // numpy-order float64 sum of NV sequences of length n, by ONE wavefront.
 // VAL(k, v) fills v[0..NV) with element k of each sequence.

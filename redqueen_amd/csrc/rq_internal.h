@@ -78,7 +78,9 @@ struct SweepArgs {
     const uint16_t* msrc;
     const int* mcount;
     int n_csr;
-    size_t lds_col, lds_ptr, lds_odf, lds_cbf, lds_wave, lds_wave_stride, lds_rank_off, lds_total;
+    int col_in_lds, win;     // general sweep: CSR copied to LDS; arrival-ring depth
+    size_t lds_col, lds_ptr, lds_odf, lds_cbf, lds_wave, lds_wave_stride, lds_rank_off, lds_win_off,
+        lds_total;
 };
 
 struct ScanArgs {
@@ -96,7 +98,7 @@ struct ScanArgs {
 };
 
 hipError_t rq_launch_gen(const GenArgs& a, hipStream_t s);
-hipError_t rq_launch_sweep(const SweepArgs& a, int spl, int nK, hipStream_t s);
+hipError_t rq_launch_sweep(const SweepArgs& a, int spl, int nK, int col16, hipStream_t s);
 hipError_t rq_launch_scan(const ScanArgs& a, int nK, hipStream_t s);
 hipError_t rq_launch_merge(const MergeArgs& a, hipStream_t s);
 hipError_t rq_launch_sweep_sorted(const SweepArgs& a, int nK, int col16, hipStream_t s);

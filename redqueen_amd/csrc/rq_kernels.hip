@@ -150,52 +150,102 @@ __global__ __launch_bounds__(256) void rq_gen_streams(GenArgs a)
 }
 
 // ============================================================================
-// 2a. general sweep: one wavefront per replica, lanes own arrival heads and
-//     pick the next event with a wave-wide min (any number of sources <= 512)
+// 2a. general sweep: one wavefront per replica.  Lanes own sources; the next
+//     event is a DPP wave-min over order-preserving 64-bit time keys (high
+//     word, then low word only on a tie).  Every source keeps a ring of its
+//     next W arrival times in LDS, refilled for all sources at once when one
+//     runs dry (one exposed load latency per refill round, not per event).
+//     Sink lists / follower list / per-source constants are read from LDS.
 // ============================================================================
-template <int SPL, int NK>
-__global__ __launch_bounds__(256) void rq_sweep(SweepArgs a)
+template <int SPL, int NK, class COL, int W>
+__global__ __launch_bounds__(512) void rq_sweep(SweepArgs a)
 {
-    extern __shared__ int lds_rank[];
+    extern __shared__ double lds_g[];
+    char* base = reinterpret_cast<char*>(lds_g);
     const int lane = lane_id();
     const int w = threadIdx.x >> 6;
+    int* cptr = reinterpret_cast<int*>(base + a.lds_ptr);
+    int* odf = reinterpret_cast<int*>(base + a.lds_odf);
+    int* cbf = reinterpret_cast<int*>(base + a.lds_cbf);
+    const COL* col;
+    if (a.col_in_lds) {
+        COL* c = reinterpret_cast<COL*>(base + a.lds_col);
+        for (int e = threadIdx.x; e < a.n_csr; e += blockDim.x) c[e] = (COL)a.csr_col[e];
+        col = c;
+    } else {
+        col = reinterpret_cast<const COL*>(a.csr_col);   // host guarantees COL == int here
+    }
+    for (int j = threadIdx.x; j <= a.n_str; j += blockDim.x) cptr[j] = a.csr_ptr[j];
+    for (int j = threadIdx.x; j < a.n_str; j += blockDim.x) {
+        odf[j] = a.outdeg_f[j];
+        cbf[j] = a.ctrl_src_id < a.src_id[j];
+    }
     const int64_t rl = (int64_t)blockIdx.x * a.wpb + w;
-    if (rl >= a.n_chunk) return;
-    const int64_t o = a.chunk0 + rl;
+    const bool live = rl < a.n_chunk;
+    const int64_t o = a.chunk0 + (live ? rl : 0);
     const int64_t i = a.rep0 + o;
     const int g = (int)(i / a.n_rep);
-
-    int* rank = lds_rank + (size_t)w * a.n_sinks_pad;
+    char* wb = base + a.lds_wave + (size_t)w * a.lds_wave_stride;
+    double* invc = reinterpret_cast<double*>(wb);
+    int* rank = reinterpret_cast<int*>(wb + a.lds_rank_off);
+    double* win = reinterpret_cast<double*>(wb + a.lds_win_off);
+    for (int j = lane; j < a.n_str; j += 64) invc[j] = a.inv_c[(int64_t)g * a.n_str + j];
     for (int c = lane; c < a.n_sinks; c += 64) rank[c] = -1;   // NaN: no row yet
+    __syncthreads();
+    if (!live) return;
 
-    // ---- arrival heads: lane owns sources [lane*SPL, lane*SPL+SPL) ----
+    // ---- arrival rings: lane owns sources [lane*SPL, lane*SPL+SPL) ----
     const double* st = a.streams + rl * a.capsum;
     const int* slen = a.slen + rl * a.n_str;
     double head[SPL];
-    int pos[SPL], len[SPL], off[SPL];
+    int pos[SPL], fil[SPL], len[SPL], off[SPL];
 #pragma unroll
     for (int q = 0; q < SPL; ++q) {
         const int j = lane * SPL + q;
         off[q] = j < a.n_str ? (int)a.st_off[j] : 0;
         len[q] = j < a.n_str ? slen[j] : 0;
         pos[q] = 0;
-        head[q] = len[q] > 0 ? st[off[q]] : RQ_INF;
+        fil[q] = 0;
     }
+    // refill every ring that is at most half full (and not exhausted)
+    auto refill = [&]() {
+#pragma unroll
+        for (int q = 0; q < SPL; ++q) {
+            const int j = lane * SPL + q;
+            const bool need = fil[q] < len[q] && fil[q] - pos[q] <= W / 2;
+            const int nf = need ? ((pos[q] + W) < len[q] ? pos[q] + W : len[q]) : fil[q];
+            // two half-ring chunks: all loads of a chunk in flight before its LDS stores
+#pragma unroll
+            for (int h = 0; h < W; h += W / 2) {
+                double v[W / 2];
+#pragma unroll
+                for (int k = 0; k < W / 2; ++k)
+                    v[k] = fil[q] + h + k < nf ? st[off[q] + fil[q] + h + k] : 0.0;
+#pragma unroll
+                for (int k = 0; k < W / 2; ++k)
+                    if (fil[q] + h + k < nf) win[j * W + ((fil[q] + h + k) & (W - 1))] = v[k];
+            }
+            fil[q] = nf;
+        }
+    };
+    refill();
     double lmin = RQ_INF;
     int larg = 0;
 #pragma unroll
-    for (int q = 0; q < SPL; ++q)
+    for (int q = 0; q < SPL; ++q) {
+        head[q] = len[q] > 0 ? win[(lane * SPL + q) * W] : RQ_INF;
         if (head[q] < lmin) {
             lmin = head[q];
             larg = q;
         }
+    }
 
     const bool opt = a.ctrl_kind == RQ_SRC_OPT;
     double opt_next = opt ? a.start : RQ_INF;
     const int64_t k = a.seed_mod > 0 ? i % a.seed_mod : i;
     OptDraws od;
     od.init(a.ctrl_seed ? a.ctrl_seed[i] : a.ctrl_seed0 + (uint32_t)k);
-    const double* invc = a.inv_c + (int64_t)g * a.n_str;
+    const COL* fol = col + cptr[a.ctrl_idx];
 
     Agg<NK> ag;
     ag.init(a.Ks);
@@ -211,15 +261,23 @@ __global__ __launch_bounds__(256) void rq_sweep(SweepArgs a)
     int status = 0;
     for (;;) {
         if (a.max_events >= 0 && n_events >= a.max_events) break;
-        const double tw = wave_min(lmin);
-        const uint64_t cand = __ballot(lmin == tw);
-        const int wl = cand ? (__ffsll((unsigned long long)cand) - 1) : 0;
-        const int wq = bcast_i(larg, wl);
+        // -------- next arrival: (time, lowest lane/source) --------
+        const uint64_t key = order_key(lmin);
+        const uint32_t khi = (uint32_t)(key >> 32), klo = (uint32_t)key;
+        const uint32_t mhi = wave_min_u32(khi);
+        uint64_t cand = __ballot(khi == mhi);
+        if (__popcll(cand) > 1) {
+            const uint32_t mlo = wave_min_u32(khi == mhi ? klo : 0xFFFFFFFFu);
+            cand = __ballot(khi == mhi && klo == mlo);
+        }
+        const int wl = __ffsll((unsigned long long)cand) - 1;
+        const double tw = bcast_d(lmin, wl);
+        const int wq = SPL == 1 ? 0 : bcast_i(larg, wl);
         const int jw = wl * SPL + wq;
         bool own;
         double tev;
         if (opt) {
-            own = opt_next < tw || (opt_next == tw && (tw == RQ_INF || a.ctrl_src_id < a.src_id[jw]));
+            own = opt_next < tw || (opt_next == tw && (tw == RQ_INF || cbf[jw]));
             tev = own ? opt_next : tw;
         } else {
             own = jw == a.ctrl_idx;
@@ -229,32 +287,39 @@ __global__ __launch_bounds__(256) void rq_sweep(SweepArgs a)
         if (evlog) es.push(tev, own ? a.ctrl_idx : jw, lane, status);
         ++n_events;
 
-        int nsinks;
         if (!own || !opt) {
-            // advance the winning head
+            // advance the winning source; refill the rings if it ran dry
+            bool dry = false;
 #pragma unroll
             for (int q = 0; q < SPL; ++q)
                 if (lane == wl && q == wq) {
                     ++pos[q];
-                    head[q] = pos[q] < len[q] ? st[off[q] + pos[q]] : RQ_INF;
+                    dry = pos[q] < len[q] && pos[q] == fil[q];
                 }
+            if (__ballot(dry)) refill();
             if (lane == wl) {
                 lmin = RQ_INF;
                 larg = 0;
 #pragma unroll
-                for (int q = 0; q < SPL; ++q)
+                for (int q = 0; q < SPL; ++q) {
+                    if (q == wq)
+                        head[q] = pos[q] < len[q] ? win[(lane * SPL + q) * W + (pos[q] & (W - 1))]
+                                                  : RQ_INF;
                     if (head[q] < lmin) {
                         lmin = head[q];
                         larg = q;
                     }
+                }
             }
         }
+        int nsinks;
         if (own) {
             nsinks = a.n_fol;
-            ag.own(rank, a.fol, a.n_fol, lane);
+            ag.own(rank, fol, a.n_fol, lane);
             if (opt) opt_next = RQ_INF;
             if (nsinks > 0) ++posts;
         } else {
+            const int e0 = cptr[jw], e1 = cptr[jw + 1];
             if (opt) {
                 // one Exp(c_j) draw per non-own event (opt_model.py:536-544)
                 const double x = od.next(lane);
@@ -263,9 +328,8 @@ __global__ __launch_bounds__(256) void rq_sweep(SweepArgs a)
                 const double c2 = tev + e;
                 if (c2 < opt_next) opt_next = c2;
             }
-            const int e0 = a.csr_ptr[jw], e1 = a.csr_ptr[jw + 1];
             nsinks = e1 - e0;
-            ag.wall(rank, a.csr_col, e0, e1, a.outdeg_f[jw], lane);
+            ag.wall(rank, col, e0, e1, odf[jw], lane);
             if (nsinks > 0) ++world;
         }
         if (nsinks > 0 && !rs.emit(tev, ag, lane, status)) break;
@@ -763,24 +827,31 @@ __global__ __launch_bounds__(64) void rq_replay(ReplayArgs a)
 // ============================================================================
 // launch wrappers
 // ============================================================================
-template <int SPL, int NK>
+template <int SPL, int NK, class COL, int W>
 static hipError_t launch_sweep_t(const SweepArgs& a, hipStream_t s)
 {
     const unsigned blocks = (unsigned)((a.n_chunk + a.wpb - 1) / a.wpb);
-    const size_t lds = (size_t)a.wpb * a.n_sinks_pad * sizeof(int);
-    hipLaunchKernelGGL((rq_sweep<SPL, NK>), dim3(blocks), dim3(64 * a.wpb), lds, s, a);
+    hipLaunchKernelGGL((rq_sweep<SPL, NK, COL, W>), dim3(blocks), dim3(64 * a.wpb), a.lds_total, s, a);
     return hipGetLastError();
 }
 
-template <int SPL>
+template <int SPL, class COL, int W>
 static hipError_t launch_sweep_k(const SweepArgs& a, int nK, hipStream_t s)
 {
     switch (nK) {
-    case 1: return launch_sweep_t<SPL, 1>(a, s);
-    case 2: return launch_sweep_t<SPL, 2>(a, s);
-    case 3: return launch_sweep_t<SPL, 3>(a, s);
-    default: return launch_sweep_t<SPL, 4>(a, s);
+    case 1: return launch_sweep_t<SPL, 1, COL, W>(a, s);
+    case 2: return launch_sweep_t<SPL, 2, COL, W>(a, s);
+    case 3: return launch_sweep_t<SPL, 3, COL, W>(a, s);
+    default: return launch_sweep_t<SPL, 4, COL, W>(a, s);
     }
+}
+
+template <int SPL>
+static hipError_t launch_sweep_c(const SweepArgs& a, int nK, int col16, hipStream_t s)
+{
+    if (a.win == 16)
+        return col16 ? launch_sweep_k<SPL, uint16_t, 16>(a, nK, s) : launch_sweep_k<SPL, int, 16>(a, nK, s);
+    return col16 ? launch_sweep_k<SPL, uint16_t, 8>(a, nK, s) : launch_sweep_k<SPL, int, 8>(a, nK, s);
 }
 
 hipError_t rq_launch_gen(const GenArgs& a, hipStream_t s)
@@ -824,14 +895,14 @@ hipError_t rq_launch_sweep_sorted(const SweepArgs& a, int nK, int col16, hipStre
     return col16 ? launch_sorted_k<uint16_t>(a, nK, s) : launch_sorted_k<int>(a, nK, s);
 }
 
-hipError_t rq_launch_sweep(const SweepArgs& a, int spl, int nK, hipStream_t s)
+hipError_t rq_launch_sweep(const SweepArgs& a, int spl, int nK, int col16, hipStream_t s)
 {
     if (a.n_chunk <= 0) return hipSuccess;
     switch (spl) {
-    case 1: return launch_sweep_k<1>(a, nK, s);
-    case 2: return launch_sweep_k<2>(a, nK, s);
-    case 4: return launch_sweep_k<4>(a, nK, s);
-    default: return launch_sweep_k<8>(a, nK, s);
+    case 1: return launch_sweep_c<1>(a, nK, col16, s);
+    case 2: return launch_sweep_c<2>(a, nK, col16, s);
+    case 4: return launch_sweep_c<4>(a, nK, col16, s);
+    default: return launch_sweep_c<8>(a, nK, col16, s);
     }
 }
 
