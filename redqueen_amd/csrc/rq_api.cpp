@@ -214,6 +214,7 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
             c = kind == RQ_SRC_REALDATA ? (int64_t)m
                                         : (int64_t)std::ceil((m + 8.0 * std::sqrt(var) + 32.0) * scale);
         if (c > (int64_t)1 << 30) return RQ_EINVAL;
+        c = (c + 7) & ~(int64_t)7;   // 64-byte chunks for the generator's stores
         p->cap[j] = (int)c;
         p->st_off[j] = p->capsum;
         p->capsum += c;
