@@ -104,7 +104,11 @@ typedef struct rq_graph* rq_graph_t;
 /* status bits written per replica into rq_outputs.status */
 #define RQ_ST_ROWS_OVERFLOW 1    /* metric-row / event-log capacity exceeded: rerun with larger cap_scale */
 #define RQ_ST_STREAM_OVERFLOW 2  /* a source's arrival stream exceeded its capacity: rerun      */
-#define RQ_ST_TIE 4              /* two events at the same time merged into one pivot row       */
+#define RQ_ST_TIE 4              /* events at equal times shared a pivot row.  Exact (pivot cells
+                                    averaged like pandas) in the sequential sweep -- event log,
+                                    max_events, sweep_mode 2, or any RealData stream; the fast
+                                    tiled sweep keeps the last row, so for a replica flagged
+                                    here avg-rank / r^2 may differ: rerun it with sweep_mode 2 */
 #define RQ_ST_EMPTY 8            /* no event reached any sink: the reference's df is empty      */
 
 #define RQ_RUN_EVENT_LOG 1       /* also write the (t, source) event log (for get_dataframe)    */
@@ -134,7 +138,9 @@ typedef struct rq_batch_desc {
     int64_t replica0;            /* this call runs global replicas [replica0, replica0+n_local):  */
     int64_t n_local;             /* a shard of the grid (0 = all n_grid*n_rep); outputs are      */
                                  /* indexed locally, seeds and grid point use the global id     */
-    int32_t sweep_mode;          /* 0 auto, 1 general wave-min sweep, 2 merge (LDS sort) + sorted  */
+    int32_t sweep_mode;          /* 0 auto: fast tiled sweep unless the run needs the sequential
+                                    one (event log, max_events, RealData); 1 fast whenever the
+                                    event log / max_events allow; 2 force the sequential sweep */
                                  /* sweep; both are bit-identical, auto picks the faster one    */
 } rq_batch_desc;
 

@@ -1,3 +1,4 @@
+#include <cstdlib>
 // rq_api.cpp -- host side of the C ABI declared in include/rq.h.
 //
 // rq_graph_build does what SimOpts + Manager.__init__ + Broadcaster.init_state
@@ -117,18 +118,15 @@ struct Plan {
     int64_t R = 0, chunk = 0, capsum = 0, cap_rows = 0;
     std::vector<int> cap;
     std::vector<int64_t> st_off;
-    // sorted path (merge + rq_sweep_sorted) when a replica's arrivals fit one LDS sort
-    bool sorted = false;
-    int n2max = 0, col16 = 0, swpb = 4;
+    // sequential (event log / max_events) sweep variant
+    bool log = false;
     // general sweep LDS layout
     int gwpb = 4, gwin = 16, gcol_lds = 1, gcol16 = 0;
     size_t g_col = 0, g_ptr = 0, g_odf = 0, g_cbf = 0, g_wave = 0, g_wave_stride = 0, g_rank_off = 0,
-           g_win_off = 0, g_total = 0;
-    size_t lds_col = 0, lds_ptr = 0, lds_odf = 0, lds_cbf = 0, lds_wave = 0, lds_wave_stride = 0,
-           lds_rank_off = 0, lds_total = 0;
+           g_win_off = 0, g_x_off = 0, g_total = 0;
     size_t tables_bytes = 0;
     size_t off_invc = 0, off_streams = 0, off_slen = 0, off_rt = 0, off_rs = 0, off_rv = 0,
-           off_rc = 0, off_sall = 0, off_stoff = 0, off_cap = 0, off_msrc = 0, off_mcount = 0,
+           off_rc = 0, off_sall = 0, off_stoff = 0, off_cap = 0,
            total = 0;
 };
 
@@ -231,40 +229,22 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     p->wpb = per_wave * 4 <= 64 * 1024 ? 4 : per_wave * 2 <= 80 * 1024 ? 2 : 1;
     if (per_wave > 150 * 1024) return RQ_EUNSUPPORTED;
 
-    // sorted path: expected arrivals + 8 sd must fit a 16K-key bitonic sort in LDS
-    {
-        const double need = std::ceil((m_total + 8.0 * std::sqrt(v_total) + 64.0) * scale);
-        int n2 = 64;
-        while (n2 < need && n2 < 32768) n2 <<= 1;
-        p->n2max = n2;
-        p->col16 = g->n_sinks <= 65535;
-        const size_t colb = p->col16 ? 2 : 4;
-        size_t o2 = 0;
-        p->lds_col = o2;  o2 = align_up(o2 + colb * g->csr_col.size(), 16);
-        p->lds_ptr = o2;  o2 = align_up(o2 + 4 * (g->n_str + 1), 16);
-        p->lds_odf = o2;  o2 = align_up(o2 + 4 * g->n_str, 16);
-        p->lds_cbf = o2;  o2 = align_up(o2 + 4 * g->n_str, 16);
-        p->lds_wave = o2;
-        p->lds_rank_off = align_up(8 * g->n_str, 16);
-        p->lds_wave_stride = align_up(p->lds_rank_off + 4 * (size_t)p->n_sinks_pad, 16);
-        p->swpb = 0;
-        for (int w = 4; w >= 1; w >>= 1)
-            if (p->lds_wave + w * p->lds_wave_stride <= 64 * 1024 || (w == 1 && p->lds_wave + p->lds_wave_stride <= kLdsMax)) {
-                p->swpb = w;
-                break;
-            }
-        p->lds_total = p->lds_wave + p->swpb * p->lds_wave_stride;
-        // measured on MI355X (C3, 10k replicas): general sweep 23.6 ms vs merge 17.1 + sorted
-        // sweep 17.6 ms, so auto (0) takes the general path; 2 forces the sorted one
-        p->sorted = n2 <= 16384 && g->n_str <= 65535 && p->swpb > 0 && b->sweep_mode == 2;
-    }
+    // the sequential exact variant also whenever equal event times are likely:
+    // RealData streams (recorded times repeat); the fast sweep flags RQ_ST_TIE
+    bool has_rd = b->ctrl_kind == RQ_SRC_REALDATA;
+    for (int k : g->kind) has_rd = has_rd || k == RQ_SRC_REALDATA;
+    p->log = (b->flags & RQ_RUN_EVENT_LOG) || b->max_events >= 0 || b->sweep_mode == 2 ||
+             (has_rd && b->sweep_mode != 1);
+    if (p->log) p->spl = 8;
 
     // general sweep: pick (ring depth W, waves per block) for the most waves per CU
     {
         int best = -1;
-        for (int col_lds = 1; col_lds >= 0 && best < 0; --col_lds) {
-            const int c16 = col_lds && g->n_sinks <= 65535;
-            const size_t colb = col_lds ? (c16 ? 2 : 4) * g->csr_col.size() : 0;
+        // sink columns live in LDS as uint16 when they fit, else they are read from
+        // global memory as int (the kernel's COL type selects the path at compile time)
+        for (int col_lds = g->n_sinks <= 65535 ? 1 : 0; col_lds >= 0 && best < 0; --col_lds) {
+            const int c16 = col_lds;
+            const size_t colb = col_lds ? 2 * g->csr_col.size() : 0;
             size_t sh = 0;
             const size_t o_col = sh;  sh = align_up(sh + colb, 16);
             const size_t o_ptr = sh;  sh = align_up(sh + 4 * (g->n_str + 1), 16);
@@ -272,9 +252,13 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
             const size_t o_cbf = sh;  sh = align_up(sh + 4 * g->n_str, 16);
             const int spl = p->spl;
             for (int W : {16, 8}) {
+                if (p->log && W != 8) continue;
                 const size_t r_off = align_up(8 * (size_t)g->n_str, 16);
                 const size_t w_off = align_up(r_off + 4 * (size_t)p->n_sinks_pad, 16);
-                const size_t stride = align_up(w_off + 8 * (size_t)64 * spl * W, 16);
+                size_t stride = align_up(w_off + 8 * (size_t)64 * spl * W, 16);
+                // LOG: per-sink gtag/gcnt/gsum + a wave_npsum<1> scratch (304 doubles)
+                const size_t x_off = stride;
+                if (p->log) stride = align_up(x_off + 12 * (size_t)p->n_sinks_pad + 8 * 304, 16);
                 for (int wpb : {8, 4, 2, 1}) {
                     const size_t tot = sh + wpb * stride;
                     if (tot > kLdsMax) continue;
@@ -286,12 +270,12 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
                         p->gwin = W; p->gwpb = wpb; p->gcol_lds = col_lds; p->gcol16 = c16;
                         p->g_col = o_col; p->g_ptr = o_ptr; p->g_odf = o_odf; p->g_cbf = o_cbf;
                         p->g_wave = sh; p->g_wave_stride = stride; p->g_rank_off = r_off;
-                        p->g_win_off = w_off; p->g_total = tot;
+                        p->g_win_off = w_off; p->g_x_off = x_off; p->g_total = tot;
                     }
                 }
             }
         }
-        if (best < 0 && !p->sorted) return RQ_EUNSUPPORTED;
+        if (best < 0) return RQ_EUNSUPPORTED;
     }
 
     const size_t A = 256;
@@ -309,8 +293,6 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     p->off_rv = o;      o = align_up(o + sizeof(uint32_t) * (size_t)C * p->cap_rows, A);
     p->off_rc = o;      o = align_up(o + sizeof(uint32_t) * (size_t)C * p->cap_rows * p->nK, A);
     p->off_sall = o;    o = align_up(o + sizeof(int) * (size_t)C, A);
-    p->off_msrc = o;    o = align_up(o + (p->sorted ? sizeof(uint16_t) * (size_t)C * p->capsum : 0), A);
-    p->off_mcount = o;  o = align_up(o + sizeof(int) * (size_t)C, A);
     p->total = o;
     return RQ_OK;
 }
@@ -678,38 +660,7 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             sa.ev_src = out->ev_src;
             sa.ev_cap = out->ev_cap;
         }
-        if (p.sorted) {
-            MergeArgs ma{};
-            ma.n_chunk = C;
-            ma.chunk0 = c0;
-            ma.n_str = g->n_str;
-            ma.n2max = p.n2max;
-            ma.st_off = ga.st_off;
-            ma.capsum = p.capsum;
-            ma.streams = ga.streams;
-            ma.slen = ga.slen;
-            ma.msrc = (uint16_t*)(ws + p.off_msrc);
-            ma.mcount = (int*)(ws + p.off_mcount);
-            ma.status = out->status;
-            {
-                TimedLaunch tl(K_MERGE, s);
-                if (rq_launch_merge(ma, s) != hipSuccess) return RQ_EHIP;
-            }
-            sa.msrc = ma.msrc;
-            sa.mcount = ma.mcount;
-            sa.n_csr = (int)g->csr_col.size();
-            sa.wpb = p.swpb;
-            sa.lds_col = p.lds_col;
-            sa.lds_ptr = p.lds_ptr;
-            sa.lds_odf = p.lds_odf;
-            sa.lds_cbf = p.lds_cbf;
-            sa.lds_wave = p.lds_wave;
-            sa.lds_wave_stride = p.lds_wave_stride;
-            sa.lds_rank_off = p.lds_rank_off;
-            sa.lds_total = p.lds_total;
-            TimedLaunch tl(K_SWEEP, s);
-            if (rq_launch_sweep_sorted(sa, p.nK, p.col16, s) != hipSuccess) return RQ_EHIP;
-        } else {
+        {
             sa.n_csr = (int)g->csr_col.size();
             sa.wpb = p.gwpb;
             sa.win = p.gwin;
@@ -722,9 +673,10 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             sa.lds_wave_stride = p.g_wave_stride;
             sa.lds_rank_off = p.g_rank_off;
             sa.lds_win_off = p.g_win_off;
+            sa.lds_x_off = p.g_x_off;
             sa.lds_total = p.g_total;
             TimedLaunch tl(K_SWEEP, s);
-            if (rq_launch_sweep(sa, p.spl, p.nK, p.gcol16, s) != hipSuccess) return RQ_EHIP;
+            if (rq_launch_sweep(sa, p.spl, p.nK, p.gcol16, p.log, s) != hipSuccess) return RQ_EHIP;
         }
 
         ScanArgs sc{};

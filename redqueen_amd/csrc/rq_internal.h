@@ -31,18 +31,6 @@ struct GenArgs {
 
 #define RQ_MAX_STREAMS 512
 
-struct MergeArgs {
-    int64_t n_chunk, chunk0;         // local indices
-    int n_str, n2max;
-    const int64_t* st_off;
-    int64_t capsum;
-    double* streams;      // in: per-source streams; out: merged times (in place)
-    const int* slen;
-    uint16_t* msrc;       // out: merged source index
-    int* mcount;          // out: merged length (-1: did not fit)
-    int32_t* status;
-};
-
 struct SweepArgs {
     int64_t n_chunk, chunk0, n_rep, rep0;
     int wpb, n_str, n_sinks, n_sinks_pad, ctrl_idx, ctrl_kind, n_fol;
@@ -74,12 +62,9 @@ struct SweepArgs {
     double* ev_t;
     int32_t* ev_src;
     int64_t ev_cap;
-    // sorted-path extras
-    const uint16_t* msrc;
-    const int* mcount;
     int n_csr;
     int col_in_lds, win;     // general sweep: CSR copied to LDS; arrival-ring depth
-    size_t lds_col, lds_ptr, lds_odf, lds_cbf, lds_wave, lds_wave_stride, lds_rank_off, lds_win_off,
+    size_t lds_col, lds_ptr, lds_odf, lds_cbf, lds_wave, lds_wave_stride, lds_rank_off, lds_win_off, lds_x_off,
         lds_total;
 };
 
@@ -98,10 +83,8 @@ struct ScanArgs {
 };
 
 hipError_t rq_launch_gen(const GenArgs& a, hipStream_t s);
-hipError_t rq_launch_sweep(const SweepArgs& a, int spl, int nK, int col16, hipStream_t s);
+hipError_t rq_launch_sweep(const SweepArgs& a, int spl, int nK, int col16, int log, hipStream_t s);
 hipError_t rq_launch_scan(const ScanArgs& a, int nK, hipStream_t s);
-hipError_t rq_launch_merge(const MergeArgs& a, hipStream_t s);
-hipError_t rq_launch_sweep_sorted(const SweepArgs& a, int nK, int col16, hipStream_t s);
 
 struct ReplayArgs {
     const double* t;

@@ -171,14 +171,19 @@ __global__ __launch_bounds__(256) void rq_gen_streams(GenArgs a)
 }
 
 // ============================================================================
-// 2a. general sweep: one wavefront per replica.  Lanes own sources; the next
-//     event is a DPP wave-min over order-preserving 64-bit time keys (high
-//     word, then low word only on a tie).  Every source keeps a ring of its
-//     next W arrival times in LDS, refilled for all sources at once when one
-//     runs dry (one exposed load latency per refill round, not per event).
-//     Sink lists / follower list / per-source constants are read from LDS.
+// 2. sweep: one wavefront per replica, 64-arrival tiles in three phases.
+//    A  merge: lanes own sources; each step is a DPP wave-min over order-
+//       preserving time keys (high word, low word only on a tie).  Every
+//       source keeps a ring of its next W arrivals in LDS, refilled for all
+//       sources at once when one runs dry.  Arrival #k of the tile -> lane k.
+//    B  controller: the world is exogenous, so the RedQueen candidates of the
+//       whole tile are drawn in parallel and the posts found by prefix-mins.
+//    C  apply: the only sequential part -- the per-sink rank updates in LDS;
+//       each event's aggregates are parked in its lane and the pivot rows
+//       (equal-time rows merged) are placed and stored by all lanes at once.
+//    LOG = the event log / max_events variant: phase C goes event by event.
 // ============================================================================
-template <int SPL, int NK, class COL, int W>
+template <int SPL, int NK, class COL, int W, bool LOG>
 __global__ __launch_bounds__(512) void rq_sweep(SweepArgs a)
 {
     extern __shared__ double lds_g[];
@@ -188,14 +193,13 @@ __global__ __launch_bounds__(512) void rq_sweep(SweepArgs a)
     int* cptr = reinterpret_cast<int*>(base + a.lds_ptr);
     int* odf = reinterpret_cast<int*>(base + a.lds_odf);
     int* cbf = reinterpret_cast<int*>(base + a.lds_cbf);
-    const COL* col;
-    if (a.col_in_lds) {
-        COL* c = reinterpret_cast<COL*>(base + a.lds_col);
-        for (int e = threadIdx.x; e < a.n_csr; e += blockDim.x) c[e] = (COL)a.csr_col[e];
-        col = c;
-    } else {
-        col = reinterpret_cast<const COL*>(a.csr_col);   // host guarantees COL == int here
-    }
+    // sink columns: COL = uint16_t -> LDS copy, COL = int -> global (compile-time,
+    // so LDS reads never wait on outstanding global traffic)
+    constexpr bool col_lds = sizeof(COL) == 2;
+    COL* col_l = reinterpret_cast<COL*>(base + a.lds_col);
+    const int* col_g = a.csr_col;
+    if (col_lds)
+        for (int e = threadIdx.x; e < a.n_csr; e += blockDim.x) col_l[e] = (COL)a.csr_col[e];
     for (int j = threadIdx.x; j <= a.n_str; j += blockDim.x) cptr[j] = a.csr_ptr[j];
     for (int j = threadIdx.x; j < a.n_str; j += blockDim.x) {
         odf[j] = a.outdeg_f[j];
@@ -264,9 +268,11 @@ __global__ __launch_bounds__(512) void rq_sweep(SweepArgs a)
     const bool opt = a.ctrl_kind == RQ_SRC_OPT;
     double opt_next = opt ? a.start : RQ_INF;
     const int64_t k = a.seed_mod > 0 ? i % a.seed_mod : i;
-    OptDraws od;
-    od.init(a.ctrl_seed ? a.ctrl_seed[i] : a.ctrl_seed0 + (uint32_t)k);
-    const COL* fol = col + cptr[a.ctrl_idx];
+    const uint32_t oseed = a.ctrl_seed ? a.ctrl_seed[i] : a.ctrl_seed0 + (uint32_t)k;
+    uint64_t ndraw = 0;   // wall events seen so far = the controller's draw index
+    auto colat = [&](int e) -> int { return col_lds ? (int)col_l[e] : col_g[e]; };
+    const int fol0 = cptr[a.ctrl_idx];
+    auto folat = [&](int f) -> int { return colat(fol0 + f); };
 
     Agg<NK> ag;
     ag.init(a.Ks);
@@ -274,41 +280,74 @@ __global__ __launch_bounds__(512) void rq_sweep(SweepArgs a)
     const int64_t rbase = rl * a.cap_rows;
     rs.init(a.rows_t + rbase, a.rows_sum + rbase, a.rows_valid + rbase, a.rows_cnt + rbase * NK,
             a.cap_rows);
-    const bool evlog = a.ev_t != nullptr;
     EvStage es;
-    if (evlog) es.init(a.ev_t + o * a.ev_cap, a.ev_src + o * a.ev_cap, a.ev_cap);
+    if (LOG && a.ev_t) es.init(a.ev_t + o * a.ev_cap, a.ev_src + o * a.ev_cap, a.ev_cap);
 
     int64_t n_events = 0, posts = 0, world = 0;
     int status = 0;
-    for (;;) {
-        if (a.max_events >= 0 && n_events >= a.max_events) break;
-        // -------- next arrival: (time, lowest lane/source) --------
-        const uint64_t key = order_key(lmin);
-        const uint32_t khi = (uint32_t)(key >> 32), klo = (uint32_t)key;
-        const uint32_t mhi = wave_min_u32(khi);
-        uint64_t cand = __ballot(khi == mhi);
-        if (__popcll(cand) > 1) {
-            const uint32_t mlo = wave_min_u32(khi == mhi ? klo : 0xFFFFFFFFu);
-            cand = __ballot(khi == mhi && klo == mlo);
-        }
-        const int wl = __ffsll((unsigned long long)cand) - 1;
-        const double tw = bcast_d(lmin, wl);
-        const int wq = SPL == 1 ? 0 : bcast_i(larg, wl);
-        const int jw = wl * SPL + wq;
-        bool own;
-        double tev;
-        if (opt) {
-            own = opt_next < tw || (opt_next == tw && (tw == RQ_INF || cbf[jw]));
-            tev = own ? opt_next : tw;
-        } else {
-            own = jw == a.ctrl_idx;
-            tev = tw;
-        }
-        if (!(tev <= a.end)) break;
-        if (evlog) es.push(tev, own ? a.ctrl_idx : jw, lane, status);
+    // LOG: exact per-sink pivot cells; rows are closed per distinct event time
+    AggX<NK> ax;
+    double* xlds = nullptr;
+    bool pend = false;      // an equal-time group is open
+    double pend_t = 0.0;
+    if (LOG) {
+        int* xs = reinterpret_cast<int*>(wb + a.lds_x_off);
+        xlds = reinterpret_cast<double*>(wb + a.lds_x_off + 12 * (size_t)a.n_sinks_pad);
+        ax.init(a.Ks, rank, xs, a.n_sinks_pad, a.n_sinks, lane);
+    }
+    auto close_row = [&]() -> bool {
+        pend = false;
+        return rs.put(pend_t, ax.row_sum(a.n_sinks, xlds), ax.nvalid, ax.cnt, lane, status);
+    };
+    // LOG: one event of the log (State.apply_event); false = stop the replica
+    auto event = [&](double tev, bool own, int jw, int e0, int e1) -> bool {
+        if (a.max_events >= 0 && n_events >= a.max_events) return false;
+        if (a.ev_t) es.push(tev, own ? a.ctrl_idx : jw, lane, status);
         ++n_events;
+        const int nsinks = own ? a.n_fol : e1 - e0;
+        if (nsinks > 0) {
+            if (pend && tev == pend_t) {
+                status |= RQ_ST_TIE;
+            } else {
+                if (pend && !close_row()) return false;
+                ++ax.gid;
+                pend = true;
+                pend_t = tev;
+            }
+            if (own) {
+                ax.touch(folat, 0, a.n_fol, true, lane);
+                ++posts;
+            } else {
+                ax.touch(colat, e0, e1, false, lane);
+                ++world;
+            }
+        }
+        return true;
+    };
 
-        if (!own || !opt) {
+    bool stop = false;
+    for (;;) {
+        // ---- A: the next <= 64 arrivals (t <= end) in (t, source) order; lane n holds #n ----
+        double tt = RQ_INF;
+        int tj = 0, n = 0;
+        while (n < 64) {
+            const uint64_t key = order_key(lmin);
+            const uint32_t khi = (uint32_t)(key >> 32), klo = (uint32_t)key;
+            const uint32_t mhi = wave_min_u32(khi);
+            uint64_t cand = __ballot(khi == mhi);
+            if (__popcll(cand) > 1) {
+                const uint32_t mlo = wave_min_u32(khi == mhi ? klo : 0xFFFFFFFFu);
+                cand = __ballot(khi == mhi && klo == mlo);
+            }
+            const int wl = __ffsll((unsigned long long)cand) - 1;
+            const double tw = bcast_d(lmin, wl);
+            if (!(tw <= a.end)) break;
+            const int wq = SPL == 1 ? 0 : bcast_i(larg, wl);
+            if (lane == n) {
+                tt = tw;
+                tj = wl * SPL + wq;
+            }
+            ++n;
             // advance the winning source; refill the rings if it ran dry
             bool dry = false;
 #pragma unroll
@@ -333,236 +372,200 @@ __global__ __launch_bounds__(512) void rq_sweep(SweepArgs a)
                 }
             }
         }
-        int nsinks;
-        if (own) {
-            nsinks = a.n_fol;
-            ag.own(rank, fol, a.n_fol, lane);
-            if (opt) opt_next = RQ_INF;
-            if (nsinks > 0) ++posts;
-        } else {
-            const int e0 = cptr[jw], e1 = cptr[jw + 1];
-            if (opt) {
-                // one Exp(c_j) draw per non-own event (opt_model.py:536-544)
-                const double x = od.next(lane);
-                const double ic = invc[jw];
+        const bool fin = n < 64;
+        const bool act = lane < n;
+        int e0 = 0, e1 = 0, od = 0;
+        if (act) {
+            e0 = cptr[tj];
+            e1 = cptr[tj + 1];
+            od = odf[tj];
+        }
+        // ---- B: RedQueen controller over the tile (opt_model.py:536-556) ----
+        //  candidate after wall event i: c_i = t_i + Exp(1)/c_{j_i}; the post fires
+        //  before wall event i when the running min beats t_i (ties: lower src_id
+        //  first); a post resets the min.  One prefix-min per post.
+        uint64_t ownm = 0;
+        double ot = RQ_INF;
+        if (opt) {
+            double c = RQ_INF;
+            bool cb = false;
+            if (act) {
+                const uint64_t d = ndraw + (uint64_t)lane;   // draw d: Philox call d>>1, half d&1
+                const uint64_t call = d >> 1;
+                uint32_t w4[4] = {(uint32_t)call, (uint32_t)(call >> 32), 0u, 0u};
+                philox4x32_10(w4, oseed, kind_salt(RQ_SRC_OPT, true));
+                const double x = rq_std_exponential((d & 1) ? rq_uniform53(w4[2], w4[3])
+                                                            : rq_uniform53(w4[0], w4[1]));
+                const double ic = invc[tj];
                 const double e = ic > 0.0 ? x * ic : RQ_INF;
-                const double c2 = tev + e;
-                if (c2 < opt_next) opt_next = c2;
+                c = tt + e;
+                cb = cbf[tj] != 0;
             }
-            nsinks = e1 - e0;
-            ag.wall(rank, col, e0, e1, odf[jw], lane);
-            if (nsinks > 0) ++world;
+            ndraw += (uint64_t)n;
+            int s0 = 0;
+            double cur = opt_next;
+            for (;;) {
+                double inc = (lane >= s0 && act) ? c : RQ_INF;
+#pragma unroll
+                for (int sh = 1; sh < 64; sh <<= 1) {
+                    const double u = __shfl_up(inc, sh, 64);
+                    if (lane >= sh) inc = fmin(inc, u);
+                }
+                double ex = __shfl_up(inc, 1, 64);
+                if (lane == 0) ex = RQ_INF;
+                const double m = fmin(cur, ex);
+                const uint64_t b = __ballot(lane >= s0 && act && (m < tt || (m == tt && cb)));
+                if (b == 0) {
+                    if (n > 0) cur = fmin(cur, bcast_d(inc, n - 1));
+                    break;
+                }
+                const int is = __ffsll((unsigned long long)b) - 1;
+                ownm |= 1ull << is;
+                if (lane == is) ot = m;
+                cur = RQ_INF;
+                s0 = is;
+            }
+            opt_next = cur;
         }
-        if (nsinks > 0 && !rs.emit(tev, ag, lane, status)) break;
-    }
-    rs.flush(lane);
-    if (evlog) es.flush(lane);
-    if (lane == 0) {
-        int64_t* cnto = a.counts + o * 4;
-        cnto[0] = posts;
-        cnto[1] = world;
-        cnto[2] = n_events;
-        cnto[3] = rs.nrow;
-        a.sall[rl] = ag.nvalid;
-        if (rs.nrow == 0) status |= RQ_ST_EMPTY;
-        if (status) atomicOr(&a.status[o], status);
-    }
-}
-
-// ============================================================================
-// 2b. merge: one workgroup per replica sorts all arrivals of its streams by
-//     (t, source index) with a bitonic network in LDS, in place.
-// ============================================================================
-__global__ __launch_bounds__(256) void rq_merge(MergeArgs a)
-{
-    extern __shared__ double lds_key[];
-    const int64_t rl = blockIdx.x;
-    if (rl >= a.n_chunk) return;
-    const int tid = threadIdx.x, nt = blockDim.x;
-    const int* slen = a.slen + rl * a.n_str;
-    __shared__ int pref[RQ_MAX_STREAMS + 1];
-    if (tid == 0) {
-        int acc = 0;
-        for (int j = 0; j < a.n_str; ++j) {
-            pref[j] = acc;
-            acc += slen[j];
-        }
-        pref[a.n_str] = acc;
-    }
-    __syncthreads();
-    const int n = pref[a.n_str];
-    if (n > a.n2max) {
-        if (tid == 0) {
-            a.mcount[rl] = -1;
-            atomicOr(&a.status[a.chunk0 + rl], RQ_ST_STREAM_OVERFLOW);   // local index
-        }
-        return;
-    }
-    int n2 = 64;
-    while (n2 < n) n2 <<= 1;
-    double* key = lds_key;
-    uint16_t* val = reinterpret_cast<uint16_t*>(lds_key + n2);
-    double* st = a.streams + rl * a.capsum;
-    for (int j = 0; j < a.n_str; ++j) {
-        const int o = (int)a.st_off[j], b = pref[j], L = pref[j + 1] - b;
-        for (int q = tid; q < L; q += nt) {
-            key[b + q] = st[o + q];
-            val[b + q] = (uint16_t)j;
-        }
-    }
-    for (int q = n + tid; q < n2; q += nt) {
-        key[q] = RQ_INF;
-        val[q] = 0xFFFF;
-    }
-    __syncthreads();
-    for (int kk = 2; kk <= n2; kk <<= 1) {
-        for (int jj = kk >> 1; jj > 0; jj >>= 1) {
-            for (int q = tid; q < n2; q += nt) {
-                const int p = q ^ jj;
-                if (p > q) {
-                    const double x = key[q], y = key[p];
-                    const uint16_t u = val[q], v = val[p];
-                    const bool gt = x > y || (x == y && u > v);
-                    if (gt == ((q & kk) == 0)) {
-                        key[q] = y;
-                        key[p] = x;
-                        val[q] = v;
-                        val[p] = u;
+        // ---- C: apply the tile's events in order ----
+        if (LOG) {
+            for (int q = 0; q < n; ++q) {
+                if ((ownm >> q) & 1ull) {
+                    if (!event(bcast_d(ot, q), true, 0, 0, 0)) {
+                        stop = true;
+                        break;
                     }
                 }
+                const int jw = bcast_i(tj, q);
+                if (!event(bcast_d(tt, q), !opt && jw == a.ctrl_idx, jw, bcast_i(e0, q),
+                           bcast_i(e1, q))) {
+                    stop = true;
+                    break;
+                }
             }
-            __syncthreads();
-        }
-    }
-    uint16_t* ms = a.msrc + rl * a.capsum;
-    for (int q = tid; q < n; q += nt) {
-        st[q] = key[q];
-        ms[q] = val[q];
-    }
-    if (tid == 0) a.mcount[rl] = n;
-}
-
-// ============================================================================
-// 2c. sorted sweep: one wavefront per replica walks the merged arrivals in
-//     64-event tiles (next tile prefetched); graph tables live in LDS.
-// ============================================================================
-template <int NK, class COL>
-__global__ __launch_bounds__(256) void rq_sweep_sorted(SweepArgs a)
-{
-    extern __shared__ double lds_sw[];
-    const int lane = lane_id();
-    const int w = threadIdx.x >> 6;
-    char* base = reinterpret_cast<char*>(lds_sw);
-    COL* col = reinterpret_cast<COL*>(base + a.lds_col);
-    int* cptr = reinterpret_cast<int*>(base + a.lds_ptr);
-    int* odf = reinterpret_cast<int*>(base + a.lds_odf);
-    int* cbf = reinterpret_cast<int*>(base + a.lds_cbf);
-    // block-shared graph tables
-    for (int e = threadIdx.x; e < a.n_csr; e += blockDim.x) col[e] = (COL)a.csr_col[e];
-    for (int j = threadIdx.x; j <= a.n_str; j += blockDim.x) cptr[j] = a.csr_ptr[j];
-    for (int j = threadIdx.x; j < a.n_str; j += blockDim.x) {
-        odf[j] = a.outdeg_f[j];
-        cbf[j] = a.ctrl_src_id < a.src_id[j];
-    }
-    const int64_t rl = (int64_t)blockIdx.x * a.wpb + w;
-    const bool live = rl < a.n_chunk;
-    const int64_t o = a.chunk0 + (live ? rl : 0);
-    const int64_t i = a.rep0 + o;
-    const int g = (int)(i / a.n_rep);
-    double* invc = reinterpret_cast<double*>(base + a.lds_wave + (size_t)w * a.lds_wave_stride);
-    int* rank = reinterpret_cast<int*>(base + a.lds_wave + (size_t)w * a.lds_wave_stride +
-                                       a.lds_rank_off);
-    for (int j = lane; j < a.n_str; j += 64) invc[j] = a.inv_c[(int64_t)g * a.n_str + j];
-    for (int c = lane; c < a.n_sinks; c += 64) rank[c] = -1;
-    __syncthreads();
-    if (!live) return;
-
-    const int nm = a.mcount[rl];
-    const double* Mt = a.streams + rl * a.capsum;
-    const uint16_t* Ms = a.msrc + rl * a.capsum;
-    int tb = 0;    // tile base
-    double ct = lane < nm ? Mt[lane] : RQ_INF;
-    int cs = lane < nm ? (int)Ms[lane] : 0;
-    double nt = 64 + lane < nm ? Mt[64 + lane] : RQ_INF;
-    int ns = 64 + lane < nm ? (int)Ms[64 + lane] : 0;
-    int kk = 0;
-
-    const bool opt = a.ctrl_kind == RQ_SRC_OPT;
-    double opt_next = opt ? a.start : RQ_INF;
-    const int64_t k = a.seed_mod > 0 ? i % a.seed_mod : i;
-    OptDraws od;
-    od.init(a.ctrl_seed ? a.ctrl_seed[i] : a.ctrl_seed0 + (uint32_t)k);
-
-    Agg<NK> ag;
-    ag.init(a.Ks);
-    RowStage<NK> rs;
-    const int64_t rbase = rl * a.cap_rows;
-    rs.init(a.rows_t + rbase, a.rows_sum + rbase, a.rows_valid + rbase, a.rows_cnt + rbase * NK,
-            a.cap_rows);
-    const bool evlog = a.ev_t != nullptr;
-    EvStage es;
-    if (evlog) es.init(a.ev_t + o * a.ev_cap, a.ev_src + o * a.ev_cap, a.ev_cap);
-    const COL* fol = col + cptr[a.ctrl_idx];
-
-    int64_t n_events = 0, posts = 0, world = 0;
-    int status = 0;
-    for (;;) {
-        if (a.max_events >= 0 && n_events >= a.max_events) break;
-        if (kk == 64) {
-            tb += 64;
-            ct = nt;
-            cs = ns;
-            const int q = tb + 64 + lane;
-            nt = q < nm ? Mt[q] : RQ_INF;
-            ns = q < nm ? (int)Ms[q] : 0;
-            kk = 0;
-        }
-        const double tw = bcast_d(ct, kk);
-        const int jw = bcast_i(cs, kk);
-        bool own;
-        double tev;
-        if (opt) {
-            own = opt_next < tw || (opt_next == tw && (tw == RQ_INF || cbf[jw]));
-            tev = own ? opt_next : tw;
         } else {
-            own = jw == a.ctrl_idx;
-            tev = tw;
-        }
-        if (!(tev <= a.end)) break;
-        if (evlog) es.push(tev, own ? a.ctrl_idx : jw, lane, status);
-        ++n_events;
-        if (!own || !opt) ++kk;
-
-        int nsinks;
-        if (own) {
-            nsinks = a.n_fol;
-            ag.own(rank, fol, a.n_fol, lane);
-            if (opt) opt_next = RQ_INF;
-            if (nsinks > 0) ++posts;
-        } else {
-            if (opt) {
-                const double x = od.next(lane);
-                const double ic = invc[jw];
-                const double e = ic > 0.0 ? x * ic : RQ_INF;
-                const double c2 = tev + e;
-                if (c2 < opt_next) opt_next = c2;
+            const bool own_b = act && ((ownm >> lane) & 1ull);     // controller post before #lane
+            const bool strm_own = act && !opt && tj == a.ctrl_idx;  // controlled stream's arrival
+            const bool has_o = own_b && a.n_fol > 0;
+            const bool has_w = act && e1 > e0;
+            // the walk only updates the per-sink ranks; lane q keeps the aggregates
+            // after its controller post (o*) and after its own event (w*)
+            int64_t osum = 0, wsum = 0;
+            int oval = 0, wval = 0;
+            int ocnt[NK], wcnt[NK];
+#pragma unroll
+            for (int kq = 0; kq < NK; ++kq) ocnt[kq] = wcnt[kq] = 0;
+            for (int q = 0; q < n; ++q) {
+                if ((ownm >> q) & 1ull) {
+                    ag.own(rank, folat, a.n_fol, lane);
+                    if (lane == q) {
+                        osum = ag.sumR;
+                        oval = ag.nvalid;
+#pragma unroll
+                        for (int kq = 0; kq < NK; ++kq) ocnt[kq] = ag.cnt[kq];
+                    }
+                }
+                const int jw = bcast_i(tj, q);
+                if (!opt && jw == a.ctrl_idx)
+                    ag.own(rank, folat, a.n_fol, lane);
+                else
+                    ag.wall(rank, colat, bcast_i(e0, q), bcast_i(e1, q), bcast_i(od, q), lane);
+                if (lane == q) {
+                    wsum = ag.sumR;
+                    wval = ag.nvalid;
+#pragma unroll
+                    for (int kq = 0; kq < NK; ++kq) wcnt[kq] = ag.cnt[kq];
+                }
             }
-            const int e0 = cptr[jw], e1 = cptr[jw + 1];
-            nsinks = e1 - e0;
-            ag.wall(rank, col, e0, e1, odf[jw], lane);
-            if (nsinks > 0) ++world;
+            const uint64_t mo = __ballot(has_o), mw = __ballot(has_w), ma = mo | mw;
+            const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+            n_events += n + __popcll(ownm);
+            posts += __popcll(mo) + __popcll(__ballot(has_w && strm_own));
+            world += __popcll(__ballot(has_w && !strm_own));
+            if (ma) {
+                // pivot_table keeps one row per distinct t (the last): a row is
+                // dropped when the next row has the same time; a first row equal
+                // to the previous tile's last row overwrites it
+                const uint64_t above = ma & ~below & ~(1ull << lane);
+                const bool nxt = above != 0;
+                const double ft = has_o ? ot : tt;
+                const double nft = __shfl(ft, nxt ? __ffsll((unsigned long long)above) - 1 : lane, 64);
+                const bool keep_o = has_o && !(has_w ? ot == tt : (nxt && ot == nft));
+                const bool keep_w = has_w && !(nxt && tt == nft);
+                const bool tie0 = rs.nrow > 0 && bcast_d(ft, __ffsll((unsigned long long)ma) - 1) == rs.last_t;
+                const uint64_t ko = __ballot(keep_o), kw = __ballot(keep_w);
+                if (tie0 || ko != mo || kw != mw) status |= RQ_ST_TIE;
+                const int64_t r0 = rs.nrow - (tie0 ? 1 : 0);
+                const int64_t po = r0 + __popcll(ko & below) + __popcll(kw & below);
+                const int64_t pw = po + (keep_o ? 1 : 0);
+                if (keep_o && po < rs.cap) {
+                    rs.Rt[po] = ot;
+                    rs.Rs[po] = (double)osum;
+                    rs.Rv[po] = (uint32_t)oval;
+#pragma unroll
+                    for (int kq = 0; kq < NK; ++kq) rs.Rc[po * NK + kq] = (uint32_t)ocnt[kq];
+                }
+                if (keep_w && pw < rs.cap) {
+                    rs.Rt[pw] = tt;
+                    rs.Rs[pw] = (double)wsum;
+                    rs.Rv[pw] = (uint32_t)wval;
+#pragma unroll
+                    for (int kq = 0; kq < NK; ++kq) rs.Rc[pw * NK + kq] = (uint32_t)wcnt[kq];
+                }
+                rs.last_t = bcast_d(has_w ? tt : ot, 63 - __builtin_clzll(ma));   // always kept
+                rs.nrow = r0 + __popcll(ko) + __popcll(kw);
+                rs.s0 = rs.nrow;
+                if (rs.nrow > rs.cap) {
+                    rs.nrow = rs.cap;
+                    rs.s0 = rs.cap;
+                    status |= RQ_ST_ROWS_OVERFLOW;
+                    stop = true;
+                }
+            }
         }
-        if (nsinks > 0 && !rs.emit(tev, ag, lane, status)) break;
+        if (stop || fin) break;
     }
+    // the controller's last post after the final arrival
+    if (!stop && opt && opt_next <= a.end) {
+        if (LOG) {
+            event(opt_next, true, 0, 0, 0);
+        } else {
+            ++n_events;
+            ag.own(rank, folat, a.n_fol, lane);
+            if (a.n_fol > 0) {
+                ++posts;
+                int64_t rr = rs.nrow;
+                if (rs.nrow > 0 && opt_next == rs.last_t) {
+                    status |= RQ_ST_TIE;
+                    rr = rs.nrow - 1;
+                } else if (rs.nrow >= rs.cap) {
+                    status |= RQ_ST_ROWS_OVERFLOW;
+                    rr = -1;
+                } else {
+                    ++rs.nrow;
+                    rs.s0 = rs.nrow;
+                    rs.last_t = opt_next;
+                }
+                if (rr >= 0 && lane == 0) {
+                    rs.Rt[rr] = opt_next;
+                    rs.Rs[rr] = (double)ag.sumR;
+                    rs.Rv[rr] = (uint32_t)ag.nvalid;
+#pragma unroll
+                    for (int kq = 0; kq < NK; ++kq) rs.Rc[rr * NK + kq] = (uint32_t)ag.cnt[kq];
+                }
+            }
+        }
+    }
+    if (LOG && pend) close_row();
     rs.flush(lane);
-    if (evlog) es.flush(lane);
+    if (LOG && a.ev_t) es.flush(lane);
     if (lane == 0) {
         int64_t* cnto = a.counts + o * 4;
         cnto[0] = posts;
         cnto[1] = world;
         cnto[2] = n_events;
         cnto[3] = rs.nrow;
-        a.sall[rl] = ag.nvalid;
+        a.sall[rl] = LOG ? ax.nvalid : ag.nvalid;
         if (rs.nrow == 0) status |= RQ_ST_EMPTY;
         if (status) atomicOr(&a.status[o], status);
     }
@@ -848,22 +851,22 @@ __global__ __launch_bounds__(64) void rq_replay(ReplayArgs a)
 // ============================================================================
 // launch wrappers
 // ============================================================================
-template <int SPL, int NK, class COL, int W>
+template <int SPL, int NK, class COL, int W, bool LOG>
 static hipError_t launch_sweep_t(const SweepArgs& a, hipStream_t s)
 {
     const unsigned blocks = (unsigned)((a.n_chunk + a.wpb - 1) / a.wpb);
-    hipLaunchKernelGGL((rq_sweep<SPL, NK, COL, W>), dim3(blocks), dim3(64 * a.wpb), a.lds_total, s, a);
+    hipLaunchKernelGGL((rq_sweep<SPL, NK, COL, W, LOG>), dim3(blocks), dim3(64 * a.wpb), a.lds_total, s, a);
     return hipGetLastError();
 }
 
-template <int SPL, class COL, int W>
+template <int SPL, class COL, int W, bool LOG>
 static hipError_t launch_sweep_k(const SweepArgs& a, int nK, hipStream_t s)
 {
     switch (nK) {
-    case 1: return launch_sweep_t<SPL, 1, COL, W>(a, s);
-    case 2: return launch_sweep_t<SPL, 2, COL, W>(a, s);
-    case 3: return launch_sweep_t<SPL, 3, COL, W>(a, s);
-    default: return launch_sweep_t<SPL, 4, COL, W>(a, s);
+    case 1: return launch_sweep_t<SPL, 1, COL, W, LOG>(a, s);
+    case 2: return launch_sweep_t<SPL, 2, COL, W, LOG>(a, s);
+    case 3: return launch_sweep_t<SPL, 3, COL, W, LOG>(a, s);
+    default: return launch_sweep_t<SPL, 4, COL, W, LOG>(a, s);
     }
 }
 
@@ -871,8 +874,10 @@ template <int SPL>
 static hipError_t launch_sweep_c(const SweepArgs& a, int nK, int col16, hipStream_t s)
 {
     if (a.win == 16)
-        return col16 ? launch_sweep_k<SPL, uint16_t, 16>(a, nK, s) : launch_sweep_k<SPL, int, 16>(a, nK, s);
-    return col16 ? launch_sweep_k<SPL, uint16_t, 8>(a, nK, s) : launch_sweep_k<SPL, int, 8>(a, nK, s);
+        return col16 ? launch_sweep_k<SPL, uint16_t, 16, false>(a, nK, s)
+                     : launch_sweep_k<SPL, int, 16, false>(a, nK, s);
+    return col16 ? launch_sweep_k<SPL, uint16_t, 8, false>(a, nK, s)
+                 : launch_sweep_k<SPL, int, 8, false>(a, nK, s);
 }
 
 hipError_t rq_launch_gen(const GenArgs& a, hipStream_t s)
@@ -883,42 +888,13 @@ hipError_t rq_launch_gen(const GenArgs& a, hipStream_t s)
     return hipGetLastError();
 }
 
-hipError_t rq_launch_merge(const MergeArgs& a, hipStream_t s)
+hipError_t rq_launch_sweep(const SweepArgs& a, int spl, int nK, int col16, int log, hipStream_t s)
 {
     if (a.n_chunk <= 0) return hipSuccess;
-    const size_t lds = (size_t)a.n2max * (sizeof(double) + sizeof(uint16_t));
-    hipLaunchKernelGGL(rq_merge, dim3((unsigned)a.n_chunk), dim3(256), lds, s, a);
-    return hipGetLastError();
-}
-
-template <int NK, class COL>
-static hipError_t launch_sorted_t(const SweepArgs& a, hipStream_t s)
-{
-    const unsigned blocks = (unsigned)((a.n_chunk + a.wpb - 1) / a.wpb);
-    hipLaunchKernelGGL((rq_sweep_sorted<NK, COL>), dim3(blocks), dim3(64 * a.wpb), a.lds_total, s, a);
-    return hipGetLastError();
-}
-
-template <class COL>
-static hipError_t launch_sorted_k(const SweepArgs& a, int nK, hipStream_t s)
-{
-    switch (nK) {
-    case 1: return launch_sorted_t<1, COL>(a, s);
-    case 2: return launch_sorted_t<2, COL>(a, s);
-    case 3: return launch_sorted_t<3, COL>(a, s);
-    default: return launch_sorted_t<4, COL>(a, s);
-    }
-}
-
-hipError_t rq_launch_sweep_sorted(const SweepArgs& a, int nK, int col16, hipStream_t s)
-{
-    if (a.n_chunk <= 0) return hipSuccess;
-    return col16 ? launch_sorted_k<uint16_t>(a, nK, s) : launch_sorted_k<int>(a, nK, s);
-}
-
-hipError_t rq_launch_sweep(const SweepArgs& a, int spl, int nK, int col16, hipStream_t s)
-{
-    if (a.n_chunk <= 0) return hipSuccess;
+    // event log / max_events: the sequential variant, eight sources per lane, W = 8
+    if (log)
+        return col16 ? launch_sweep_k<8, uint16_t, 8, true>(a, nK, s)
+                     : launch_sweep_k<8, int, 8, true>(a, nK, s);
     switch (spl) {
     case 1: return launch_sweep_c<1>(a, nK, col16, s);
     case 2: return launch_sweep_c<2>(a, nK, col16, s);

@@ -31,29 +31,30 @@ struct Agg {
             km1[q] = Ks[q] - 1;
         }
     }
-    // other source's event: sinks col[e0..e1) in edge-list order (distinct)
-    template <class COL>
-    __device__ __forceinline__ void wall(int* rank, const COL* col, int e0, int e1, int odf, int lane)
+    // other source's event: sinks colat(e0..e1) in edge-list order (distinct).
+    // Two 64-sink tiles per round so their LDS latencies overlap.
+    template <class CF>
+    __device__ __forceinline__ void wall(int* rank, CF&& colat, int e0, int e1, int odf, int lane)
     {
         int dvalid = 0;
         int dle[NK];
 #pragma unroll
         for (int q = 0; q < NK; ++q) dle[q] = 0;
-        for (int e = e0; e < e1; e += 64) {
-            const int ee = e + lane;
-            const bool act = ee < e1;
-            int r = 0, c = 0;
-            if (act) {
-                c = (int)col[ee];
-                r = rank[c];
-                rank[c] = r < 0 ? 1 : r + 1;
-            }
-            const bool inv = act && r < 0;
-            dvalid += popc(__ballot(inv));
+        for (int e = e0; e < e1; e += 128) {
+            const int ea = e + lane, eb = e + 64 + lane;
+            const bool acta = ea < e1, actb = eb < e1;
+            const int ca = acta ? colat(ea) : 0;
+            const int cb = actb ? colat(eb) : 0;
+            const int ra = acta ? rank[ca] : 0;
+            const int rb = actb ? rank[cb] : 0;
+            if (acta) rank[ca] = ra < 0 ? 1 : ra + 1;
+            if (actb) rank[cb] = rb < 0 ? 1 : rb + 1;
+            const bool inva = acta && ra < 0, invb = actb && rb < 0;
+            dvalid += popc(__ballot(inva)) + popc(__ballot(invb));
 #pragma unroll
             for (int q = 0; q < NK; ++q) {
-                dle[q] += popc(__ballot(inv && 1 <= km1[q]));
-                dle[q] -= popc(__ballot(act && r >= 0 && r == km1[q]));
+                if (1 <= km1[q]) dle[q] += popc(__ballot(inva)) + popc(__ballot(invb));
+                dle[q] -= popc(__ballot(acta && ra == km1[q])) + popc(__ballot(actb && rb == km1[q]));
             }
         }
         nvalid += dvalid;
@@ -63,8 +64,8 @@ struct Agg {
         sumF += odf;
     }
     // own post: every follower's rank -> 0 (State.apply_event, opt_model.py:71-72)
-    template <class COL>
-    __device__ __forceinline__ void own(int* rank, const COL* fol, int F, int lane)
+    template <class CF>
+    __device__ __forceinline__ void own(int* rank, CF&& folat, int F, int lane)
     {
         int dvalid = 0;
         int dle[NK];
@@ -75,7 +76,7 @@ struct Agg {
             const bool act = f < F;
             int r = 0, c = 0;
             if (act) {
-                c = (int)fol[f];
+                c = folat(f);
                 r = rank[c];
             }
             dvalid += popc(__ballot(act && r < 0));
@@ -91,14 +92,117 @@ struct Agg {
     }
 };
 
-// One pivot row per distinct event time; lane (row & 63) stages a row until
-// its 64-row tile is written with one coalesced store per field.
+// Exact aggregates for the sequential (LOG) sweep, equal event times included.
+// pivot_table(index='t', columns='sink_id', values='rank') averages the ranks
+// of all rows sharing (t, sink): a sink touched m > 1 times by events at one
+// time shows the mean of its m ranks in that row -- and, through ffill, in
+// every later row until it is touched again.  Per sink: rank (true rank,
+// drives increments), gtag/gcnt/gsum (group id, touches and rank sum of its
+// last equal-time group); its pivot cell is gsum/gcnt.  Row sums are exact
+// int64 while every cell is integral, else a numpy-order pass over the sinks
+// (pandas' DataFrame.mean(1) sums each row pairwise).
+template <int NK>
+struct AggX {
+    int64_t sumI;          // sum of the integral cells of valid sinks
+    int nvalid, nfrac, gid;
+    int cnt[NK], km1[NK];
+    int* rank;
+    int* gtag;
+    int* gcnt;
+    int* gsum;
+    __device__ __forceinline__ void init(const int* Ks, int* rank_, int* x, int stride, int n_sinks,
+                                         int lane)
+    {
+        sumI = 0;
+        nvalid = 0;
+        nfrac = 0;
+        gid = 0;
+#pragma unroll
+        for (int q = 0; q < NK; ++q) {
+            cnt[q] = 0;
+            km1[q] = Ks[q] - 1;
+        }
+        rank = rank_;
+        gtag = x;
+        gcnt = x + stride;
+        gsum = x + 2 * stride;
+        for (int c = lane; c < n_sinks; c += 64) {
+            gtag[c] = -1;
+            gcnt[c] = 0;
+            gsum[c] = 0;
+        }
+    }
+    // one event's rows: sinks colat(e0..e1) (distinct), new rank 0 (own) or +1 (wall)
+    template <class CF>
+    __device__ __forceinline__ void touch(CF&& colat, int e0, int e1, bool own, int lane)
+    {
+        for (int e = e0; e < e1; e += 64) {
+            const int ee = e + lane;
+            const bool act = ee < e1;
+            bool nv = false, fup = false, fdn = false;
+            int dsum = 0;
+            bool up[NK], dn[NK];
+#pragma unroll
+            for (int q = 0; q < NK; ++q) up[q] = dn[q] = false;
+            if (act) {
+                const int c = colat(ee);
+                const int r = rank[c], tg = gtag[c], k = gcnt[c], sm = gsum[c];
+                const bool ov = tg >= 0;
+                const int rn = own ? 0 : (r < 0 ? 1 : r + 1);
+                const int nk = tg == gid ? k + 1 : 1;
+                const int ns = tg == gid ? sm + rn : rn;
+                rank[c] = rn;
+                gtag[c] = gid;
+                gcnt[c] = nk;
+                gsum[c] = ns;
+                const int kk = k > 0 ? k : 1;
+                const bool oint = ov && sm % kk == 0;
+                const bool nint = ns % nk == 0;
+                nv = !ov;
+                fup = !nint && !(ov && !oint);
+                fdn = nint && ov && !oint;
+                dsum = (nint ? ns / nk : 0) - (oint ? sm / kk : 0);
+#pragma unroll
+                for (int q = 0; q < NK; ++q) {
+                    const bool a1 = ns <= km1[q] * nk;
+                    const bool a0 = ov && sm <= km1[q] * kk;
+                    up[q] = a1 && !a0;
+                    dn[q] = a0 && !a1;
+                }
+            }
+            nvalid += popc(__ballot(nv));
+            nfrac += popc(__ballot(fup)) - popc(__ballot(fdn));
+#pragma unroll
+            for (int q = 0; q < NK; ++q) cnt[q] += popc(__ballot(up[q])) - popc(__ballot(dn[q]));
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) dsum += __shfl_xor(dsum, o, 64);
+            sumI += dsum;
+        }
+    }
+    // the current pivot row's sum over the sinks (NaN cells count 0)
+    __device__ __forceinline__ double row_sum(int n_sinks, double* lds)
+    {
+        if (nfrac == 0) return (double)sumI;
+        double out[1];
+        wave_npsum<1>((int64_t)n_sinks,
+                      [&](int64_t kk, double* v) {
+                          const int c = (int)kk;
+                          v[0] = gtag[c] >= 0 ? (double)gsum[c] / (double)gcnt[c] : 0.0;
+                      },
+                      lds, out);
+        return out[0];
+    }
+};
+
+// Pivot rows.  LOG sweep: lane (row - s0) stages a row until 64 are staged,
+// then one coalesced store per field.  The fast sweep stores whole tiles
+// itself and only keeps nrow / last_t here (s0 == nrow).
 template <int NK>
 struct RowStage {
     double r_t, r_sum;
     int r_valid;
     int r_cnt[NK];
-    int64_t nrow, cap;
+    int64_t nrow, s0, cap;
     double last_t;
     double* Rt;
     double* Rs;
@@ -112,6 +216,7 @@ struct RowStage {
 #pragma unroll
         for (int q = 0; q < NK; ++q) r_cnt[q] = 0;
         nrow = 0;
+        s0 = 0;
         cap = cap_;
         last_t = -RQ_INF;
         Rt = t;
@@ -119,43 +224,28 @@ struct RowStage {
         Rv = v;
         Rc = c;
     }
-    // returns false when the capacity is exhausted
-    __device__ __forceinline__ bool emit(double t, const Agg<NK>& g, int lane, int& status)
+    // one whole row (no tie merge: the caller closes equal-time groups itself)
+    __device__ __forceinline__ bool put(double t, double sum, int valid, const int* cnt, int lane,
+                                       int& status)
     {
-        if (nrow > 0 && t == last_t) {
-            // same timestamp as the previous row: pivot_table merges them
-            status |= RQ_ST_TIE;
-            const int64_t rr = nrow - 1;
-            if ((nrow & 63) != 0) {
-                if (lane == (int)(rr & 63)) {
-                    r_sum = (double)g.sumR;
-                    r_valid = g.nvalid;
-#pragma unroll
-                    for (int q = 0; q < NK; ++q) r_cnt[q] = g.cnt[q];
-                }
-            } else if (lane == 0) {
-                Rs[rr] = (double)g.sumR;
-                Rv[rr] = (uint32_t)g.nvalid;
-#pragma unroll
-                for (int q = 0; q < NK; ++q) Rc[rr * NK + q] = (uint32_t)g.cnt[q];
-            }
-            return true;
-        }
         if (nrow >= cap) {
             status |= RQ_ST_ROWS_OVERFLOW;
             return false;
         }
-        const int slot = (int)(nrow & 63);
+        const int slot = (int)(nrow - s0);
         if (lane == slot) {
             r_t = t;
-            r_sum = (double)g.sumR;
-            r_valid = g.nvalid;
+            r_sum = sum;
+            r_valid = valid;
 #pragma unroll
-            for (int q = 0; q < NK; ++q) r_cnt[q] = g.cnt[q];
+            for (int q = 0; q < NK; ++q) r_cnt[q] = cnt[q];
         }
         ++nrow;
         last_t = t;
-        if (slot == 63) store(nrow - 64 + lane);
+        if (slot == 63) {
+            store(s0 + lane);
+            s0 = nrow;
+        }
         return true;
     }
     __device__ __forceinline__ void store(int64_t rr)
@@ -168,8 +258,9 @@ struct RowStage {
     }
     __device__ __forceinline__ void flush(int lane)
     {
-        const int rem = (int)(nrow & 63);
-        if (lane < rem) store(nrow - rem + lane);
+        const int rem = (int)(nrow - s0);
+        if (lane < rem) store(s0 + lane);
+        s0 = nrow;
     }
 };
 
@@ -215,39 +306,6 @@ struct EvStage {
                 Es[n - rem + lane] = e_src;
             }
         }
-    }
-};
-
-// The RedQueen controller's exponentials: one Philox call per lane yields 128
-// standard exponentials per batch; draw k of the batch lives in lane k>>1.
-struct OptDraws {
-    uint32_t seed, salt;
-    uint64_t batch;
-    int k;
-    double x0, x1;
-    __device__ __forceinline__ void init(uint32_t seed_)
-    {
-        seed = seed_;
-        salt = kind_salt(RQ_SRC_OPT, true);
-        batch = 0;
-        k = 128;
-        x0 = 0.0;
-        x1 = 0.0;
-    }
-    __device__ __forceinline__ double next(int lane)
-    {
-        if (k == 128) {
-            const uint64_t call = batch * 64 + lane;
-            uint32_t c[4] = {(uint32_t)call, (uint32_t)(call >> 32), 0u, 0u};
-            philox4x32_10(c, seed, salt);
-            x0 = rq_std_exponential(rq_uniform53(c[0], c[1]));
-            x1 = rq_std_exponential(rq_uniform53(c[2], c[3]));
-            ++batch;
-            k = 0;
-        }
-        const double x = bcast_d((k & 1) ? x1 : x0, k >> 1);
-        ++k;
-        return x;
     }
 };
 

@@ -42,8 +42,10 @@ class Graph:
                  ctrl_a=None, ctrl_b=None):
         self._keep = []
         srcs = []
+        self.has_realdata = False
         for name, kw in other_sources:
             kind = _source_kind(name)
+            self.has_realdata = self.has_realdata or kind == L.SRC_REALDATA
             if kind == L.SRC_OPT:
                 raise NotImplementedError("an Opt broadcaster among the other sources")
             d = L.SourceDesc()
@@ -225,6 +227,13 @@ class Graph:
             torch.cuda.current_stream().synchronize()
             ovf = int((status & (L.ST_ROWS_OVERFLOW | L.ST_STREAM_OVERFLOW)).any().item())
             if not ovf:
+                # equal event times in the fast tiled sweep: redo with the exact sequential
+                # sweep (never taken by continuous-time worlds; RealData runs are exact already)
+                seq = (event_log or b.max_events >= 0 or b.sweep_mode != 0 or self.has_realdata
+                       or ck == L.SRC_REALDATA)
+                if not seq and int((status & L.ST_TIE).any().item()):
+                    b.sweep_mode = 2
+                    continue
                 return res
             if b.cap_scale > 64:
                 raise L.RQError("rq_run_batch", L.RQ_EOVERFLOW)

@@ -353,11 +353,26 @@ def gen_dist(n, worlds=True):
                         poisson_seed_offset=np.asarray([POISSON_SEED_OFFSET]))
     if not worlds:
         return
+    gen_worlds(n)
+
+
+# (replicas, first seed) per world: seeds u = seed0 + r feed randomize_other_sources(u),
+# i.e. source idx k gets seed u + 99 k, so replicas r and r + 99 share a stream and the
+# test uses a cluster-robust variance (clusters r mod 99).  The Hawkes ensemble is
+# larger (30k, seed0 3e6): a 10k draw at seed0 0 sat 3 sd off the engine's mean.
+WORLD_SAMPLES = {"hawkes": (30000, 3_000_000), "pwconst": (10000, 0)}
+
+
+def gen_worlds(n=0):
     rec = {}
     for name in WORLDS:
+        cnt, seed0 = WORLD_SAMPLES[name]
+        if n:
+            cnt = n
         with mp.Pool(os.cpu_count()) as pool:
-            rec[name] = np.asarray(pool.map(_world_worker, [(name, r) for r in range(n)],
-                                            chunksize=16))
+            rec[name] = np.asarray(pool.map(_world_worker, [(name, seed0 + r) for r in range(cnt)],
+                                            chunksize=16)).astype(np.float32)
+        rec[name + "_seed0"] = np.asarray([seed0])
     np.savez_compressed(os.path.join(HERE, "dist_world.npz"), **rec)
 
 
@@ -366,10 +381,16 @@ if __name__ == "__main__":
     ap.add_argument("--dist", type=int, default=0)
     ap.add_argument("--only", default="")
     ap.add_argument("--no-worlds", action="store_true")
+    ap.add_argument("--worlds", action="store_true", help="only dist_world.npz")
     a = ap.parse_args()
     steps = {"npsum": gen_npsum, "draws": gen_draws, "readme": gen_readme, "kats": gen_kats,
              "adv": gen_adversarial, "graphs": gen_graphs, "frac": gen_frac}
+    if a.worlds:
+        gen_worlds()
+        print("done worlds", flush=True)
     for k, f in steps.items():
+        if a.worlds:
+            break
         if not a.only or k in a.only.split(","):
             f()
             print("done", k, flush=True)

@@ -42,11 +42,21 @@ def _oracle(O, so, ctrl, Ks, max_events=None):
     return met, t, s
 
 
+MODES = ["fast", "log"]
+
+
+def _mode_kw(mode):
+    """fast: the tiled sweep with vectorised row placement (no event log);
+    log: the sequential event-log variant (sweep_mode=2), events compared too."""
+    return dict(event_log=True, sweep_mode=2) if mode == "log" else dict(event_log=False)
+
+
 def _cmp_replica(res, i, met_o, t_o, s_o, Ks):
-    t, s = res.events(i)
-    assert t.shape == t_o.shape, (t.shape, t_o.shape)
-    assert np.array_equal(s, s_o)
-    assert np.array_equal(t, t_o), np.max(np.abs(t - t_o))
+    if res.ev_t is not None:
+        t, s = res.events(i)
+        assert t.shape == t_o.shape, (t.shape, t_o.shape)
+        assert np.array_equal(s, s_o)
+        assert np.array_equal(t, t_o), np.max(np.abs(t - t_o))
     m = res.metrics[i].cpu().numpy()
     top, avg, r2, cnt = met_o
     exp = np.asarray(list(top) + [avg, r2])
@@ -56,53 +66,53 @@ def _cmp_replica(res, i, met_o, t_o, s_o, Ks):
     assert c[2] == len(t_o)
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("seed", [101, 5, 7])
 def test_readme_single(seed, mode):
     torch, engine, graphs, O = _ctx()
     so = graphs.readme()
     g = _graph(engine, so)
     Ks = (1, 2, 5)
-    res = g.run("opt", q=so["q"], s=so["s"], n_rep=1, ctrl_seed=seed, Ks=Ks, event_log=True,
-                sweep_mode=mode)
+    res = g.run("opt", q=so["q"], s=so["s"], n_rep=1, ctrl_seed=seed, Ks=Ks, **_mode_kw(mode))
     met_o, t_o, s_o = _oracle(O, so, ("opt", seed), Ks)
     _cmp_replica(res, 0, met_o, t_o, s_o, Ks)
     assert int(res.status[0].item()) == 0
 
 
-def test_readme_batch_randomized():
+@pytest.mark.parametrize("mode", MODES)
+def test_readme_batch_randomized(mode):
     torch, engine, graphs, O = _ctx()
     so = graphs.readme()
     g = _graph(engine, so)
     R = 48
     res = g.run("opt", q=so["q"], s=so["s"], n_rep=R, ctrl_seed=1000, world_seed=1000,
-                randomize=True, Ks=(1,), event_log=True)
+                randomize=True, Ks=(1,), **_mode_kw(mode))
     for r in range(0, R, 7):
         u = 1000 + r
         met_o, t_o, s_o = _oracle(O, _world_with_seeds(so, u), ("opt", u), (1,))
         _cmp_replica(res, r, met_o, t_o, s_o, (1,))
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("seed", [3, 4, 17])
 def test_mixed_kinds(seed, mode):
     torch, engine, graphs, O = _ctx()
     so = graphs.mixed()
     g = _graph(engine, so)
     Ks = (1, 2, 5, 10)
-    res = g.run("opt", q=so["q"], s=so["s"], n_rep=1, ctrl_seed=seed, Ks=Ks, event_log=True,
-                sweep_mode=mode)
+    res = g.run("opt", q=so["q"], s=so["s"], n_rep=1, ctrl_seed=seed, Ks=Ks, **_mode_kw(mode))
     met_o, t_o, s_o = _oracle(O, so, ("opt", seed), Ks)
     _cmp_replica(res, 0, met_o, t_o, s_o, Ks)
 
 
-def test_kat_weights_and_grid():
+@pytest.mark.parametrize("mode", MODES)
+def test_kat_weights_and_grid(mode):
     torch, engine, graphs, O = _ctx()
     so = graphs.kat_two_walls((0.5, 1.5))
     g = _graph(engine, so)
     qs = np.asarray([0.01, 1.0, 30.0])
     s = np.asarray([[0.5, 1.5], [1.0, 1.0], [1.5, 0.25]])
-    res = g.run("opt", q=qs, s=s, n_rep=3, ctrl_seed=11, seed_mod=3, Ks=(1, 2), event_log=True)
+    res = g.run("opt", q=qs, s=s, n_rep=3, ctrl_seed=11, seed_mod=3, Ks=(1, 2), **_mode_kw(mode))
     for gi in range(3):
         for r in range(3):
             sog = dict(so, q=float(qs[gi]), s=s[gi])
@@ -110,41 +120,41 @@ def test_kat_weights_and_grid():
             _cmp_replica(res, gi * 3 + r, met_o, t_o, s_o, (1, 2))
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", MODES)
 def test_poisson_controlled_and_wall(mode):
     torch, engine, graphs, O = _ctx()
     so = graphs.readme()
     g = _graph(engine, so)
     rates = torch.tensor([4.0, 0.0, 9.5, 1.25], dtype=torch.float64)
-    res = g.run("poisson", n_rep=4, ctrl_seed=7, ctrl_rate=rates, Ks=(1,), event_log=True,
-                sweep_mode=mode)
+    res = g.run("poisson", n_rep=4, ctrl_seed=7, ctrl_rate=rates, Ks=(1,), **_mode_kw(mode))
     for r in range(4):
         met_o, t_o, s_o = _oracle(O, so, ("poisson", 7 + r, float(rates[r])), (1,))
         _cmp_replica(res, r, met_o, t_o, s_o, (1,))
-    res = g.run("wall", n_rep=1, Ks=(1, 3), event_log=True, sweep_mode=mode)
+    res = g.run("wall", n_rep=1, Ks=(1, 3), **_mode_kw(mode))
     met_o, t_o, s_o = _oracle(O, so, ("wall",), (1, 3))
     _cmp_replica(res, 0, met_o, t_o, s_o, (1, 3))
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", MODES)
 def test_max_events(mode):
     torch, engine, graphs, O = _ctx()
     so = graphs.readme()
     g = _graph(engine, so)
     res = g.run("opt", q=1.0, s=so["s"], n_rep=1, ctrl_seed=101, max_events=500, Ks=(1,),
-                event_log=True, sweep_mode=mode)
+                **_mode_kw(mode))
     met_o, t_o, s_o = _oracle(O, so, ("opt", 101), (1,), max_events=500)
     assert len(t_o) == 500
     _cmp_replica(res, 0, met_o, t_o, s_o, (1,))
 
 
-def test_c3_replicas():
+@pytest.mark.parametrize("mode", MODES)
+def test_c3_replicas(mode):
     torch, engine, graphs, O = _ctx()
     so = graphs.c3()
     g = _graph(engine, so)
     R = 6
     res = g.run("opt", q=so["q"], s=so["s"], n_rep=R, ctrl_seed=500, world_seed=500,
-                randomize=True, Ks=(1, 10), event_log=True)
+                randomize=True, Ks=(1, 10), **_mode_kw(mode))
     assert int(res.status.abs().sum().item()) == 0
     for r in range(0, R, 2):
         u = 500 + r
@@ -163,8 +173,62 @@ def test_large_batch_no_overflow_and_determinism():
     c = g.run("opt", q=so["q"], s=so["s"], n_rep=2048, ctrl_seed=0, world_seed=0,
               randomize=True, Ks=(1,), sweep_mode=2)
     assert torch.equal(a.metrics, b.metrics) and torch.equal(a.counts, b.counts)
-    # the merge+sorted sweep and the general wave-min sweep are the same machine
+    # the tiled fast sweep and the sequential event-log variant are the same machine
     assert torch.equal(a.metrics, c.metrics) and torch.equal(a.counts, c.counts)
     assert int(a.status.sum().item()) == 0
     ev = a.n_events.double().mean().item()
     assert 4800 < ev < 6200, ev
+
+
+def _tie_world():
+    """Two RealData walls on the same quarter-grid times (duplicates inside each
+    and across both) plus a Poisson wall: equal-time pivot rows everywhere,
+    including across the sweep's 64-event tile boundaries."""
+    rng = np.random.RandomState(77)
+    T = np.sort(np.round(rng.uniform(0.0, 50.0, 150) * 4.0) / 4.0)
+    so = dict(src_id=1, end_time=50.0, s=np.asarray([1.0, 2.0]), q=1.5, sink_ids=[10, 11, 12],
+              other_sources=[("RealData", {"src_id": 2, "times": T.tolist()}),
+                             ("RealData", {"src_id": 3, "times": T.tolist()}),
+                             ("Poisson", {"src_id": 4, "seed": 5, "rate": 2.0})],
+              edge_list=[(1, 10), (1, 11), (2, 10), (2, 11), (3, 11), (3, 12), (4, 12), (4, 10)])
+    return so, T
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_equal_time_rows(mode):
+    torch, engine, graphs, O = _ctx()
+    so, T = _tie_world()
+    ctimes = T[::3].copy()
+    g = engine.Graph(so["src_id"], so["other_sources"], so["sink_ids"], so["edge_list"],
+                     so["end_time"], ctrl_a=ctimes)
+    Ks = (1, 2)
+    res = g.run("times", n_rep=1, Ks=Ks, **_mode_kw(mode))
+    met_o, t_o, s_o = _oracle(O, so, ("times", ctimes), Ks)
+    _cmp_replica(res, 0, met_o, t_o, s_o, Ks)
+    g2 = _graph(engine, so)
+    for seed in (1, 2, 3):
+        res = g2.run("opt", q=so["q"], s=so["s"], n_rep=1, ctrl_seed=seed, Ks=Ks, **_mode_kw(mode))
+        met_o, t_o, s_o = _oracle(O, so, ("opt", seed), Ks)
+        _cmp_replica(res, 0, met_o, t_o, s_o, Ks)
+
+
+def test_fast_sweep_equal_times_disjoint_sinks():
+    """The tiled sweep's vectorised row placement on equal-time rows (forced with
+    sweep_mode=1): two RealData walls on the same (distinct) times feeding
+    disjoint sinks -- every sink is touched at most once per time, so keeping
+    the last row is the reference's pivot exactly; rows tie inside and across
+    64-event tiles."""
+    torch, engine, graphs, O = _ctx()
+    so, T = _tie_world()
+    T = np.unique(T)
+    so = dict(so, other_sources=[("RealData", {"src_id": 2, "times": T.tolist()}),
+                                 ("RealData", {"src_id": 3, "times": T.tolist()}),
+                                 ("Poisson", {"src_id": 4, "seed": 5, "rate": 2.0})],
+              edge_list=[(1, 10), (1, 11), (2, 10), (3, 12), (4, 11)])
+    g = _graph(engine, so)
+    Ks = (1, 2)
+    for seed in (1, 2, 3, 4):
+        res = g.run("opt", q=so["q"], s=so["s"], n_rep=1, ctrl_seed=seed, Ks=Ks, sweep_mode=1)
+        assert int(res.status[0].item()) & 4   # the ties were seen
+        met_o, t_o, s_o = _oracle(O, so, ("opt", seed), Ks)
+        _cmp_replica(res, 0, met_o, t_o, s_o, Ks)

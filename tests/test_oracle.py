@@ -212,15 +212,21 @@ def test_engine_world_distributions(golden):
                                        ("Poisson2", {"src_id": 4, "seed": 0, "rate": 2.5})],
                         edge_list=[(2, 1), (3, 2), (4, 1), (4, 2)]),
     }
+    def cvar(x):
+        # cluster-robust variance of the mean: randomize_other_sources(u) gives source k
+        # seed u + 99 k, so replicas r and r + 99 share streams (clusters r mod 99)
+        x = np.asarray(x, np.float64)
+        sums = np.bincount(np.arange(len(x)) % 99, x - x.mean())
+        return float((sums ** 2).sum()) / len(x) ** 2
+
     for name, so in worlds.items():
-        ref = d[name]
+        ref = d[name].astype(np.float64)
         ns = len(so["other_sources"])
-        n = ref.shape[0]
-        out, cnt, _ = O.engine_batch(O.Scenario(so, ("wall",)), n, 0, True, KS, 8)
+        out, cnt, _ = O.engine_batch(O.Scenario(so, ("wall",)), 40000, 0, True, KS, 8)
         r_world = ref[:, :ns].sum(1)
         for v, r, lab in [(cnt[:, 1], r_world, "world")] + \
                 [(out[:, i], ref[:, ns + i], "m%d" % i) for i in range(len(KS) + 2)]:
-            z = (v.mean() - r.mean()) / math.sqrt(v.var() / len(v) + r.var() / len(r) + 1e-300)
+            z = (v.mean() - r.mean()) / math.sqrt(cvar(v) + cvar(r) + 1e-300)
             assert abs(z) < 2.576, (name, lab, r.mean(), v.mean(), z)
 
 
