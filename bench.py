@@ -87,6 +87,7 @@ def main():
                      so["end_time"])
     R = a.replicas
     Ks = (1,)
+    plan = g.run("opt", q=so["q"], s=so["s"], n_rep=R, randomize=True, Ks=Ks, plan_only=True)
 
     def step(k):
         base = (k * world + rank) * R
@@ -161,7 +162,6 @@ def main():
     achieved = sweep_bytes / (sweep_ms * 1e-3) / 1e9
     scan_ms = ms[2] / max(1, int(nl[2]))
     gen_ms = ms[0] / max(1, int(nl[0]))
-    merge_ms = ms[4] / max(1, int(nl[4]))
     scan_gbs = SCAN_B_PER_ROW * rows_step / (scan_ms * 1e-3) / 1e9 if scan_ms > 0 else None
     gen_gbs = GEN_B_PER_WALL_EVENT * (ev_rank - posts_step) / (gen_ms * 1e-3) / 1e9 \
         if gen_ms > 0 else None
@@ -194,8 +194,8 @@ def main():
             "events_per_sec": ev_rate,
             "events_per_replica": local_ev / replicas,
             "overflow": int(status.item()),
-            "kernels_ms_per_launch": {"gen_streams": gen_ms, "merge": merge_ms, "sweep": sweep_ms,
-                                      "scan": scan_ms},
+            "kernels_ms_per_launch": {"gen_streams": gen_ms, "sweep": sweep_ms, "scan": scan_ms},
+            "sweep_plan": plan,
             "roofline": {"bound": "hbm", "kernel": "rq_sweep", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": None,

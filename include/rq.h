@@ -140,7 +140,8 @@ typedef struct rq_batch_desc {
                                  /* indexed locally, seeds and grid point use the global id     */
     int32_t sweep_mode;          /* 0 auto: fast tiled sweep unless the run needs the sequential
                                     one (event log, max_events, RealData); 1 fast whenever the
-                                    event log / max_events allow; 2 force the sequential sweep */
+                                    event log / max_events allow; 2 force the sequential sweep;
+                                    3 as 0 but never the K=1 sink-bitset variant             */
                                  /* sweep; both are bit-identical, auto picks the faster one    */
 } rq_batch_desc;
 
@@ -170,6 +171,13 @@ int rq_graph_followers(rq_graph_t g, int64_t* ids);
 int rq_workspace_size(rq_graph_t g, const rq_batch_desc* b, size_t* bytes);
 /* suggested per-replica event-log capacity for RQ_RUN_EVENT_LOG */
 int rq_event_capacity(rq_graph_t g, const rq_batch_desc* b, int64_t* cap);
+/* how rq_run_batch will run this batch (diagnostics / occupancy reporting):
+ * info[0] sweep variant (0 fast tiled, 1 sequential exact, 2 fast tiled on K=1 sink
+ * bitsets), [1] sources per lane,
+ * [2] arrival-ring depth W, [3] waves per block, [4] blocks per CU (runtime occupancy,
+ * 0 without a device), [5] sink columns in LDS (1) or global (0), [6] dynamic LDS
+ * bytes per block, [7] replicas per chunk */
+int rq_plan_info(rq_graph_t g, const rq_batch_desc* b, int64_t* info);
 
 int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out,
                  void* workspace, size_t workspace_bytes, void* hip_stream);

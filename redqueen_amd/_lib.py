@@ -83,6 +83,7 @@ def lib():
     L.rq_graph_followers.argtypes = [_P, _pi64]
     L.rq_workspace_size.argtypes = [_P, C.POINTER(BatchDesc), C.POINTER(C.c_size_t)]
     L.rq_event_capacity.argtypes = [_P, C.POINTER(BatchDesc), _pi64]
+    L.rq_plan_info.argtypes = [_P, C.POINTER(BatchDesc), _pi64]
     L.rq_run_batch.argtypes = [_P, C.POINTER(BatchDesc), C.POINTER(Outputs), _P, C.c_size_t, _P]
     L.rq_replay_workspace_size.argtypes = [C.c_int64, C.c_int32, C.POINTER(C.c_size_t)]
     L.rq_metrics_replay.argtypes = [_P, _P, _P, _P, C.c_int64, C.c_int32, C.c_int64, C.c_double,
@@ -113,5 +114,5 @@ def check(fn, code):
 
 EXPORTED = ["rq_abi_version", "rq_strerror", "rq_graph_build", "rq_graph_free", "rq_graph_info",
             "rq_graph_source_ids", "rq_graph_followers", "rq_workspace_size",
-            "rq_event_capacity", "rq_run_batch", "rq_replay_workspace_size",
+            "rq_event_capacity", "rq_plan_info", "rq_run_batch", "rq_replay_workspace_size",
             "rq_metrics_replay", "rq_timing", "rq_timing_read"]

@@ -103,6 +103,10 @@ struct rq_graph {
     std::vector<int> csr_ptr, csr_col, outdeg_f, fol;
     std::vector<int64_t> fol_ids;
     std::vector<int> col_to_fol;     // sink column -> follower position or -1
+    // per-stream sink bitsets (32 sinks per word) for the K=1 bitset sweep, n_sinks <= 2048
+    int nw = 0;
+    std::vector<uint32_t> masks;
+    DevBuf<uint32_t> d_mask;
     // controlled-slot arrays (PiecewiseConst / RealData controlled runs)
     int ctrl_arr_off = 0, ctrl_arr_n = 0;
     DevBuf<int64_t> d_src_id;
@@ -118,8 +122,8 @@ struct Plan {
     int64_t R = 0, chunk = 0, capsum = 0, cap_rows = 0;
     std::vector<int> cap;
     std::vector<int64_t> st_off;
-    // sequential (event log / max_events) sweep variant
-    bool log = false;
+    // sequential (event log / max_events) sweep variant; K=1 sink-bitset variant
+    bool log = false, bits = false;
     // general sweep LDS layout
     int gwpb = 4, gwin = 16, gcol_lds = 1, gcol16 = 0;
     size_t g_col = 0, g_ptr = 0, g_odf = 0, g_cbf = 0, g_wave = 0, g_wave_stride = 0, g_rank_off = 0,
@@ -131,6 +135,7 @@ struct Plan {
 };
 
 constexpr size_t kLdsMax = 160 * 1024;
+constexpr int kBitsMaxSinks = 2048;   // bitset sweep: one 32-sink word per lane
 
 double stream_mean_var(const rq_graph* g, int j, int kind, const rq_batch_desc* b, double* var)
 {
@@ -235,7 +240,12 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     for (int k : g->kind) has_rd = has_rd || k == RQ_SRC_REALDATA;
     p->log = (b->flags & RQ_RUN_EVENT_LOG) || b->max_events >= 0 || b->sweep_mode == 2 ||
              (has_rd && b->sweep_mode != 1);
+    for (int q = 0; q < b->nK; ++q) p->log = p->log || b->Ks[q] > 32767;   // int16 ranks
     if (p->log) p->spl = 8;
+
+    p->bits = !p->log && p->nK == 1 && b->Ks[0] == 1 && g->nw > 0 && b->sweep_mode != 3 &&
+              (size_t)g->n_str * g->nw * 4 <= 64 * 1024;
+    if (p->bits) p->spl = g->n_str <= 64 ? 1 : g->n_str <= 128 ? 2 : g->n_str <= 256 ? 4 : 8;
 
     // general sweep: pick (ring depth W, waves per block) for the most waves per CU
     {
@@ -244,7 +254,9 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
         // global memory as int (the kernel's COL type selects the path at compile time)
         for (int col_lds = g->n_sinks <= 65535 ? 1 : 0; col_lds >= 0 && best < 0; --col_lds) {
             const int c16 = col_lds;
-            const size_t colb = col_lds ? 2 * g->csr_col.size() : 0;
+            // BITS: sink bitsets [n_str][nw] replace the columns (and the per-wave ranks)
+            const size_t colb = p->bits ? 4 * (size_t)g->n_str * g->nw
+                                        : (col_lds ? 2 * g->csr_col.size() : 0);
             size_t sh = 0;
             const size_t o_col = sh;  sh = align_up(sh + colb, 16);
             const size_t o_ptr = sh;  sh = align_up(sh + 4 * (g->n_str + 1), 16);
@@ -254,17 +266,23 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
             for (int W : {16, 8}) {
                 if (p->log && W != 8) continue;
                 const size_t r_off = align_up(8 * (size_t)g->n_str, 16);
-                const size_t w_off = align_up(r_off + 4 * (size_t)p->n_sinks_pad, 16);
-                size_t stride = align_up(w_off + 8 * (size_t)64 * spl * W, 16);
+                const size_t rank_b = p->log ? 4 : (p->bits ? 0 : 2);   // fast: int16 saturating
+                const size_t w_off = align_up(r_off + rank_b * (size_t)p->n_sinks_pad, 16);
+                // rings: W arrivals for each real source (lanes past n_str own none)
+                size_t stride = align_up(w_off + 8 * (size_t)g->n_str * W, 16);
                 // LOG: per-sink gtag/gcnt/gsum + a wave_npsum<1> scratch (304 doubles)
                 const size_t x_off = stride;
                 if (p->log) stride = align_up(x_off + 12 * (size_t)p->n_sinks_pad + 8 * 304, 16);
-                for (int wpb : {8, 4, 2, 1}) {
+                for (int wpb : {16, 12, 10, 8, 6, 5, 4, 3, 2, 1}) {
+                    if (p->log && wpb > 4) continue;   // LOG instances: 256-thread blocks
                     const size_t tot = sh + wpb * stride;
                     if (tot > kLdsMax) continue;
-                    const int blocks = (int)std::min<size_t>(kLdsMax / tot, 16);
-                    const int waves = std::min(blocks * wpb, 16);   // VGPR-limited beyond
-                    const int score = waves * 4 + (W == 16 ? 1 : 0);
+                    // resident waves per CU: the runtime's occupancy for this instance
+                    // (VGPR/SGPR/LDS); without a device, the LDS bound capped at 16
+                    int blocks = rq_sweep_blocks_per_cu(spl, p->nK, c16, W, p->log, p->bits, wpb, tot);
+                    if (blocks <= 0) blocks = (int)std::min<size_t>(kLdsMax / tot, 16 / wpb);
+                    const int waves = blocks * wpb;
+                    const int score = waves * 4 + (W == 16 ? 1 : 0);   // W=16 refills half as often
                     if (score > best) {
                         best = score;
                         p->gwin = W; p->gwpb = wpb; p->gcol_lds = col_lds; p->gcol16 = c16;
@@ -454,7 +472,18 @@ int rq_graph_build(const rq_graph_desc* d, rq_graph_t* out)
         g->csr_ptr.push_back((int)g->csr_col.size());
     }
 
+    if (g->n_sinks <= kBitsMaxSinks) {
+        g->nw = (g->n_sinks + 31) / 32;
+        g->masks.assign((size_t)g->n_str * g->nw, 0u);
+        for (int j = 0; j < g->n_str; ++j)
+            for (int e = g->csr_ptr[j]; e < g->csr_ptr[j + 1]; ++e) {
+                const int c = g->csr_col[e];
+                g->masks[(size_t)j * g->nw + c / 32] |= 1u << (c % 32);
+            }
+    }
+
     int rc;
+    if (g->nw > 0 && (rc = g->d_mask.upload(g->masks))) return rc;
     if ((rc = g->d_src_id.upload(g->src_id)) || (rc = g->d_kind.upload(g->kind)) ||
         (rc = g->d_orig.upload(g->orig_idx)) || (rc = g->d_arr_off.upload(g->arr_off)) ||
         (rc = g->d_arr_n.upload(g->arr_n)) || (rc = g->d_csr_ptr.upload(g->csr_ptr)) ||
@@ -506,6 +535,23 @@ int rq_workspace_size(rq_graph_t g, const rq_batch_desc* b, size_t* bytes)
     const int rc = make_plan(g, b, &p);
     if (rc) return rc;
     *bytes = p.total;
+    return RQ_OK;
+}
+
+int rq_plan_info(rq_graph_t g, const rq_batch_desc* b, int64_t* info)
+{
+    if (!info) return RQ_EINVAL;
+    Plan p;
+    const int rc = make_plan(g, b, &p);
+    if (rc) return rc;
+    info[0] = p.log ? 1 : (p.bits ? 2 : 0);
+    info[1] = p.spl;
+    info[2] = p.gwin;
+    info[3] = p.gwpb;
+    info[4] = rq_sweep_blocks_per_cu(p.spl, p.nK, p.gcol16, p.gwin, p.log, p.bits, p.gwpb, p.g_total);
+    info[5] = p.gcol_lds;
+    info[6] = (int64_t)p.g_total;
+    info[7] = p.chunk;
     return RQ_OK;
 }
 
@@ -674,9 +720,13 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             sa.lds_rank_off = p.g_rank_off;
             sa.lds_win_off = p.g_win_off;
             sa.lds_x_off = p.g_x_off;
+            sa.lds_mask = p.g_col;   // BITS: the bitsets take the columns' place
+            sa.masks = g->d_mask.p;
+            sa.nw = g->nw;
+            if (const char* d = getenv("RQ_SWEEP_DBG")) sa.dbg = atoi(d);   // profiling only
             sa.lds_total = p.g_total;
             TimedLaunch tl(K_SWEEP, s);
-            if (rq_launch_sweep(sa, p.spl, p.nK, p.gcol16, p.log, s) != hipSuccess) return RQ_EHIP;
+            if (rq_launch_sweep(sa, p.spl, p.nK, p.gcol16, p.log, p.bits, s) != hipSuccess) return RQ_EHIP;
         }
 
         ScanArgs sc{};

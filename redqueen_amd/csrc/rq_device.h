@@ -114,6 +114,18 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
     return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
+// sum over the 64 lanes (same DPP pattern, adds; disabled rows add 0), via lane 63
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v)
+{
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 // order-preserving map of a double onto uint64 (negative values reversed)
 __device__ __forceinline__ uint64_t order_key(double t)
 {

@@ -28,6 +28,7 @@
 #include "rq_device.h"
 #include "rq_internal.h"
 #include "rq_sweep_core.h"
+#include <type_traits>
 
 #pragma clang fp contract(off)
 
@@ -183,8 +184,8 @@ __global__ __launch_bounds__(256) void rq_gen_streams(GenArgs a)
 //       (equal-time rows merged) are placed and stored by all lanes at once.
 //    LOG = the event log / max_events variant: phase C goes event by event.
 // ============================================================================
-template <int SPL, int NK, class COL, int W, bool LOG>
-__global__ __launch_bounds__(512) void rq_sweep(SweepArgs a)
+template <int SPL, int NK, class COL, int W, bool LOG, bool BITS>
+__global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
 {
     extern __shared__ double lds_g[];
     char* base = reinterpret_cast<char*>(lds_g);
@@ -198,8 +199,12 @@ __global__ __launch_bounds__(512) void rq_sweep(SweepArgs a)
     constexpr bool col_lds = sizeof(COL) == 2;
     COL* col_l = reinterpret_cast<COL*>(base + a.lds_col);
     const int* col_g = a.csr_col;
-    if (col_lds)
+    if (col_lds && !BITS)
         for (int e = threadIdx.x; e < a.n_csr; e += blockDim.x) col_l[e] = (COL)a.csr_col[e];
+    // BITS: per-stream sink bitsets instead of the columns
+    uint32_t* msk = reinterpret_cast<uint32_t*>(base + a.lds_mask);
+    if (BITS)
+        for (int e = threadIdx.x; e < a.n_str * a.nw; e += blockDim.x) msk[e] = a.masks[e];
     for (int j = threadIdx.x; j <= a.n_str; j += blockDim.x) cptr[j] = a.csr_ptr[j];
     for (int j = threadIdx.x; j < a.n_str; j += blockDim.x) {
         odf[j] = a.outdeg_f[j];
@@ -212,10 +217,14 @@ __global__ __launch_bounds__(512) void rq_sweep(SweepArgs a)
     const int g = (int)(i / a.n_rep);
     char* wb = base + a.lds_wave + (size_t)w * a.lds_wave_stride;
     double* invc = reinterpret_cast<double*>(wb);
-    int* rank = reinterpret_cast<int*>(wb + a.lds_rank_off);
+    // ranks: exact int for the LOG variant (pivot cells average them); the fast
+    // sweep only compares them with K-1, so int16 saturating at 32767 is exact
+    using RT = typename std::conditional<LOG, int, int16_t>::type;
+    RT* rank = reinterpret_cast<RT*>(wb + a.lds_rank_off);
     double* win = reinterpret_cast<double*>(wb + a.lds_win_off);
     for (int j = lane; j < a.n_str; j += 64) invc[j] = a.inv_c[(int64_t)g * a.n_str + j];
-    for (int c = lane; c < a.n_sinks; c += 64) rank[c] = -1;   // NaN: no row yet
+    if (!BITS)
+        for (int c = lane; c < a.n_sinks; c += 64) rank[c] = -1;   // NaN: no row yet
     __syncthreads();
     if (!live) return;
 
@@ -276,6 +285,8 @@ __global__ __launch_bounds__(512) void rq_sweep(SweepArgs a)
 
     Agg<NK> ag;
     ag.init(a.Ks);
+    AggB agb;
+    if (BITS) agb.init(msk, a.nw, a.ctrl_idx, lane);
     RowStage<NK> rs;
     const int64_t rbase = rl * a.cap_rows;
     rs.init(a.rows_t + rbase, a.rows_sum + rbase, a.rows_valid + rbase, a.rows_cnt + rbase * NK,
@@ -293,7 +304,7 @@ __global__ __launch_bounds__(512) void rq_sweep(SweepArgs a)
     if (LOG) {
         int* xs = reinterpret_cast<int*>(wb + a.lds_x_off);
         xlds = reinterpret_cast<double*>(wb + a.lds_x_off + 12 * (size_t)a.n_sinks_pad);
-        ax.init(a.Ks, rank, xs, a.n_sinks_pad, a.n_sinks, lane);
+        ax.init(a.Ks, reinterpret_cast<int*>(rank), xs, a.n_sinks_pad, a.n_sinks, lane);
     }
     auto close_row = [&]() -> bool {
         pend = false;
@@ -386,7 +397,7 @@ __global__ __launch_bounds__(512) void rq_sweep(SweepArgs a)
         //  first); a post resets the min.  One prefix-min per post.
         uint64_t ownm = 0;
         double ot = RQ_INF;
-        if (opt) {
+        if (opt && a.dbg != 3) {
             double c = RQ_INF;
             bool cb = false;
             if (act) {
@@ -443,6 +454,8 @@ __global__ __launch_bounds__(512) void rq_sweep(SweepArgs a)
                     break;
                 }
             }
+        } else if (a.dbg == 1) {
+            n_events += n;
         } else {
             const bool own_b = act && ((ownm >> lane) & 1ull);     // controller post before #lane
             const bool strm_own = act && !opt && tj == a.ctrl_idx;  // controlled stream's arrival
@@ -455,7 +468,31 @@ __global__ __launch_bounds__(512) void rq_sweep(SweepArgs a)
             int ocnt[NK], wcnt[NK];
 #pragma unroll
             for (int kq = 0; kq < NK; ++kq) ocnt[kq] = wcnt[kq] = 0;
-            for (int q = 0; q < n; ++q) {
+            if (BITS) {
+                const int deg = e1 - e0;
+                for (int q = 0; q < n; ++q) {
+                    if ((ownm >> q) & 1ull) {
+                        agb.own();
+                        agb.sync();
+                        if (lane == q) {
+                            osum = agb.sumR;
+                            oval = agb.nvalid;
+                            ocnt[0] = agb.cnt[0];
+                        }
+                    }
+                    const int jw = bcast_i(tj, q);
+                    if (!opt && jw == a.ctrl_idx)
+                        agb.own();
+                    else
+                        agb.wall(jw, bcast_i(deg, q), bcast_i(od, q), lane);
+                    agb.sync();
+                    if (lane == q) {
+                        wsum = agb.sumR;
+                        wval = agb.nvalid;
+                        wcnt[0] = agb.cnt[0];
+                    }
+                }
+            } else for (int q = 0; q < n; ++q) {
                 if ((ownm >> q) & 1ull) {
                     ag.own(rank, folat, a.n_fol, lane);
                     if (lane == q) {
@@ -468,7 +505,7 @@ __global__ __launch_bounds__(512) void rq_sweep(SweepArgs a)
                 const int jw = bcast_i(tj, q);
                 if (!opt && jw == a.ctrl_idx)
                     ag.own(rank, folat, a.n_fol, lane);
-                else
+                else if (a.dbg != 2)
                     ag.wall(rank, colat, bcast_i(e0, q), bcast_i(e1, q), bcast_i(od, q), lane);
                 if (lane == q) {
                     wsum = ag.sumR;
@@ -531,7 +568,15 @@ __global__ __launch_bounds__(512) void rq_sweep(SweepArgs a)
             event(opt_next, true, 0, 0, 0);
         } else {
             ++n_events;
-            ag.own(rank, folat, a.n_fol, lane);
+            if (BITS) {
+                agb.own();
+                agb.sync();
+                ag.sumR = agb.sumR;
+                ag.nvalid = agb.nvalid;
+                ag.cnt[0] = agb.cnt[0];
+            } else {
+                ag.own(rank, folat, a.n_fol, lane);
+            }
             if (a.n_fol > 0) {
                 ++posts;
                 int64_t rr = rs.nrow;
@@ -557,6 +602,10 @@ __global__ __launch_bounds__(512) void rq_sweep(SweepArgs a)
         }
     }
     if (LOG && pend) close_row();
+    if (BITS) {
+        agb.sync();
+        ag.nvalid = agb.nvalid;
+    }
     rs.flush(lane);
     if (LOG && a.ev_t) es.flush(lane);
     if (lane == 0) {
@@ -565,7 +614,7 @@ __global__ __launch_bounds__(512) void rq_sweep(SweepArgs a)
         cnto[1] = world;
         cnto[2] = n_events;
         cnto[3] = rs.nrow;
-        a.sall[rl] = LOG ? ax.nvalid : ag.nvalid;
+        a.sall[rl] = LOG ? ax.nvalid : ag.nvalid;   // BITS: synced below
         if (rs.nrow == 0) status |= RQ_ST_EMPTY;
         if (status) atomicOr(&a.status[o], status);
     }
@@ -851,11 +900,11 @@ __global__ __launch_bounds__(64) void rq_replay(ReplayArgs a)
 // ============================================================================
 // launch wrappers
 // ============================================================================
-template <int SPL, int NK, class COL, int W, bool LOG>
+template <int SPL, int NK, class COL, int W, bool LOG, bool BITS = false>
 static hipError_t launch_sweep_t(const SweepArgs& a, hipStream_t s)
 {
     const unsigned blocks = (unsigned)((a.n_chunk + a.wpb - 1) / a.wpb);
-    hipLaunchKernelGGL((rq_sweep<SPL, NK, COL, W, LOG>), dim3(blocks), dim3(64 * a.wpb), a.lds_total, s, a);
+    hipLaunchKernelGGL((rq_sweep<SPL, NK, COL, W, LOG, BITS>), dim3(blocks), dim3(64 * a.wpb), a.lds_total, s, a);
     return hipGetLastError();
 }
 
@@ -871,8 +920,11 @@ static hipError_t launch_sweep_k(const SweepArgs& a, int nK, hipStream_t s)
 }
 
 template <int SPL>
-static hipError_t launch_sweep_c(const SweepArgs& a, int nK, int col16, hipStream_t s)
+static hipError_t launch_sweep_c(const SweepArgs& a, int nK, int col16, int bits, hipStream_t s)
 {
+    if (bits)   // K = 1 on sink bitsets
+        return a.win == 16 ? launch_sweep_t<SPL, 1, uint16_t, 16, false, true>(a, s)
+                           : launch_sweep_t<SPL, 1, uint16_t, 8, false, true>(a, s);
     if (a.win == 16)
         return col16 ? launch_sweep_k<SPL, uint16_t, 16, false>(a, nK, s)
                      : launch_sweep_k<SPL, int, 16, false>(a, nK, s);
@@ -888,7 +940,7 @@ hipError_t rq_launch_gen(const GenArgs& a, hipStream_t s)
     return hipGetLastError();
 }
 
-hipError_t rq_launch_sweep(const SweepArgs& a, int spl, int nK, int col16, int log, hipStream_t s)
+hipError_t rq_launch_sweep(const SweepArgs& a, int spl, int nK, int col16, int log, int bits, hipStream_t s)
 {
     if (a.n_chunk <= 0) return hipSuccess;
     // event log / max_events: the sequential variant, eight sources per lane, W = 8
@@ -896,10 +948,51 @@ hipError_t rq_launch_sweep(const SweepArgs& a, int spl, int nK, int col16, int l
         return col16 ? launch_sweep_k<8, uint16_t, 8, true>(a, nK, s)
                      : launch_sweep_k<8, int, 8, true>(a, nK, s);
     switch (spl) {
-    case 1: return launch_sweep_c<1>(a, nK, col16, s);
-    case 2: return launch_sweep_c<2>(a, nK, col16, s);
-    case 4: return launch_sweep_c<4>(a, nK, col16, s);
-    default: return launch_sweep_c<8>(a, nK, col16, s);
+    case 1: return launch_sweep_c<1>(a, nK, col16, bits, s);
+    case 2: return launch_sweep_c<2>(a, nK, col16, bits, s);
+    case 4: return launch_sweep_c<4>(a, nK, col16, bits, s);
+    default: return launch_sweep_c<8>(a, nK, col16, bits, s);
+    }
+}
+
+// blocks of 64*wpb threads per CU the chosen sweep instance reaches with `lds`
+// bytes of dynamic LDS (VGPR, SGPR and LDS limits all applied by the runtime)
+template <int SPL, int NK, class COL, int W, bool LOG, bool BITS = false>
+static int occ_t(int wpb, size_t lds)
+{
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rq_sweep<SPL, NK, COL, W, LOG, BITS>, 64 * wpb,
+                                                      lds) != hipSuccess)
+        return 0;
+    return nb;
+}
+template <int SPL, class COL, int W, bool LOG>
+static int occ_k(int nK, int wpb, size_t lds)
+{
+    switch (nK) {
+    case 1: return occ_t<SPL, 1, COL, W, LOG>(wpb, lds);
+    case 2: return occ_t<SPL, 2, COL, W, LOG>(wpb, lds);
+    case 3: return occ_t<SPL, 3, COL, W, LOG>(wpb, lds);
+    default: return occ_t<SPL, 4, COL, W, LOG>(wpb, lds);
+    }
+}
+template <int SPL>
+static int occ_c(int nK, int col16, int W, int bits, int wpb, size_t lds)
+{
+    if (bits)
+        return W == 16 ? occ_t<SPL, 1, uint16_t, 16, false, true>(wpb, lds)
+                       : occ_t<SPL, 1, uint16_t, 8, false, true>(wpb, lds);
+    if (W == 16) return col16 ? occ_k<SPL, uint16_t, 16, false>(nK, wpb, lds) : occ_k<SPL, int, 16, false>(nK, wpb, lds);
+    return col16 ? occ_k<SPL, uint16_t, 8, false>(nK, wpb, lds) : occ_k<SPL, int, 8, false>(nK, wpb, lds);
+}
+int rq_sweep_blocks_per_cu(int spl, int nK, int col16, int W, int log, int bits, int wpb, size_t lds)
+{
+    if (log) return col16 ? occ_k<8, uint16_t, 8, true>(nK, wpb, lds) : occ_k<8, int, 8, true>(nK, wpb, lds);
+    switch (spl) {
+    case 1: return occ_c<1>(nK, col16, W, bits, wpb, lds);
+    case 2: return occ_c<2>(nK, col16, W, bits, wpb, lds);
+    case 4: return occ_c<4>(nK, col16, W, bits, wpb, lds);
+    default: return occ_c<8>(nK, col16, W, bits, wpb, lds);
     }
 }
 

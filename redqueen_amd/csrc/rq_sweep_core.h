@@ -33,8 +33,8 @@ struct Agg {
     }
     // other source's event: sinks colat(e0..e1) in edge-list order (distinct).
     // Two 64-sink tiles per round so their LDS latencies overlap.
-    template <class CF>
-    __device__ __forceinline__ void wall(int* rank, CF&& colat, int e0, int e1, int odf, int lane)
+    template <class RT, class CF>
+    __device__ __forceinline__ void wall(RT* rank, CF&& colat, int e0, int e1, int odf, int lane)
     {
         int dvalid = 0;
         int dle[NK];
@@ -45,10 +45,11 @@ struct Agg {
             const bool acta = ea < e1, actb = eb < e1;
             const int ca = acta ? colat(ea) : 0;
             const int cb = actb ? colat(eb) : 0;
-            const int ra = acta ? rank[ca] : 0;
-            const int rb = actb ? rank[cb] : 0;
-            if (acta) rank[ca] = ra < 0 ? 1 : ra + 1;
-            if (actb) rank[cb] = rb < 0 ? 1 : rb + 1;
+            const int ra = acta ? (int)rank[ca] : 0;
+            const int rb = actb ? (int)rank[cb] : 0;
+            constexpr int kSat = sizeof(RT) == 2 ? 32767 : 0x7FFFFFFF;   // saturating (K <= 32767)
+            if (acta) rank[ca] = (RT)(ra < 0 ? 1 : (ra < kSat ? ra + 1 : ra));
+            if (actb) rank[cb] = (RT)(rb < 0 ? 1 : (rb < kSat ? rb + 1 : rb));
             const bool inva = acta && ra < 0, invb = actb && rb < 0;
             dvalid += popc(__ballot(inva)) + popc(__ballot(invb));
 #pragma unroll
@@ -64,8 +65,8 @@ struct Agg {
         sumF += odf;
     }
     // own post: every follower's rank -> 0 (State.apply_event, opt_model.py:71-72)
-    template <class CF>
-    __device__ __forceinline__ void own(int* rank, CF&& folat, int F, int lane)
+    template <class RT, class CF>
+    __device__ __forceinline__ void own(RT* rank, CF&& folat, int F, int lane)
     {
         int dvalid = 0;
         int dle[NK];
@@ -77,18 +78,65 @@ struct Agg {
             int r = 0, c = 0;
             if (act) {
                 c = folat(f);
-                r = rank[c];
+                r = (int)rank[c];
             }
             dvalid += popc(__ballot(act && r < 0));
 #pragma unroll
             for (int q = 0; q < NK; ++q) dle[q] -= popc(__ballot(act && r >= 0 && r <= km1[q]));
-            if (act) rank[c] = 0;
+            if (act) rank[c] = (RT)0;
         }
 #pragma unroll
         for (int q = 0; q < NK; ++q) cnt[q] += dle[q] + (0 <= km1[q] ? F : 0);
         nvalid += dvalid;
         sumR -= sumF;
         sumF = 0;
+    }
+};
+
+// K = 1 aggregates on sink bitsets (n_sinks <= 2048): lane w holds word w of
+//   T = valid sinks with rank 0 (the top-1 set) and V = sinks with a row.
+// A wall event of source j with follower word m: V |= m, T &= ~m (NaN -> 1 and
+// 0 -> 1 both leave / stay out of the top); a post: T |= F, V |= F.  Counts
+// come from one DPP wave sum of popc(T) | popc(V) << 16; sumR/sumF as in Agg.
+struct AggB {
+    int64_t sumR, sumF;
+    int nvalid;
+    int cnt[1];
+    uint32_t T, V, F;
+    const uint32_t* M;   // LDS [n_str][nw]
+    int nw;
+    __device__ __forceinline__ void init(const uint32_t* M_, int nw_, int ctrl_idx, int lane)
+    {
+        sumR = 0;
+        sumF = 0;
+        nvalid = 0;
+        cnt[0] = 0;
+        T = 0u;
+        V = 0u;
+        M = M_;
+        nw = nw_;
+        F = lane < nw ? M[ctrl_idx * nw + lane] : 0u;
+    }
+    __device__ __forceinline__ void wall(int j, int deg, int odf, int lane)
+    {
+        const uint32_t m = lane < nw ? M[j * nw + lane] : 0u;
+        V |= m;
+        T &= ~m;
+        sumR += deg;
+        sumF += odf;
+    }
+    __device__ __forceinline__ void own()
+    {
+        T |= F;
+        V |= F;
+        sumR -= sumF;
+        sumF = 0;
+    }
+    __device__ __forceinline__ void sync()
+    {
+        const uint32_t tot = wave_sum_u32((uint32_t)__popc(T) | ((uint32_t)__popc(V) << 16));
+        cnt[0] = (int)(tot & 0xFFFFu);
+        nvalid = (int)(tot >> 16);
     }
 };
 

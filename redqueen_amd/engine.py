@@ -135,7 +135,8 @@ class Graph:
 
     def run(self, ctrl="opt", q=1.0, s=None, n_rep=1, ctrl_seed=0, world_seed=0,
             randomize=False, seed_mod=0, ctrl_rate=None, Ks=(1,), max_events=None,
-            event_log=False, cap_scale=1.0, chunk=0, stream=None, check=True, sweep_mode=0, replica0=0, n_local=0):
+            event_log=False, cap_scale=1.0, chunk=0, stream=None, check=True, sweep_mode=0, replica0=0, n_local=0,
+            plan_only=False):
         """Enqueue one batch.  ``q``: scalar or [n_grid]; ``s``: per grid point
         row(s) over the sorted followers ([n_grid, F]) or anything ``s_matrix``
         takes.  Seeds: int base (seed + replica id) or a device uint32 tensor."""
@@ -199,6 +200,12 @@ class Graph:
         b.replica0 = int(replica0)
         b.n_local = int(n_local)
         lib = L.lib()
+        if plan_only:
+            info = (C.c_int64 * 8)()
+            L.check("rq_plan_info", lib.rq_plan_info(self._h, C.byref(b), info))
+            keys = ("variant", "sources_per_lane", "ring_depth", "waves_per_block",
+                    "blocks_per_cu", "columns_in_lds", "lds_bytes_per_block", "chunk")
+            return dict(zip(keys, (int(v) for v in info)))
         while True:
             nbytes = C.c_size_t()
             L.check("rq_workspace_size", lib.rq_workspace_size(self._h, C.byref(b), C.byref(nbytes)))
@@ -229,7 +236,7 @@ class Graph:
             if not ovf:
                 # equal event times in the fast tiled sweep: redo with the exact sequential
                 # sweep (never taken by continuous-time worlds; RealData runs are exact already)
-                seq = (event_log or b.max_events >= 0 or b.sweep_mode != 0 or self.has_realdata
+                seq = (event_log or b.max_events >= 0 or b.sweep_mode in (1, 2) or self.has_realdata
                        or ck == L.SRC_REALDATA)
                 if not seq and int((status & L.ST_TIE).any().item()):
                     b.sweep_mode = 2

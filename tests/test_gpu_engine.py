@@ -42,13 +42,16 @@ def _oracle(O, so, ctrl, Ks, max_events=None):
     return met, t, s
 
 
-MODES = ["fast", "log"]
+MODES = ["fast", "scatter", "log"]
 
 
 def _mode_kw(mode):
-    """fast: the tiled sweep with vectorised row placement (no event log);
-    log: the sequential event-log variant (sweep_mode=2), events compared too."""
-    return dict(event_log=True, sweep_mode=2) if mode == "log" else dict(event_log=False)
+    """fast: the tiled sweep (K=1 runs on sink bitsets); scatter: the tiled sweep
+    with per-sink LDS ranks (sweep_mode=3); log: the sequential event-log variant
+    (sweep_mode=2), events compared too."""
+    if mode == "log":
+        return dict(event_log=True, sweep_mode=2)
+    return dict(event_log=False, sweep_mode=3 if mode == "scatter" else 0)
 
 
 def _cmp_replica(res, i, met_o, t_o, s_o, Ks):
@@ -172,9 +175,14 @@ def test_large_batch_no_overflow_and_determinism():
               randomize=True, Ks=(1,), chunk=300)
     c = g.run("opt", q=so["q"], s=so["s"], n_rep=2048, ctrl_seed=0, world_seed=0,
               randomize=True, Ks=(1,), sweep_mode=2)
+    d = g.run("opt", q=so["q"], s=so["s"], n_rep=2048, ctrl_seed=0, world_seed=0,
+              randomize=True, Ks=(1,), sweep_mode=3)
+    assert g.run("opt", q=so["q"], s=so["s"], n_rep=2048, Ks=(1,), plan_only=True)["variant"] == 2
     assert torch.equal(a.metrics, b.metrics) and torch.equal(a.counts, b.counts)
-    # the tiled fast sweep and the sequential event-log variant are the same machine
+    # the bitset sweep, the sequential event-log variant and the rank-scatter sweep
+    # are the same machine
     assert torch.equal(a.metrics, c.metrics) and torch.equal(a.counts, c.counts)
+    assert torch.equal(a.metrics, d.metrics) and torch.equal(a.counts, d.counts)
     assert int(a.status.sum().item()) == 0
     ev = a.n_events.double().mean().item()
     assert 4800 < ev < 6200, ev
@@ -226,8 +234,7 @@ def test_fast_sweep_equal_times_disjoint_sinks():
                                  ("Poisson", {"src_id": 4, "seed": 5, "rate": 2.0})],
               edge_list=[(1, 10), (1, 11), (2, 10), (3, 12), (4, 11)])
     g = _graph(engine, so)
-    Ks = (1, 2)
-    for seed in (1, 2, 3, 4):
+    for seed, Ks in [(1, (1, 2)), (2, (1, 2)), (3, (1,)), (4, (1,))]:   # (1,): bitset variant
         res = g.run("opt", q=so["q"], s=so["s"], n_rep=1, ctrl_seed=seed, Ks=Ks, sweep_mode=1)
         assert int(res.status[0].item()) & 4   # the ties were seen
         met_o, t_o, s_o = _oracle(O, so, ("opt", seed), Ks)
