@@ -126,6 +126,26 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v)
     return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
+// N independent 64-lane sums interleaved stage by stage (so the DPP read-after-
+// write hazards of one chain are covered by the others); totals end in lane 63
+template <int N>
+__device__ __forceinline__ void wave_sum_u32_n(uint32_t (&v)[N])
+{
+#define RQ_SUM_STAGE(CTRL, RM)                                                                   \
+    _Pragma("unroll") for (int k = 0; k < N; ++k) v[k] +=                                       \
+        (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[k], CTRL, RM, 0xF, false);
+    RQ_SUM_STAGE(0xB1, 0xF)
+    RQ_SUM_STAGE(0x4E, 0xF)
+    RQ_SUM_STAGE(0x141, 0xF)
+    RQ_SUM_STAGE(0x140, 0xF)
+    RQ_SUM_STAGE(0x142, 0xA)
+    RQ_SUM_STAGE(0x143, 0xC)
+#undef RQ_SUM_STAGE
+}
+
+// v into lane l (v, l uniform): v_cmp + v_cndmask
+__device__ __forceinline__ int writelane(int old, int v, int l) { return lane_id() == l ? v : old; }
+
 // order-preserving map of a double onto uint64 (negative values reversed)
 __device__ __forceinline__ uint64_t order_key(double t)
 {

@@ -469,29 +469,54 @@ __global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
 #pragma unroll
             for (int kq = 0; kq < NK; ++kq) ocnt[kq] = wcnt[kq] = 0;
             if (BITS) {
+                // batches of 8 events: follower words loaded up front, the 8 wave
+                // sums interleaved; aggregates land in lane q via v_writelane
                 const int deg = e1 - e0;
-                for (int q = 0; q < n; ++q) {
-                    if ((ownm >> q) & 1ull) {
-                        agb.own();
-                        agb.sync();
-                        if (lane == q) {
-                            osum = agb.sumR;
-                            oval = agb.nvalid;
-                            ocnt[0] = agb.cnt[0];
+                int wsl = 0, wsh = 0, osl = 0, osh = 0, oc0 = 0, wc0 = 0;
+                for (int q0 = 0; q0 < n; q0 += 8) {
+                    uint32_t m[8], pk[8];
+                    int jk[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        jk[k] = bcast_i(tj, q0 + k < n ? q0 + k : n - 1);
+                        m[k] = lane < agb.nw ? agb.M[jk[k] * agb.nw + lane] : 0u;
+                    }
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const int q = q0 + k;
+                        pk[k] = 0u;
+                        if (q < n) {
+                            if ((ownm >> q) & 1ull) {
+                                agb.own();
+                                agb.sync();
+                                osl = writelane(osl, (int)(uint32_t)agb.sumR, q);
+                                osh = writelane(osh, (int)(agb.sumR >> 32), q);
+                                oval = writelane(oval, agb.nvalid, q);
+                                oc0 = writelane(oc0, agb.cnt[0], q);
+                            }
+                            if (!opt && jk[k] == a.ctrl_idx)
+                                agb.own();
+                            else
+                                agb.wall_m(m[k], bcast_i(deg, q), bcast_i(od, q));
+                            pk[k] = agb.packed();
+                            wsl = writelane(wsl, (int)(uint32_t)agb.sumR, q);
+                            wsh = writelane(wsh, (int)(agb.sumR >> 32), q);
                         }
                     }
-                    const int jw = bcast_i(tj, q);
-                    if (!opt && jw == a.ctrl_idx)
-                        agb.own();
-                    else
-                        agb.wall(jw, bcast_i(deg, q), bcast_i(od, q), lane);
-                    agb.sync();
-                    if (lane == q) {
-                        wsum = agb.sumR;
-                        wval = agb.nvalid;
-                        wcnt[0] = agb.cnt[0];
+                    wave_sum_u32_n<8>(pk);
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        if (q0 + k < n) {
+                            const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)pk[k], 63);
+                            wval = writelane(wval, (int)(tot >> 16), q0 + k);
+                            wc0 = writelane(wc0, (int)(tot & 0xFFFFu), q0 + k);
+                        }
                     }
                 }
+                wsum = (int64_t)(((uint64_t)(uint32_t)wsh << 32) | (uint32_t)wsl);
+                osum = (int64_t)(((uint64_t)(uint32_t)osh << 32) | (uint32_t)osl);
+                wcnt[0] = wc0;
+                ocnt[0] = oc0;
             } else for (int q = 0; q < n; ++q) {
                 if ((ownm >> q) & 1ull) {
                     ag.own(rank, folat, a.n_fol, lane);

@@ -125,6 +125,18 @@ struct AggB {
         sumR += deg;
         sumF += odf;
     }
+    // wall event with this lane's follower word already loaded
+    __device__ __forceinline__ void wall_m(uint32_t m, int deg, int odf)
+    {
+        V |= m;
+        T &= ~m;
+        sumR += deg;
+        sumF += odf;
+    }
+    __device__ __forceinline__ uint32_t packed() const
+    {
+        return (uint32_t)__popc(T) | ((uint32_t)__popc(V) << 16);
+    }
     __device__ __forceinline__ void own()
     {
         T |= F;
