@@ -141,7 +141,10 @@ typedef struct rq_batch_desc {
     int32_t sweep_mode;          /* 0 auto: fast tiled sweep unless the run needs the sequential
                                     one (event log, max_events, RealData); 1 fast whenever the
                                     event log / max_events allow; 2 force the sequential sweep;
-                                    3 as 0 but never the K=1 sink-bitset variant             */
+                                    3 as 0 but never the K=1 sink-bitset variant;
+                                    4 / 5 as 0 / 1 on the legacy kernels (arrival streams
+                                    pre-generated into HBM by rq_gen_streams, serial wave-min
+                                    merge) -- kept for A/B parity checks of the fused sweep  */
                                  /* sweep; both are bit-identical, auto picks the faster one    */
 } rq_batch_desc;
 

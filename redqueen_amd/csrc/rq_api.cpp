@@ -124,10 +124,13 @@ struct Plan {
     std::vector<int64_t> st_off;
     // sequential (event log / max_events) sweep variant; K=1 sink-bitset variant
     bool log = false, bits = false;
+    // fused windowed sweep (n_str <= 64): arrivals generated in-kernel, window depth fw_h
+    bool fw = false;
+    int fw_h = 8, mstride = 1;
     // general sweep LDS layout
     int gwpb = 4, gwin = 16, gcol_lds = 1, gcol16 = 0;
     size_t g_col = 0, g_ptr = 0, g_odf = 0, g_cbf = 0, g_wave = 0, g_wave_stride = 0, g_rank_off = 0,
-           g_win_off = 0, g_x_off = 0, g_total = 0;
+           g_win_off = 0, g_x_off = 0, g_total = 0, g_stage_off = 0;
     size_t tables_bytes = 0;
     size_t off_invc = 0, off_streams = 0, off_slen = 0, off_rt = 0, off_rs = 0, off_rv = 0,
            off_rc = 0, off_sall = 0, off_stoff = 0, off_cap = 0,
@@ -239,12 +242,13 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     bool has_rd = b->ctrl_kind == RQ_SRC_REALDATA;
     for (int k : g->kind) has_rd = has_rd || k == RQ_SRC_REALDATA;
     p->log = (b->flags & RQ_RUN_EVENT_LOG) || b->max_events >= 0 || b->sweep_mode == 2 ||
-             (has_rd && b->sweep_mode != 1);
+             (has_rd && b->sweep_mode != 1 && b->sweep_mode != 5);
     for (int q = 0; q < b->nK; ++q) p->log = p->log || b->Ks[q] > 32767;   // int16 ranks
     if (p->log) p->spl = 8;
 
+    p->mstride = g->nw | 1;   // odd row stride: one LDS bank per stream for a given word
     p->bits = !p->log && p->nK == 1 && b->Ks[0] == 1 && g->nw > 0 && b->sweep_mode != 3 &&
-              (size_t)g->n_str * g->nw * 4 <= 64 * 1024;
+              (size_t)g->n_str * p->mstride * 4 <= 64 * 1024;
     if (p->bits) p->spl = g->n_str <= 64 ? 1 : g->n_str <= 128 ? 2 : g->n_str <= 256 ? 4 : 8;
 
     // general sweep: pick (ring depth W, waves per block) for the most waves per CU
@@ -255,7 +259,7 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
         for (int col_lds = g->n_sinks <= 65535 ? 1 : 0; col_lds >= 0 && best < 0; --col_lds) {
             const int c16 = col_lds;
             // BITS: sink bitsets [n_str][nw] replace the columns (and the per-wave ranks)
-            const size_t colb = p->bits ? 4 * (size_t)g->n_str * g->nw
+            const size_t colb = p->bits ? 4 * (size_t)g->n_str * p->mstride
                                         : (col_lds ? 2 * g->csr_col.size() : 0);
             size_t sh = 0;
             const size_t o_col = sh;  sh = align_up(sh + colb, 16);
@@ -296,6 +300,47 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
         if (best < 0) return RQ_EUNSUPPORTED;
     }
 
+    // fused windowed sweep: one stream per lane, rings of W arrivals generated in LDS,
+    // a window of H per ring in registers; (W, H, waves per block) for the most waves per CU
+    p->fw = !p->log && g->n_str <= 64 && b->sweep_mode != 4 && b->sweep_mode != 5;
+    if (p->fw) {
+        int best = -1;
+        const int c16 = p->bits ? 1 : (g->n_sinks <= 65535 ? 1 : 0);
+        const size_t colb = p->bits ? 4 * (size_t)g->n_str * p->mstride
+                                    : (c16 ? 2 * g->csr_col.size() : 0);
+        size_t sh = 0;
+        const size_t o_col = sh;  sh = align_up(sh + colb, 16);
+        const size_t o_ptr = sh;  sh = align_up(sh + 4 * (g->n_str + 1), 16);
+        const size_t o_odf = sh;  sh = align_up(sh + 4 * g->n_str, 16);
+        const size_t o_cbf = sh;  sh = align_up(sh + 4 * g->n_str, 16);
+        int only_w = 0;
+        if (const char* e = getenv("RQ_FW_W")) only_w = atoi(e);   // tuning only
+        for (int W : {16, 8}) {
+            if (only_w && W != only_w) continue;
+            const int H = W / 2;
+            const size_t r_off = align_up(8 * (size_t)g->n_str, 16);
+            const size_t w_off = align_up(r_off + (p->bits ? 0 : 2 * (size_t)p->n_sinks_pad), 16);
+            const size_t s_off = align_up(w_off + 8 * (size_t)g->n_str * (W + 1), 16);
+            const size_t stride = align_up(s_off + 64 * 12, 16);
+            for (int wpb : {16, 12, 10, 8, 6, 5, 4, 3, 2, 1}) {
+                const size_t tot = sh + wpb * stride;
+                if (tot > kLdsMax) continue;
+                int blocks = rq_fw_blocks_per_cu(p->nK, c16, W, p->bits, wpb, tot);
+                if (blocks <= 0) blocks = (int)std::min<size_t>(kLdsMax / tot, 16 / wpb);
+                const int waves = blocks * wpb;
+                const int score = waves * 4 + (W == 16 ? 1 : 0);
+                if (score > best) {
+                    best = score;
+                    p->gwin = W; p->fw_h = H; p->gwpb = wpb; p->gcol_lds = c16; p->gcol16 = c16;
+                    p->g_col = o_col; p->g_ptr = o_ptr; p->g_odf = o_odf; p->g_cbf = o_cbf;
+                    p->g_wave = sh; p->g_wave_stride = stride; p->g_rank_off = r_off;
+                    p->g_win_off = w_off; p->g_stage_off = s_off; p->g_x_off = 0; p->g_total = tot;
+                }
+            }
+        }
+        if (best < 0) p->fw = false;
+    }
+
     const size_t A = 256;
     const int64_t C = p->chunk;
     size_t o = 0;
@@ -304,8 +349,9 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     p->off_cap = o;     o = o + sizeof(int) * g->n_str;
     p->tables_bytes = o;
     o = align_up(o, A);
-    p->off_streams = o; o = align_up(o + sizeof(double) * (size_t)C * p->capsum, A);
-    p->off_slen = o;    o = align_up(o + sizeof(int) * (size_t)C * g->n_str, A);
+    const int64_t strm = p->fw ? 0 : C;   // the fused sweep keeps its arrivals in LDS
+    p->off_streams = o; o = align_up(o + sizeof(double) * (size_t)strm * p->capsum, A);
+    p->off_slen = o;    o = align_up(o + sizeof(int) * (size_t)strm * g->n_str, A);
     p->off_rt = o;      o = align_up(o + sizeof(double) * (size_t)C * p->cap_rows, A);
     p->off_rs = o;      o = align_up(o + sizeof(double) * (size_t)C * p->cap_rows, A);
     p->off_rv = o;      o = align_up(o + sizeof(uint32_t) * (size_t)C * p->cap_rows, A);
@@ -544,11 +590,12 @@ int rq_plan_info(rq_graph_t g, const rq_batch_desc* b, int64_t* info)
     Plan p;
     const int rc = make_plan(g, b, &p);
     if (rc) return rc;
-    info[0] = p.log ? 1 : (p.bits ? 2 : 0);
+    info[0] = (p.log ? 1 : (p.bits ? 2 : 0)) + (p.fw ? 10 : 0);
     info[1] = p.spl;
     info[2] = p.gwin;
     info[3] = p.gwpb;
-    info[4] = rq_sweep_blocks_per_cu(p.spl, p.nK, p.gcol16, p.gwin, p.log, p.bits, p.gwpb, p.g_total);
+    info[4] = p.fw ? rq_fw_blocks_per_cu(p.nK, p.gcol16, p.gwin, p.bits, p.gwpb, p.g_total)
+                   : rq_sweep_blocks_per_cu(p.spl, p.nK, p.gcol16, p.gwin, p.log, p.bits, p.gwpb, p.g_total);
     info[5] = p.gcol_lds;
     info[6] = (int64_t)p.g_total;
     info[7] = p.chunk;
@@ -658,7 +705,7 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
         ga.streams = (double*)(ws + p.off_streams);
         ga.slen = (int*)(ws + p.off_slen);
         ga.status = out->status;
-        {
+        if (!p.fw) {
             TimedLaunch tl(K_GEN, s);
             if (rq_launch_gen(ga, s) != hipSuccess) return RQ_EHIP;
         }
@@ -723,10 +770,15 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             sa.lds_mask = p.g_col;   // BITS: the bitsets take the columns' place
             sa.masks = g->d_mask.p;
             sa.nw = g->nw;
+            sa.mstride = p.mstride;
             if (const char* d = getenv("RQ_SWEEP_DBG")) sa.dbg = atoi(d);   // profiling only
             sa.lds_total = p.g_total;
+            sa.lds_stage_off = p.g_stage_off;
+            sa.gen = ga;
             TimedLaunch tl(K_SWEEP, s);
-            if (rq_launch_sweep(sa, p.spl, p.nK, p.gcol16, p.log, p.bits, s) != hipSuccess) return RQ_EHIP;
+            const hipError_t e = p.fw ? rq_launch_sweep_fw(sa, p.nK, p.gcol16, p.gwin, p.bits, s)
+                                      : rq_launch_sweep(sa, p.spl, p.nK, p.gcol16, p.log, p.bits, s);
+            if (e != hipSuccess) return RQ_EHIP;
         }
 
         ScanArgs sc{};

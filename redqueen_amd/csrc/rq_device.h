@@ -92,6 +92,21 @@ __device__ __forceinline__ int bcast_i(int v, int src_lane)
     return __builtin_amdgcn_readlane(v, src_lane);
 }
 
+__device__ __forceinline__ int64_t bcast_i64(int64_t v, int src_lane)
+{
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, src_lane);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), src_lane);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// order this wave's LDS stores before its later LDS loads of other lanes' data
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ int popc(uint64_t m) { return __popcll(m); }
 
 // ---- DPP wave reductions (result in lane 63, returned through v_readlane) ----
@@ -145,6 +160,103 @@ __device__ __forceinline__ void wave_sum_u32_n(uint32_t (&v)[N])
 
 // v into lane l (v, l uniform): v_cmp + v_cndmask
 __device__ __forceinline__ int writelane(int old, int v, int l) { return lane_id() == l ? v : old; }
+
+// ---- DPP prefix scans (inclusive): row shifts 1, 2, 4, 8 then row broadcasts 15, 31.
+// A lane whose DPP source is out of its row (or whose row is masked off) reads 0,
+// the identity of both OR and ADD.
+template <int CTRL, int RM>
+__device__ __forceinline__ uint32_t dpp0(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, RM, 0xF, false);
+}
+__device__ __forceinline__ uint32_t wave_scan_add(uint32_t v)
+{
+    v += dpp0<0x111, 0xF>(v);
+    v += dpp0<0x112, 0xF>(v);
+    v += dpp0<0x114, 0xF>(v);
+    v += dpp0<0x118, 0xF>(v);
+    v += dpp0<0x142, 0xA>(v);
+    v += dpp0<0x143, 0xC>(v);
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_scan_or(uint32_t v)
+{
+    v |= dpp0<0x111, 0xF>(v);
+    v |= dpp0<0x112, 0xF>(v);
+    v |= dpp0<0x114, 0xF>(v);
+    v |= dpp0<0x118, 0xF>(v);
+    v |= dpp0<0x142, 0xA>(v);
+    v |= dpp0<0x143, 0xC>(v);
+    return v;
+}
+// Segmented scans: a segment starts at every lane whose flag is set.  c[s] = ~0
+// unless a segment starts inside this lane's window before step s (Hillis-Steele
+// with head flags); the flags do not depend on the scanned words, so they are
+// built once per tile.  The combine is an AND with c[s], never a select: a select
+// may be lowered to an EXEC-masked DPP op, and DPP reads 0 from lanes EXEC disables.
+struct SegFlags {
+    uint32_t c0, c1, c2, c3, c4, c5;
+    __device__ __forceinline__ void init(bool head)
+    {
+        uint32_t f = head ? 1u : 0u;
+        c0 = f - 1u;  f |= dpp0<0x111, 0xF>(f);
+        c1 = f - 1u;  f |= dpp0<0x112, 0xF>(f);
+        c2 = f - 1u;  f |= dpp0<0x114, 0xF>(f);
+        c3 = f - 1u;  f |= dpp0<0x118, 0xF>(f);
+        c4 = f - 1u;  f |= dpp0<0x142, 0xA>(f);
+        c5 = f - 1u;
+    }
+    __device__ __forceinline__ uint32_t scan_or(uint32_t v) const
+    {
+        v |= dpp0<0x111, 0xF>(v) & c0;
+        v |= dpp0<0x112, 0xF>(v) & c1;
+        v |= dpp0<0x114, 0xF>(v) & c2;
+        v |= dpp0<0x118, 0xF>(v) & c3;
+        v |= dpp0<0x142, 0xA>(v) & c4;
+        v |= dpp0<0x143, 0xC>(v) & c5;
+        return v;
+    }
+    __device__ __forceinline__ uint32_t scan_add(uint32_t v) const
+    {
+        v += dpp0<0x111, 0xF>(v) & c0;
+        v += dpp0<0x112, 0xF>(v) & c1;
+        v += dpp0<0x114, 0xF>(v) & c2;
+        v += dpp0<0x118, 0xF>(v) & c3;
+        v += dpp0<0x142, 0xA>(v) & c4;
+        v += dpp0<0x143, 0xC>(v) & c5;
+        return v;
+    }
+};
+
+// min of a double over the 64 lanes (every lane gets it)
+__device__ __forceinline__ double wave_min_f64(double x)
+{
+#define RQ_MIN_STAGE(CTRL, RM)                                                                     \
+    {                                                                                              \
+        const uint64_t b = rq_dbl_bits(x);                                                         \
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, RM,   \
+                                                                  0xF, false);                     \
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0x7FF00000, (int)(uint32_t)(b >> 32), \
+                                                                  CTRL, RM, 0xF, false);           \
+        x = fmin(x, rq_bits_dbl(((uint64_t)hi << 32) | lo));                                       \
+    }
+    RQ_MIN_STAGE(0xB1, 0xF)
+    RQ_MIN_STAGE(0x4E, 0xF)
+    RQ_MIN_STAGE(0x141, 0xF)
+    RQ_MIN_STAGE(0x140, 0xF)
+    RQ_MIN_STAGE(0x142, 0xA)
+    RQ_MIN_STAGE(0x143, 0xC)
+#undef RQ_MIN_STAGE
+    return bcast_d(x, 63);
+}
+
+// the next double above finite x
+__device__ __forceinline__ double next_up(double x)
+{
+    if (x == 0.0) return rq_bits_dbl(1ull);
+    const uint64_t b = rq_dbl_bits(x);
+    return rq_bits_dbl(x > 0.0 ? b + 1 : b - 1);
+}
 
 // order-preserving map of a double onto uint64 (negative values reversed)
 __device__ __forceinline__ uint64_t order_key(double t)

@@ -1,0 +1,171 @@
+// rq_gen.h -- one source's arrival stream as a step machine (one lane, one source).
+//
+// Shared by rq_gen_streams (streams written to HBM) and the fused sweep (rings
+// refilled in LDS), so both produce the same bits.  One step() = one candidate:
+//   Poisson / Poisson2  opt_model.py:424-433 / :396-405 -- exponential gaps
+//                       t += Exp(1) / rate (one draw per arrival)
+//   Hawkes              opt_model.py:466-490 -- Ogata thinning, bound B = lambda at
+//                       the last accepted arrival (not refreshed on rejection), the
+//                       exponential kernel's O(1) recurrence for lambda; two draws
+//                       (Exp, uniform) per candidate
+//   PiecewiseConst      opt_model.py:642-663 -- thinning of exponential gaps at the
+//                       max rate; two draws per candidate
+//   RealData            opt_model.py:722-750 -- the given (host-filtered) times
+// Draw d of a stream is half d&1 of Philox4x32-10 call d>>1 under key (seed, salt):
+// the first half of a call is only taken with d even, so every candidate of a
+// two-draw kind is exactly one call.
+#pragma once
+#include "rq_device.h"
+#include "rq_internal.h"
+
+namespace rq {
+
+struct SrcGen {
+    uint32_t k0, k1;        // Philox key (seed, kind salt)
+    uint32_t w2, w3;        // second half of the last call
+    uint32_t d;             // next draw index (< 2^32 draws per source)
+    int kind;
+    bool done, needB;
+    double t;               // candidate base time
+    double tau, eta, B;     // Hawkes: last accepted time, excitation at tau, bound
+    double inv;             // 1 / rate (Poisson), 1 / max rate (PWConst), 1 / B (Hawkes)
+    double p0, p1, nbeta;   // rate | (l_0, alpha, -beta)
+    const double* ta;       // PWConst change times / RealData times
+    const double* tb;       // PWConst rates
+    int na, ri;
+
+    __device__ __forceinline__ void none()
+    {
+        kind = RQ_SRC_NONE;
+        done = true;
+        d = 0u;
+    }
+
+    __device__ __forceinline__ void init(const GenArgs& a, int j, int64_t i)
+    {
+        const bool is_ctrl = j == a.ctrl_idx;
+        kind = is_ctrl ? a.ctrl_stream_kind : a.kind[j];
+        const int64_t k = a.seed_mod > 0 ? i % a.seed_mod : i;
+        uint32_t seed;
+        if (is_ctrl) {
+            seed = a.ctrl_seed ? a.ctrl_seed[i] : a.ctrl_seed0 + (uint32_t)k;
+        } else if (a.randomize) {
+            const uint32_t u = a.world_seed ? a.world_seed[i] : a.world_seed0 + (uint32_t)k;
+            seed = u + 99u * (uint32_t)a.orig_idx[j];   // randomize_other_sources, opt_model.py:795-804
+        } else {
+            seed = a.seed[j];
+        }
+        k0 = seed;
+        k1 = kind_salt(kind, is_ctrl);
+        w2 = w3 = 0u;
+        d = 0u;
+        done = false;
+        needB = true;
+        t = a.start;
+        tau = a.start;
+        eta = 0.0;
+        B = 0.0;
+        inv = 0.0;
+        p0 = p1 = nbeta = 0.0;
+        ta = tb = nullptr;
+        na = ri = 0;
+        if (kind == RQ_SRC_POISSON || kind == RQ_SRC_POISSON2) {
+            const double rate = is_ctrl ? a.ctrl_rate[i] : a.p0[j];
+            if (rate > 0.0) inv = 1.0 / rate;
+            else done = true;
+        } else if (kind == RQ_SRC_HAWKES) {
+            p0 = a.p0[j];
+            p1 = a.p1[j];
+            nbeta = -a.p2[j];
+        } else if (kind == RQ_SRC_PWCONST) {
+            na = a.arr_n[j];
+            ta = a.arr_a + a.arr_off[j];
+            tb = a.arr_b + a.arr_off[j];
+            double mx = tb[0];
+            for (int q = 1; q < na; ++q) mx = tb[q] > mx ? tb[q] : mx;
+            if (mx > 0.0) inv = 1.0 / mx;
+            else done = true;
+            p0 = mx;
+        } else if (kind == RQ_SRC_REALDATA) {
+            na = a.arr_n[j];
+            ta = a.arr_a + a.arr_off[j];
+            done = na <= 0;
+        } else {
+            done = true;   // the controlled slot of an Opt / wall-only run: no stream
+        }
+    }
+
+    // one candidate; true (and *out) when it is an arrival.  Sets done past `end`.
+    __device__ __forceinline__ bool step(double* out, double end)
+    {
+        if (done) return false;
+        if (kind == RQ_SRC_REALDATA) {
+            *out = ta[ri];
+            ++ri;
+            done = ri >= na;
+            return true;
+        }
+        if (kind == RQ_SRC_HAWKES && needB) {
+            B = p0 + eta;
+            if (!(B > 0.0)) {
+                done = true;
+                return false;
+            }
+            inv = 1.0 / B;
+            t = tau;
+            needB = false;
+        }
+        double u1, u2 = 0.0;
+        if ((d & 1u) == 0u) {
+            const uint32_t call = d >> 1;
+            uint32_t c[4] = {call, 0u, 0u, 0u};
+            philox4x32_10(c, k0, k1);
+            w2 = c[2];
+            w3 = c[3];
+            u1 = rq_uniform53(c[0], c[1]);
+            u2 = rq_uniform53(c[2], c[3]);
+        } else {
+            u1 = rq_uniform53(w2, w3);
+        }
+        const bool poisson = kind == RQ_SRC_POISSON || kind == RQ_SRC_POISSON2;
+        d += poisson ? 1u : 2u;
+        const double tc = t + rq_std_exponential(u1) * inv;
+        if (!(tc <= end)) {
+            done = true;
+            return false;
+        }
+        t = tc;
+        if (poisson) {
+            *out = tc;
+            return true;
+        }
+        if (kind == RQ_SRC_HAWKES) {
+            const double decay = rq_exp(nbeta * (tc - tau));
+            const double rate = p0 + eta * decay;
+            if (u2 < rate / B) {
+                eta = eta * decay + p1;
+                tau = tc;
+                needB = true;
+                *out = tc;
+                return true;
+            }
+            return false;
+        }
+        // PiecewiseConst: rate(t) = rates[bisect_right(change_times, t) - 1]
+        int lo = 0, hi = na;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (tc < ta[mid]) hi = mid;
+            else lo = mid + 1;
+        }
+        int idx = lo - 1;
+        if (idx < 0) idx += na;
+        if (u2 < tb[idx] / p0) {
+            *out = tc;
+            return true;
+        }
+        return false;
+    }
+};
+
+}  // namespace rq

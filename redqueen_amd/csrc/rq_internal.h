@@ -64,11 +64,12 @@ struct SweepArgs {
     int64_t ev_cap;
     int n_csr;
     const uint32_t* masks;   // [n_str][nw] sink bitsets (BITS variant)
-    int nw;
+    int nw, mstride;         // words per bitset; LDS row stride in words (odd: bank spread)
     int dbg;                 // profiling: 1 skip phase C, 2 skip sink updates, 3 skip phase B
     int col_in_lds, win;     // general sweep: CSR copied to LDS; arrival-ring depth
     size_t lds_col, lds_ptr, lds_odf, lds_cbf, lds_wave, lds_wave_stride, lds_rank_off, lds_win_off, lds_x_off, lds_mask,
-        lds_total;
+        lds_total, lds_stage_off;
+    GenArgs gen;             // fused sweep: arrival generation parameters
 };
 
 struct ScanArgs {
@@ -89,6 +90,8 @@ hipError_t rq_launch_gen(const GenArgs& a, hipStream_t s);
 hipError_t rq_launch_sweep(const SweepArgs& a, int spl, int nK, int col16, int log, int bits, hipStream_t s);
 hipError_t rq_launch_scan(const ScanArgs& a, int nK, hipStream_t s);
 int rq_sweep_blocks_per_cu(int spl, int nK, int col16, int W, int log, int bits, int wpb, size_t lds);
+hipError_t rq_launch_sweep_fw(const SweepArgs& a, int nK, int col16, int W, int bits, hipStream_t s);
+int rq_fw_blocks_per_cu(int nK, int col16, int W, int bits, int wpb, size_t lds);
 
 struct ReplayArgs {
     const double* t;

@@ -28,6 +28,7 @@
 #include "rq_device.h"
 #include "rq_internal.h"
 #include "rq_sweep_core.h"
+#include "rq_gen.h"
 #include <type_traits>
 
 #pragma clang fp contract(off)
@@ -44,24 +45,11 @@ __global__ __launch_bounds__(256) void rq_gen_streams(GenArgs a)
     if (rl >= a.n_chunk) return;
     const int64_t o = a.chunk0 + rl;      // local output index
     const int64_t i = a.rep0 + o;         // global replica id (seeds)
-    const bool is_ctrl = j == a.ctrl_idx;
-    const int kind = is_ctrl ? a.ctrl_stream_kind : a.kind[j];
-
-    const int64_t k = a.seed_mod > 0 ? i % a.seed_mod : i;
-    uint32_t seed;
-    if (is_ctrl) {
-        seed = a.ctrl_seed ? a.ctrl_seed[i] : a.ctrl_seed0 + (uint32_t)k;
-    } else if (a.randomize) {
-        const uint32_t u = a.world_seed ? a.world_seed[i] : a.world_seed0 + (uint32_t)k;
-        seed = u + 99u * (uint32_t)a.orig_idx[j];
-    } else {
-        seed = a.seed[j];
-    }
-    PhiloxStream ps(seed, kind_salt(kind, is_ctrl));
+    SrcGen gen;
+    gen.init(a, j, i);
 
     double* out = a.streams + rl * a.capsum + a.st_off[j];   // 64-byte aligned (host pads)
     const int cap = a.cap[j];                                   // multiple of 8
-    const double start = a.start, end = a.end;
     int n = 0;
     bool ovf = false;
     // arrivals are staged 8 at a time in registers (compile-time shift, no
@@ -83,77 +71,9 @@ __global__ __launch_bounds__(256) void rq_gen_streams(GenArgs a)
         }                                                                        \
     } while (0)
 
-    if (kind == RQ_SRC_POISSON || kind == RQ_SRC_POISSON2) {
-        const double rate = is_ctrl ? a.ctrl_rate[i] : a.p0[j];
-        if (rate > 0.0) {
-            const double inv = 1.0 / rate;
-            double t = start;
-            for (;;) {
-                t = t + rq_std_exponential(ps.next()) * inv;
-                if (!(t <= end)) break;
-                RQ_EMIT(t);
-                if (ovf) break;
-            }
-        }
-    } else if (kind == RQ_SRC_HAWKES) {
-        const double l0 = a.p0[j], alpha = a.p1[j], nbeta = -a.p2[j];
-        double tau = start, eta = 0.0;
-        bool done = false;
-        while (!done && !ovf) {
-            const double B = l0 + eta;
-            if (!(B > 0.0)) break;
-            const double inv = 1.0 / B;
-            double t = tau;
-            for (;;) {
-                const double x = rq_std_exponential(ps.next());
-                const double v = ps.next();
-                const double tc = t + x * inv;
-                if (!(tc <= end)) {
-                    done = true;
-                    break;
-                }
-                const double decay = rq_exp(nbeta * (tc - tau));
-                const double rate = l0 + eta * decay;
-                if (v < rate / B) {
-                    eta = eta * decay + alpha;
-                    tau = tc;
-                    RQ_EMIT(tc);
-                    break;
-                }
-                t = tc;
-            }
-        }
-    } else if (kind == RQ_SRC_PWCONST) {
-        const int off = a.arr_off[j], na = a.arr_n[j];
-        const double* ct = a.arr_a + off;
-        const double* rt = a.arr_b + off;
-        double mx = rt[0];
-        for (int q = 1; q < na; ++q) mx = rt[q] > mx ? rt[q] : mx;
-        if (mx > 0.0) {
-            const double inv = 1.0 / mx;
-            double t = start;
-            for (;;) {
-                t = t + rq_std_exponential(ps.next()) * inv;
-                if (!(t <= end)) break;
-                const double v = ps.next();
-                int lo = 0, hi = na;   // bisect_right(change_times, t)
-                while (lo < hi) {
-                    const int mid = (lo + hi) >> 1;
-                    if (t < ct[mid]) hi = mid;
-                    else lo = mid + 1;
-                }
-                int idx = lo - 1;
-                if (idx < 0) idx += na;
-                if (v < rt[idx] / mx) {
-                    RQ_EMIT(t);
-                    if (ovf) break;
-                }
-            }
-        }
-    } else if (kind == RQ_SRC_REALDATA) {
-        // host pre-sorted, filtered to [start, end]
-        const int off = a.arr_off[j], na = a.arr_n[j];
-        for (int q = 0; q < na && !ovf; ++q) RQ_EMIT(a.arr_a[off + q]);
+    while (!gen.done && !ovf) {
+        double tv;
+        if (gen.step(&tv, a.end)) RQ_EMIT(tv);
     }
 #undef RQ_EMIT
     {   // the last partial chunk: values sit in sb[8-r .. 7]
@@ -204,7 +124,10 @@ __global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
     // BITS: per-stream sink bitsets instead of the columns
     uint32_t* msk = reinterpret_cast<uint32_t*>(base + a.lds_mask);
     if (BITS)
-        for (int e = threadIdx.x; e < a.n_str * a.nw; e += blockDim.x) msk[e] = a.masks[e];
+        for (int e = threadIdx.x; e < a.n_str * a.mstride; e += blockDim.x) {
+            const int jj = e / a.mstride, ww = e - jj * a.mstride;
+            msk[e] = ww < a.nw ? a.masks[jj * a.nw + ww] : 0u;
+        }
     for (int j = threadIdx.x; j <= a.n_str; j += blockDim.x) cptr[j] = a.csr_ptr[j];
     for (int j = threadIdx.x; j < a.n_str; j += blockDim.x) {
         odf[j] = a.outdeg_f[j];
@@ -286,7 +209,7 @@ __global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
     Agg<NK> ag;
     ag.init(a.Ks);
     AggB agb;
-    if (BITS) agb.init(msk, a.nw, a.ctrl_idx, lane);
+    if (BITS) agb.init(msk, a.nw, a.mstride, a.ctrl_idx, lane);
     RowStage<NK> rs;
     const int64_t rbase = rl * a.cap_rows;
     rs.init(a.rows_t + rbase, a.rows_sum + rbase, a.rows_valid + rbase, a.rows_cnt + rbase * NK,
@@ -397,47 +320,8 @@ __global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
         //  first); a post resets the min.  One prefix-min per post.
         uint64_t ownm = 0;
         double ot = RQ_INF;
-        if (opt && a.dbg != 3) {
-            double c = RQ_INF;
-            bool cb = false;
-            if (act) {
-                const uint64_t d = ndraw + (uint64_t)lane;   // draw d: Philox call d>>1, half d&1
-                const uint64_t call = d >> 1;
-                uint32_t w4[4] = {(uint32_t)call, (uint32_t)(call >> 32), 0u, 0u};
-                philox4x32_10(w4, oseed, kind_salt(RQ_SRC_OPT, true));
-                const double x = rq_std_exponential((d & 1) ? rq_uniform53(w4[2], w4[3])
-                                                            : rq_uniform53(w4[0], w4[1]));
-                const double ic = invc[tj];
-                const double e = ic > 0.0 ? x * ic : RQ_INF;
-                c = tt + e;
-                cb = cbf[tj] != 0;
-            }
-            ndraw += (uint64_t)n;
-            int s0 = 0;
-            double cur = opt_next;
-            for (;;) {
-                double inc = (lane >= s0 && act) ? c : RQ_INF;
-#pragma unroll
-                for (int sh = 1; sh < 64; sh <<= 1) {
-                    const double u = __shfl_up(inc, sh, 64);
-                    if (lane >= sh) inc = fmin(inc, u);
-                }
-                double ex = __shfl_up(inc, 1, 64);
-                if (lane == 0) ex = RQ_INF;
-                const double m = fmin(cur, ex);
-                const uint64_t b = __ballot(lane >= s0 && act && (m < tt || (m == tt && cb)));
-                if (b == 0) {
-                    if (n > 0) cur = fmin(cur, bcast_d(inc, n - 1));
-                    break;
-                }
-                const int is = __ffsll((unsigned long long)b) - 1;
-                ownm |= 1ull << is;
-                if (lane == is) ot = m;
-                cur = RQ_INF;
-                s0 = is;
-            }
-            opt_next = cur;
-        }
+        if (opt && a.dbg != 3)
+            controller_tile(n, act, tt, tj, invc, cbf, oseed, ndraw, opt_next, ownm, ot);
         // ---- C: apply the tile's events in order ----
         if (LOG) {
             for (int q = 0; q < n; ++q) {
@@ -479,7 +363,7 @@ __global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
 #pragma unroll
                     for (int k = 0; k < 8; ++k) {
                         jk[k] = bcast_i(tj, q0 + k < n ? q0 + k : n - 1);
-                        m[k] = lane < agb.nw ? agb.M[jk[k] * agb.nw + lane] : 0u;
+                        m[k] = lane < agb.nw ? agb.M[jk[k] * agb.stride + lane] : 0u;
                     }
 #pragma unroll
                     for (int k = 0; k < 8; ++k) {
@@ -539,51 +423,12 @@ __global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
                     for (int kq = 0; kq < NK; ++kq) wcnt[kq] = ag.cnt[kq];
                 }
             }
-            const uint64_t mo = __ballot(has_o), mw = __ballot(has_w), ma = mo | mw;
-            const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+            const uint64_t mo = __ballot(has_o), ma = mo | __ballot(has_w);
             n_events += n + __popcll(ownm);
             posts += __popcll(mo) + __popcll(__ballot(has_w && strm_own));
             world += __popcll(__ballot(has_w && !strm_own));
-            if (ma) {
-                // pivot_table keeps one row per distinct t (the last): a row is
-                // dropped when the next row has the same time; a first row equal
-                // to the previous tile's last row overwrites it
-                const uint64_t above = ma & ~below & ~(1ull << lane);
-                const bool nxt = above != 0;
-                const double ft = has_o ? ot : tt;
-                const double nft = __shfl(ft, nxt ? __ffsll((unsigned long long)above) - 1 : lane, 64);
-                const bool keep_o = has_o && !(has_w ? ot == tt : (nxt && ot == nft));
-                const bool keep_w = has_w && !(nxt && tt == nft);
-                const bool tie0 = rs.nrow > 0 && bcast_d(ft, __ffsll((unsigned long long)ma) - 1) == rs.last_t;
-                const uint64_t ko = __ballot(keep_o), kw = __ballot(keep_w);
-                if (tie0 || ko != mo || kw != mw) status |= RQ_ST_TIE;
-                const int64_t r0 = rs.nrow - (tie0 ? 1 : 0);
-                const int64_t po = r0 + __popcll(ko & below) + __popcll(kw & below);
-                const int64_t pw = po + (keep_o ? 1 : 0);
-                if (keep_o && po < rs.cap) {
-                    rs.Rt[po] = ot;
-                    rs.Rs[po] = (double)osum;
-                    rs.Rv[po] = (uint32_t)oval;
-#pragma unroll
-                    for (int kq = 0; kq < NK; ++kq) rs.Rc[po * NK + kq] = (uint32_t)ocnt[kq];
-                }
-                if (keep_w && pw < rs.cap) {
-                    rs.Rt[pw] = tt;
-                    rs.Rs[pw] = (double)wsum;
-                    rs.Rv[pw] = (uint32_t)wval;
-#pragma unroll
-                    for (int kq = 0; kq < NK; ++kq) rs.Rc[pw * NK + kq] = (uint32_t)wcnt[kq];
-                }
-                rs.last_t = bcast_d(has_w ? tt : ot, 63 - __builtin_clzll(ma));   // always kept
-                rs.nrow = r0 + __popcll(ko) + __popcll(kw);
-                rs.s0 = rs.nrow;
-                if (rs.nrow > rs.cap) {
-                    rs.nrow = rs.cap;
-                    rs.s0 = rs.cap;
-                    status |= RQ_ST_ROWS_OVERFLOW;
-                    stop = true;
-                }
-            }
+            if (ma && place_rows<NK>(rs, ma, has_o, has_w, ot, tt, osum, oval, ocnt, wsum, wval, wcnt, status))
+                stop = true;
         }
         if (stop || fin) break;
     }
@@ -640,6 +485,344 @@ __global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
         cnto[2] = n_events;
         cnto[3] = rs.nrow;
         a.sall[rl] = LOG ? ax.nvalid : ag.nvalid;   // BITS: synced below
+        if (rs.nrow == 0) status |= RQ_ST_EMPTY;
+        if (status) atomicOr(&a.status[o], status);
+    }
+}
+
+// ============================================================================
+// 2b. fused windowed sweep (n_str <= 64).  Lane j owns stream j and GENERATES its
+//     arrivals (SrcGen) into an LDS ring -- no stream buffer, no generator
+//     kernel.  A tile is every pending arrival earlier than a cut tau, found from
+//     the next H arrivals of each ring held in registers (a ring's unseen
+//     arrivals are >= its H-th, so tau <= min over rings of the H-th keeps the
+//     tile complete); tau adapts so a tile holds <= 64 arrivals.  The tile is
+//     staged in source order and rank-sorted into (t, stream) order -- the
+//     reference's (time, src_id) order (opt_model.py:279-281).  Phase B is the
+//     same controller; phase C for K = 1 runs lane-parallel over the tile's
+//     events: per sink-bitset word, segmented prefix ORs (segments start at the
+//     posts) give each event's top-1 set, plain prefix ORs its valid set.
+// ============================================================================
+template <int NK, class COL, int W, int H, bool BITS>
+__global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
+{
+    static_assert((W & (W - 1)) == 0 && H <= W, "ring");
+    extern __shared__ double lds_g[];
+    char* base = reinterpret_cast<char*>(lds_g);
+    const int lane = lane_id();
+    const int w = threadIdx.x >> 6;
+    int* cptr = reinterpret_cast<int*>(base + a.lds_ptr);
+    int* odf = reinterpret_cast<int*>(base + a.lds_odf);
+    int* cbf = reinterpret_cast<int*>(base + a.lds_cbf);
+    constexpr bool col_lds = sizeof(COL) == 2;
+    COL* col_l = reinterpret_cast<COL*>(base + a.lds_col);
+    const int* col_g = a.csr_col;
+    if (col_lds && !BITS)
+        for (int e = threadIdx.x; e < a.n_csr; e += blockDim.x) col_l[e] = (COL)a.csr_col[e];
+    uint32_t* msk = reinterpret_cast<uint32_t*>(base + a.lds_mask);
+    const int ms = a.mstride;
+    if (BITS)
+        for (int e = threadIdx.x; e < a.n_str * ms; e += blockDim.x) {
+            const int jj = e / ms, ww = e - jj * ms;
+            msk[e] = ww < a.nw ? a.masks[jj * a.nw + ww] : 0u;
+        }
+    for (int j = threadIdx.x; j <= a.n_str; j += blockDim.x) cptr[j] = a.csr_ptr[j];
+    for (int j = threadIdx.x; j < a.n_str; j += blockDim.x) {
+        odf[j] = a.outdeg_f[j];
+        cbf[j] = a.ctrl_src_id < a.src_id[j];
+    }
+    const int64_t rl = (int64_t)blockIdx.x * a.wpb + w;
+    const bool live = rl < a.n_chunk;
+    const int64_t o = a.chunk0 + (live ? rl : 0);
+    const int64_t i = a.rep0 + o;
+    const int g = (int)(i / a.n_rep);
+    char* wb = base + a.lds_wave + (size_t)w * a.lds_wave_stride;
+    double* invc = reinterpret_cast<double*>(wb);
+    int16_t* rank = reinterpret_cast<int16_t*>(wb + a.lds_rank_off);   // saturating, exact vs K-1
+    double* ring = reinterpret_cast<double*>(wb + a.lds_win_off) + lane * (W + 1);   // odd stride
+    double* st_t = reinterpret_cast<double*>(wb + a.lds_stage_off);
+    int* st_j = reinterpret_cast<int*>(st_t + 64);
+    for (int j = lane; j < a.n_str; j += 64) invc[j] = a.inv_c[(int64_t)g * a.n_str + j];
+    if (!BITS)
+        for (int c = lane; c < a.n_sinks; c += 64) rank[c] = -1;   // NaN: no row yet
+    __syncthreads();
+    if (!live) return;
+
+    SrcGen gen;
+    if (lane < a.n_str) gen.init(a.gen, lane, i);
+    else gen.none();
+    int pos = 0, fil = 0;   // arrivals consumed / generated by this lane's source
+
+    const bool opt = a.ctrl_kind == RQ_SRC_OPT;
+    double opt_next = opt ? a.start : RQ_INF;
+    const int64_t k = a.seed_mod > 0 ? i % a.seed_mod : i;
+    const uint32_t oseed = a.ctrl_seed ? a.ctrl_seed[i] : a.ctrl_seed0 + (uint32_t)k;
+    uint64_t ndraw = 0;   // wall events seen so far = the controller's draw index
+    auto colat = [&](int e) -> int { return col_lds ? (int)col_l[e] : col_g[e]; };
+    const int fol0 = cptr[a.ctrl_idx];
+    auto folat = [&](int f) -> int { return colat(fol0 + f); };
+
+    Agg<NK> ag;
+    ag.init(a.Ks);
+    AggB agb;
+    if (BITS) agb.init(msk, a.nw, ms, a.ctrl_idx, lane);
+    RowStage<NK> rs;
+    const int64_t rbase = rl * a.cap_rows;
+    rs.init(a.rows_t + rbase, a.rows_sum + rbase, a.rows_valid + rbase, a.rows_cnt + rbase * NK,
+            a.cap_rows);
+
+    int64_t n_events = 0, posts = 0, world = 0;
+    int status = 0;
+    double span = -1.0;   // adaptive tile width in time (< 0: not estimated yet)
+    bool stop = false;
+    for (;;) {
+        // ---- A1: every unfinished ring shows >= H arrivals (refill all to W at once) ----
+        if (__ballot(!gen.done && fil - pos < H)) {
+            while (__ballot(!gen.done && fil - pos < W)) {
+                if (!gen.done && fil - pos < W) {
+                    double tv;
+                    if (gen.step(&tv, a.end)) {
+                        ring[fil & (W - 1)] = tv;
+                        ++fil;
+                    }
+                }
+            }
+        }
+        const int avail = fil - pos;
+        double v[H];
+#pragma unroll
+        for (int q = 0; q < H; ++q) v[q] = q < avail ? ring[(pos + q) & (W - 1)] : RQ_INF;
+        const bool more = !gen.done || avail > H;        // arrivals past the window exist
+        const double tfirst = wave_min_f64(v[0]);
+        if (!(tfirst < RQ_INF)) break;                   // everything consumed
+        const double tmax = wave_min_f64(more ? v[H - 1] : RQ_INF);
+
+        // ---- A2: the cut (exclusive): complete below tmax, <= 64 arrivals ----
+        int c = 0, n = 0;
+        bool trunc = !(tmax > tfirst);   // a ring's window is all at tfirst: equal-time prefix
+        if (!trunc) {
+            double cut = tmax;
+            if (span > 0.0 && tfirst + span < cut) cut = tfirst + span;
+            if (!(cut > tfirst)) cut = next_up(tfirst);
+            for (;;) {
+                c = 0;
+#pragma unroll
+                for (int q = 0; q < H; ++q) c += v[q] < cut ? 1 : 0;
+                n = (int)wave_sum_u32((uint32_t)c);
+                if (n <= 64) break;
+                const double nc = tfirst + (cut - tfirst) * 0.5;
+                const double lo = next_up(tfirst);
+                if (nc > tfirst && nc < cut) {
+                    cut = nc < lo ? lo : nc;
+                } else if (cut != lo) {
+                    cut = lo;
+                } else {
+                    trunc = true;   // > 64 arrivals share tfirst
+                    break;
+                }
+            }
+            if (!trunc) span = (cut - tfirst) * (48.0 / (double)(n > 8 ? n : 8));
+        }
+        if (trunc) {
+            // the arrivals equal to tfirst, in stream order, up to the first ring whose
+            // window may continue at tfirst, at most 64
+            c = 0;
+#pragma unroll
+            for (int q = 0; q < H; ++q) c += v[q] == tfirst ? 1 : 0;
+            const uint64_t bl = __ballot(more && v[H - 1] == tfirst);
+            const int lb = bl ? __ffsll((unsigned long long)bl) - 1 : 64;
+            if (lane > lb) c = 0;
+        }
+        const int off = (int)wave_scan_add((uint32_t)c) - c;
+        if (trunc) {
+            c = off >= 64 ? 0 : (c < 64 - off ? c : 64 - off);
+            n = (int)wave_sum_u32((uint32_t)c);
+        }
+
+        // ---- A3: stage in stream order, rank-sort into (t, stream) order ----
+#pragma unroll
+        for (int q = 0; q < H; ++q)
+            if (q < c) {
+                st_t[off + q] = v[q];
+                st_j[off + q] = lane;
+            }
+        wave_lds_sync();
+        const bool act = lane < n;
+        const double ti = act ? st_t[lane] : RQ_INF;
+        const int ji = act ? st_j[lane] : 0;
+        int rnk = 0;
+        for (int q = 0; q < n; ++q) {
+            const double tq = bcast_d(ti, q);
+            rnk += (tq < ti || (tq == ti && q < lane)) ? 1 : 0;
+        }
+        wave_lds_sync();
+        if (act) {
+            st_t[rnk] = ti;
+            st_j[rnk] = ji;
+        }
+        wave_lds_sync();
+        const double tt = act ? st_t[lane] : RQ_INF;
+        const int tj = act ? st_j[lane] : 0;
+        pos += c;
+        const bool fin = !__ballot(!gen.done || pos < fil);
+
+        int e0 = 0, e1 = 0, od = 0;
+        if (act) {
+            e0 = cptr[tj];
+            e1 = cptr[tj + 1];
+            od = odf[tj];
+        }
+        // ---- B: RedQueen controller over the tile ----
+        uint64_t ownm = 0;
+        double ot = RQ_INF;
+        if (opt) controller_tile(n, act, tt, tj, invc, cbf, oseed, ndraw, opt_next, ownm, ot);
+
+        // ---- C: aggregates after each event ----
+        const bool own_b = act && ((ownm >> lane) & 1ull);       // controller post before #lane
+        const bool strm_own = act && !opt && tj == a.ctrl_idx;   // controlled stream's arrival
+        const bool has_o = own_b && a.n_fol > 0;
+        const bool has_w = act && e1 > e0;
+        int64_t osum = 0, wsum = 0;
+        int oval = 0, wval = 0;
+        int ocnt[NK], wcnt[NK];
+#pragma unroll
+        for (int kq = 0; kq < NK; ++kq) ocnt[kq] = wcnt[kq] = 0;
+        if (BITS) {
+            // segments of the tile start at its own events (posts / own-stream arrivals)
+            const bool rst = own_b || strm_own;
+            const uint64_t rm = __ballot(rst);
+            const bool hasr = (rm & (~0ull >> (63 - lane))) != 0;   // own event at or before #lane
+            const bool wl = act && !strm_own;                        // a wall event
+            const int deg = wl ? e1 - e0 : 0;
+            const int odv = wl ? od : 0;
+            SegFlags sf;
+            sf.init(rst);
+            // sumR / sumF: wall adds deg / odf, an own event drops sumF from sumR
+            const int pdeg = (int)wave_scan_add((uint32_t)deg);
+            const int64_t sfq = (int64_t)(int)sf.scan_add((uint32_t)odv) + (hasr ? 0 : agb.sumF);
+            int64_t dec = 0;
+            for (uint64_t b = rm; b; b &= b - 1) {
+                const int r = __ffsll((unsigned long long)b) - 1;
+                const int64_t D = r == 0 ? agb.sumF : bcast_i64(sfq, r - 1);
+                if (lane >= r) dec += D;
+            }
+            wsum = agb.sumR + pdeg - dec;
+            osum = agb.sumR + (pdeg - deg) - dec;
+            // sink bitsets, one word at a time, every event of the tile at once
+            const bool vfull = agb.nvalid == a.n_sinks;
+            const int last = n - 1;
+            const uint32_t* mr = msk + (wl ? tj : 0) * ms;
+            int cw = 0, vw = 0, vo = 0;
+            uint32_t nT = agb.T, nV = agb.V;
+            for (int ww = 0; ww < a.nw; ++ww) {
+                const uint32_t Fw = (uint32_t)__builtin_amdgcn_readlane((int)agb.F, ww);
+                const uint32_t Tw = (uint32_t)__builtin_amdgcn_readlane((int)agb.T, ww);
+                const uint32_t m = wl ? mr[ww] : 0u;
+                const uint32_t u = sf.scan_or(m);                  // wall union since the segment start
+                const uint32_t tq = (hasr ? Fw : Tw) & ~u;         // top-1 set after #lane
+                cw += __popc(tq);
+                nT = (uint32_t)writelane((int)nT, __builtin_amdgcn_readlane((int)tq, last), ww);
+                if (!vfull) {
+                    const uint32_t Vw = (uint32_t)__builtin_amdgcn_readlane((int)agb.V, ww);
+                    const uint32_t x = wave_scan_or(m);
+                    const uint32_t vq = Vw | x | (hasr ? Fw : 0u);  // valid set after #lane
+                    vw += __popc(vq);
+                    const uint32_t xe = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xF, 0xF, false);
+                    vo += __popc(Vw | xe | Fw);                     // after the post before #lane
+                    nV = (uint32_t)writelane((int)nV, __builtin_amdgcn_readlane((int)vq, last), ww);
+                }
+            }
+            wcnt[0] = cw;
+            ocnt[0] = a.n_fol;   // a post puts every follower at rank 0
+            wval = vfull ? a.n_sinks : vw;
+            oval = vfull ? a.n_sinks : vo;
+            if (n > 0) {
+                agb.T = nT;
+                if (!vfull) {
+                    agb.V = nV;
+                    agb.nvalid = bcast_i(vw, last);
+                }
+                agb.sumR = bcast_i64(wsum, last);
+                agb.sumF = bcast_i64(sfq, last);
+            }
+        } else {
+            for (int q = 0; q < n; ++q) {
+                if ((ownm >> q) & 1ull) {
+                    ag.own(rank, folat, a.n_fol, lane);
+                    if (lane == q) {
+                        osum = ag.sumR;
+                        oval = ag.nvalid;
+#pragma unroll
+                        for (int kq = 0; kq < NK; ++kq) ocnt[kq] = ag.cnt[kq];
+                    }
+                }
+                const int jw = bcast_i(tj, q);
+                if (!opt && jw == a.ctrl_idx)
+                    ag.own(rank, folat, a.n_fol, lane);
+                else
+                    ag.wall(rank, colat, bcast_i(e0, q), bcast_i(e1, q), bcast_i(od, q), lane);
+                if (lane == q) {
+                    wsum = ag.sumR;
+                    wval = ag.nvalid;
+#pragma unroll
+                    for (int kq = 0; kq < NK; ++kq) wcnt[kq] = ag.cnt[kq];
+                }
+            }
+        }
+        const uint64_t mo = __ballot(has_o), ma = mo | __ballot(has_w);
+        n_events += n + __popcll(ownm);
+        posts += __popcll(mo) + __popcll(__ballot(has_w && strm_own));
+        world += __popcll(__ballot(has_w && !strm_own));
+        if (ma && place_rows<NK>(rs, ma, has_o, has_w, ot, tt, osum, oval, ocnt, wsum, wval, wcnt, status))
+            stop = true;
+        if (stop || fin) break;
+    }
+    // the controller's last post after the final arrival
+    if (!stop && opt && opt_next <= a.end) {
+        ++n_events;
+        if (BITS) {
+            agb.own();
+            agb.sync();
+            ag.sumR = agb.sumR;
+            ag.nvalid = agb.nvalid;
+            ag.cnt[0] = agb.cnt[0];
+        } else {
+            ag.own(rank, folat, a.n_fol, lane);
+        }
+        if (a.n_fol > 0) {
+            ++posts;
+            int64_t rr = rs.nrow;
+            if (rs.nrow > 0 && opt_next == rs.last_t) {
+                status |= RQ_ST_TIE;
+                rr = rs.nrow - 1;
+            } else if (rs.nrow >= rs.cap) {
+                status |= RQ_ST_ROWS_OVERFLOW;
+                rr = -1;
+            } else {
+                ++rs.nrow;
+                rs.s0 = rs.nrow;
+                rs.last_t = opt_next;
+            }
+            if (rr >= 0 && lane == 0) {
+                rs.Rt[rr] = opt_next;
+                rs.Rs[rr] = (double)ag.sumR;
+                rs.Rv[rr] = (uint32_t)ag.nvalid;
+#pragma unroll
+                for (int kq = 0; kq < NK; ++kq) rs.Rc[rr * NK + kq] = (uint32_t)ag.cnt[kq];
+            }
+        }
+    }
+    if (BITS) {
+        agb.sync();
+        ag.nvalid = agb.nvalid;
+    }
+    if (lane == 0) {
+        int64_t* cnto = a.counts + o * 4;
+        cnto[0] = posts;
+        cnto[1] = world;
+        cnto[2] = n_events;
+        cnto[3] = rs.nrow;
+        a.sall[rl] = ag.nvalid;
         if (rs.nrow == 0) status |= RQ_ST_EMPTY;
         if (status) atomicOr(&a.status[o], status);
     }
@@ -1019,6 +1202,57 @@ int rq_sweep_blocks_per_cu(int spl, int nK, int col16, int W, int log, int bits,
     case 4: return occ_c<4>(nK, col16, W, bits, wpb, lds);
     default: return occ_c<8>(nK, col16, W, bits, wpb, lds);
     }
+}
+
+// fused windowed sweep: (W, H) in {(16, 8), (8, 4)}
+template <int NK, class COL, int W, bool BITS>
+static hipError_t launch_fw_t(const SweepArgs& a, hipStream_t s)
+{
+    const unsigned blocks = (unsigned)((a.n_chunk + a.wpb - 1) / a.wpb);
+    hipLaunchKernelGGL((rq_sweep_fw<NK, COL, W, W / 2, BITS>), dim3(blocks), dim3(64 * a.wpb), a.lds_total, s, a);
+    return hipGetLastError();
+}
+template <class COL, int W>
+static hipError_t launch_fw_k(const SweepArgs& a, int nK, hipStream_t s)
+{
+    switch (nK) {
+    case 1: return launch_fw_t<1, COL, W, false>(a, s);
+    case 2: return launch_fw_t<2, COL, W, false>(a, s);
+    case 3: return launch_fw_t<3, COL, W, false>(a, s);
+    default: return launch_fw_t<4, COL, W, false>(a, s);
+    }
+}
+hipError_t rq_launch_sweep_fw(const SweepArgs& a, int nK, int col16, int W, int bits, hipStream_t s)
+{
+    if (a.n_chunk <= 0) return hipSuccess;
+    if (bits) return W == 16 ? launch_fw_t<1, uint16_t, 16, true>(a, s) : launch_fw_t<1, uint16_t, 8, true>(a, s);
+    if (W == 16) return col16 ? launch_fw_k<uint16_t, 16>(a, nK, s) : launch_fw_k<int, 16>(a, nK, s);
+    return col16 ? launch_fw_k<uint16_t, 8>(a, nK, s) : launch_fw_k<int, 8>(a, nK, s);
+}
+template <int NK, class COL, int W, bool BITS>
+static int occ_fw_t(int wpb, size_t lds)
+{
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rq_sweep_fw<NK, COL, W, W / 2, BITS>, 64 * wpb, lds) !=
+        hipSuccess)
+        return 0;
+    return nb;
+}
+template <class COL, int W>
+static int occ_fw_k(int nK, int wpb, size_t lds)
+{
+    switch (nK) {
+    case 1: return occ_fw_t<1, COL, W, false>(wpb, lds);
+    case 2: return occ_fw_t<2, COL, W, false>(wpb, lds);
+    case 3: return occ_fw_t<3, COL, W, false>(wpb, lds);
+    default: return occ_fw_t<4, COL, W, false>(wpb, lds);
+    }
+}
+int rq_fw_blocks_per_cu(int nK, int col16, int W, int bits, int wpb, size_t lds)
+{
+    if (bits) return W == 16 ? occ_fw_t<1, uint16_t, 16, true>(wpb, lds) : occ_fw_t<1, uint16_t, 8, true>(wpb, lds);
+    if (W == 16) return col16 ? occ_fw_k<uint16_t, 16>(nK, wpb, lds) : occ_fw_k<int, 16>(nK, wpb, lds);
+    return col16 ? occ_fw_k<uint16_t, 8>(nK, wpb, lds) : occ_fw_k<int, 8>(nK, wpb, lds);
 }
 
 template <int NK>

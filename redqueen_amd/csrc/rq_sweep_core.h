@@ -103,9 +103,9 @@ struct AggB {
     int nvalid;
     int cnt[1];
     uint32_t T, V, F;
-    const uint32_t* M;   // LDS [n_str][nw]
-    int nw;
-    __device__ __forceinline__ void init(const uint32_t* M_, int nw_, int ctrl_idx, int lane)
+    const uint32_t* M;   // LDS [n_str][stride], words [0, nw) used
+    int nw, stride;
+    __device__ __forceinline__ void init(const uint32_t* M_, int nw_, int stride_, int ctrl_idx, int lane)
     {
         sumR = 0;
         sumF = 0;
@@ -115,11 +115,12 @@ struct AggB {
         V = 0u;
         M = M_;
         nw = nw_;
-        F = lane < nw ? M[ctrl_idx * nw + lane] : 0u;
+        stride = stride_;
+        F = lane < nw ? M[ctrl_idx * stride + lane] : 0u;
     }
     __device__ __forceinline__ void wall(int j, int deg, int odf, int lane)
     {
-        const uint32_t m = lane < nw ? M[j * nw + lane] : 0u;
+        const uint32_t m = lane < nw ? M[j * stride + lane] : 0u;
         V |= m;
         T &= ~m;
         sumR += deg;
@@ -323,6 +324,109 @@ struct RowStage {
         s0 = nrow;
     }
 };
+
+// ---- B: RedQueen controller over a tile (opt_model.py:502-544) ----
+//  Lane q < n holds wall event q (time tt, stream tj).  Candidate after wall event
+//  q: c_q = t_q + Exp(1)/c_{j_q} (draw ndraw + q of the controller's stream); the
+//  post fires before wall event q when the running min beats t_q (ties: lower
+//  src_id first, cbf); a post resets the min.  One prefix-min per post.
+//  Out: ownm bit q = a post right before wall event q, at time ot (lane q).
+__device__ __forceinline__ void controller_tile(int n, bool act, double tt, int tj, const double* invc,
+                                                const int* cbf, uint32_t oseed, uint64_t& ndraw,
+                                                double& opt_next, uint64_t& ownm, double& ot)
+{
+    const int lane = lane_id();
+    double c = RQ_INF;
+    bool cb = false;
+    if (act) {
+        const uint64_t d = ndraw + (uint64_t)lane;   // draw d: Philox call d>>1, half d&1
+        const uint64_t call = d >> 1;
+        uint32_t w4[4] = {(uint32_t)call, (uint32_t)(call >> 32), 0u, 0u};
+        philox4x32_10(w4, oseed, kind_salt(RQ_SRC_OPT, true));
+        const double x = rq_std_exponential((d & 1) ? rq_uniform53(w4[2], w4[3])
+                                                    : rq_uniform53(w4[0], w4[1]));
+        const double ic = invc[tj];
+        const double e = ic > 0.0 ? x * ic : RQ_INF;
+        c = tt + e;
+        cb = cbf[tj] != 0;
+    }
+    ndraw += (uint64_t)n;
+    int s0 = 0;
+    double cur = opt_next;
+    for (;;) {
+        double inc = (lane >= s0 && act) ? c : RQ_INF;
+#pragma unroll
+        for (int sh = 1; sh < 64; sh <<= 1) {
+            const double u = __shfl_up(inc, sh, 64);
+            if (lane >= sh) inc = fmin(inc, u);
+        }
+        double ex = __shfl_up(inc, 1, 64);
+        if (lane == 0) ex = RQ_INF;
+        const double m = fmin(cur, ex);
+        const uint64_t b = __ballot(lane >= s0 && act && (m < tt || (m == tt && cb)));
+        if (b == 0) {
+            if (n > 0) cur = fmin(cur, bcast_d(inc, n - 1));
+            break;
+        }
+        const int is = __ffsll((unsigned long long)b) - 1;
+        ownm |= 1ull << is;
+        if (lane == is) ot = m;
+        cur = RQ_INF;
+        s0 = is;
+    }
+    opt_next = cur;
+}
+
+// ---- pivot rows of a tile: lane q may hold a post row (before its wall event,
+//  aggregates o*) and a wall row (w*).  pivot_table keeps one row per distinct t
+//  (the last): a row is dropped when the next row has the same time; a first row
+//  equal to the previous tile's last row overwrites it.  ma = ballot(has_o|has_w),
+//  nonzero.  Returns true when the row capacity overflowed (stop the replica).
+template <int NK>
+__device__ __forceinline__ bool place_rows(RowStage<NK>& rs, uint64_t ma, bool has_o, bool has_w, double ot,
+                                           double tt, int64_t osum, int oval, const int* ocnt,
+                                           int64_t wsum, int wval, const int* wcnt, int& status)
+{
+    const int lane = lane_id();
+    const uint64_t mo = __ballot(has_o), mw = __ballot(has_w);
+    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const uint64_t above = ma & ~below & ~(1ull << lane);
+    const bool nxt = above != 0;
+    const double ft = has_o ? ot : tt;
+    const double nft = __shfl(ft, nxt ? __ffsll((unsigned long long)above) - 1 : lane, 64);
+    const bool keep_o = has_o && !(has_w ? ot == tt : (nxt && ot == nft));
+    const bool keep_w = has_w && !(nxt && tt == nft);
+    const bool tie0 = rs.nrow > 0 && bcast_d(ft, __ffsll((unsigned long long)ma) - 1) == rs.last_t;
+    const uint64_t ko = __ballot(keep_o), kw = __ballot(keep_w);
+    if (tie0 || ko != mo || kw != mw) status |= RQ_ST_TIE;
+    const int64_t r0 = rs.nrow - (tie0 ? 1 : 0);
+    const int64_t po = r0 + __popcll(ko & below) + __popcll(kw & below);
+    const int64_t pw = po + (keep_o ? 1 : 0);
+    if (keep_o && po < rs.cap) {
+        rs.Rt[po] = ot;
+        rs.Rs[po] = (double)osum;
+        rs.Rv[po] = (uint32_t)oval;
+#pragma unroll
+        for (int kq = 0; kq < NK; ++kq) rs.Rc[po * NK + kq] = (uint32_t)ocnt[kq];
+    }
+    if (keep_w && pw < rs.cap) {
+        rs.Rt[pw] = tt;
+        rs.Rs[pw] = (double)wsum;
+        rs.Rv[pw] = (uint32_t)wval;
+#pragma unroll
+        for (int kq = 0; kq < NK; ++kq) rs.Rc[pw * NK + kq] = (uint32_t)wcnt[kq];
+    }
+    rs.last_t = bcast_d(has_w ? tt : ot, 63 - __builtin_clzll(ma));   // always kept
+    rs.nrow = r0 + __popcll(ko) + __popcll(kw);
+    rs.s0 = rs.nrow;
+    if (rs.nrow > rs.cap) {
+        rs.nrow = rs.cap;
+        rs.s0 = rs.cap;
+        status |= RQ_ST_ROWS_OVERFLOW;
+        return true;
+    }
+    return false;
+}
 
 // optional (t, source index) event log, staged the same way
 struct EvStage {

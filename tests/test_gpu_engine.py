@@ -42,16 +42,17 @@ def _oracle(O, so, ctrl, Ks, max_events=None):
     return met, t, s
 
 
-MODES = ["fast", "scatter", "log"]
+MODES = ["fast", "scatter", "log", "legacy"]
 
 
 def _mode_kw(mode):
-    """fast: the tiled sweep (K=1 runs on sink bitsets); scatter: the tiled sweep
+    """fast: the fused windowed sweep (K=1 runs on sink bitsets); scatter: the same
     with per-sink LDS ranks (sweep_mode=3); log: the sequential event-log variant
-    (sweep_mode=2), events compared too."""
+    (sweep_mode=2), events compared too; legacy: pre-generated streams + serial
+    wave-min merge (sweep_mode=4)."""
     if mode == "log":
         return dict(event_log=True, sweep_mode=2)
-    return dict(event_log=False, sweep_mode=3 if mode == "scatter" else 0)
+    return dict(event_log=False, sweep_mode={"scatter": 3, "legacy": 4}.get(mode, 0))
 
 
 def _cmp_replica(res, i, met_o, t_o, s_o, Ks):
@@ -177,12 +178,16 @@ def test_large_batch_no_overflow_and_determinism():
               randomize=True, Ks=(1,), sweep_mode=2)
     d = g.run("opt", q=so["q"], s=so["s"], n_rep=2048, ctrl_seed=0, world_seed=0,
               randomize=True, Ks=(1,), sweep_mode=3)
-    assert g.run("opt", q=so["q"], s=so["s"], n_rep=2048, Ks=(1,), plan_only=True)["variant"] == 2
+    e = g.run("opt", q=so["q"], s=so["s"], n_rep=2048, ctrl_seed=0, world_seed=0,
+              randomize=True, Ks=(1,), sweep_mode=4)
+    assert g.run("opt", q=so["q"], s=so["s"], n_rep=2048, Ks=(1,), plan_only=True)["variant"] == 12
     assert torch.equal(a.metrics, b.metrics) and torch.equal(a.counts, b.counts)
-    # the bitset sweep, the sequential event-log variant and the rank-scatter sweep
-    # are the same machine
+    # the fused bitset sweep, the sequential event-log variant, the rank-scatter sweep
+    # and the legacy pre-generated-stream sweep are the same machine
     assert torch.equal(a.metrics, c.metrics) and torch.equal(a.counts, c.counts)
     assert torch.equal(a.metrics, d.metrics) and torch.equal(a.counts, d.counts)
+    assert torch.equal(a.metrics, e.metrics) and torch.equal(a.counts, e.counts)
+    assert torch.equal(a.status, e.status)
     assert int(a.status.sum().item()) == 0
     ev = a.n_events.double().mean().item()
     assert 4800 < ev < 6200, ev
@@ -239,3 +244,32 @@ def test_fast_sweep_equal_times_disjoint_sinks():
         assert int(res.status[0].item()) & 4   # the ties were seen
         met_o, t_o, s_o = _oracle(O, so, ("opt", seed), Ks)
         _cmp_replica(res, 0, met_o, t_o, s_o, Ks)
+
+
+@pytest.mark.parametrize("Ks", [(1,), (1, 3)])
+def test_fused_window_equal_time_blocks(Ks):
+    """Tile formation when many arrivals share one time: a RealData wall with 300
+    arrivals at t=5 (more than a ring, a window and a tile hold), runs of 40 at
+    other times, and Poisson / Hawkes walls around them.  The fused windowed
+    sweep (sweep_mode=1) must play exactly the events, rows and TIE flags of the
+    legacy serial-merge sweep (sweep_mode=4) -- both keep the last of equal-time
+    rows, so both differ from the reference's averaged pivot cells here.
+    (sweep_mode 5 = mode 1 on the legacy kernels.)"""
+    torch, engine, graphs, O = _ctx()
+    T = np.sort(np.concatenate([np.full(300, 5.0), np.full(40, 7.25), np.full(40, 2.0),
+                                np.linspace(0.5, 19.5, 77)]))
+    so = dict(src_id=1, end_time=20.0, s=np.asarray([1.0, 2.0, 0.5]), q=0.7, sink_ids=[10, 11, 12, 13],
+              other_sources=[("RealData", {"src_id": 2, "times": T.tolist()}),
+                             ("Poisson", {"src_id": 3, "seed": 5, "rate": 30.0}),
+                             ("Hawkes", {"src_id": 4, "seed": 9, "l_0": 5.0, "alpha": 2.0, "beta": 5.0}),
+                             ("RealData", {"src_id": 5, "times": [5.0] * 9 + [7.25, 9.0]})],
+              edge_list=[(1, 10), (1, 11), (1, 13), (2, 10), (2, 12), (3, 11), (4, 12), (4, 13),
+                         (5, 13), (5, 10)])
+    g = _graph(engine, so)
+    for seed in (1, 2, 3):
+        a = g.run("opt", q=so["q"], s=so["s"], n_rep=4, ctrl_seed=seed, Ks=Ks, sweep_mode=1)
+        b = g.run("opt", q=so["q"], s=so["s"], n_rep=4, ctrl_seed=seed, Ks=Ks, sweep_mode=5)
+        assert torch.equal(a.counts, b.counts)
+        assert torch.equal(a.metrics, b.metrics)
+        assert torch.equal(a.status, b.status)
+        assert int(a.status[0].item()) & 4
