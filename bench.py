@@ -60,6 +60,27 @@ def cpu_baseline(so, n_threads, sample, Ks=(1,)):
     return sample / el, tot / el, el
 
 
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_c3_pmc_summary.json")
+
+
+def pmc_traffic(workload, R, plan):
+    """HBM bytes per sweep launch from the committed rocprofv3 PMC summary of this
+    same command (scripts/gpu_pmc.sh -> scripts/pmc_summary.py: FETCH_SIZE x2 per
+    the gfx950 correction + WRITE_SIZE), when workload, replicas and plan match."""
+    try:
+        d = json.load(open(PMC_SUMMARY))
+    except (OSError, ValueError):
+        return None, None
+    meta = d.get("_meta", {})
+    if meta.get("workload") != workload or meta.get("replicas") != R or \
+            meta.get("variant") != plan["variant"]:
+        return None, None
+    for k, v in d.items():
+        if k.startswith("rq_sweep") and "hbm_write_bytes" in v and "hbm_read_bytes" in v:
+            return v["hbm_read_bytes"] + v["hbm_write_bytes"], os.path.relpath(PMC_SUMMARY, ROOT)
+    return None, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -105,30 +126,40 @@ def main():
         means = m.mean(0)
         return res, means, ev
 
-    # warmup (also sizes the workspace and checks for capacity overflow once)
-    L.lib().rq_timing(1)
-    for k in range(a.warmup):
-        res, means, ev = step(k + 10_000)
-    torch.cuda.synchronize()
+    # capacity check once (overflow -> the engine reruns with doubled capacities), then
+    # warmup at full size so the timed region starts with every buffer allocated
     ok = g.run("opt", q=so["q"], s=so["s"], n_rep=min(R, 512), ctrl_seed=0, world_seed=0,
                randomize=True, Ks=Ks, check=True)
     del ok
+    def accumulate(res, ev, acc):
+        acc[0] += ev
+        acc[1] += res.counts[:, 3].sum()
+        acc[2] += res.counts[:, 0].sum()
+        acc[3] |= (res.status & (L.ST_ROWS_OVERFLOW | L.ST_STREAM_OVERFLOW)).max()
+
+    def new_acc():
+        return [torch.zeros((), dtype=torch.int64, device=dev) for _ in range(3)] + \
+            [torch.zeros((), dtype=torch.int32, device=dev)]
+
+    # the warmup runs the exact timed body: HIP loads a kernel's code object on its first
+    # launch (tens of ms for torch's), which must not land in the timed region
+    L.lib().rq_timing(1)
+    acc = new_acc()
+    for k in range(max(1, a.warmup)):
+        res, means, ev = step(k + 10_000)
+        accumulate(res, ev, acc)
+    torch.cuda.synchronize()
 
     L.lib().rq_timing(1)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    total_ev = torch.zeros((), dtype=torch.int64, device=dev)
-    rows = torch.zeros((), dtype=torch.int64, device=dev)
-    posts = torch.zeros((), dtype=torch.int64, device=dev)
-    status = torch.zeros((), dtype=torch.int32, device=dev)
+    acc = new_acc()
     for k in range(a.steps):
         res, means, ev = step(k)
-        total_ev += ev
-        rows += res.counts[:, 3].sum()
-        posts += res.counts[:, 0].sum()
-        status |= (res.status & (L.ST_ROWS_OVERFLOW | L.ST_STREAM_OVERFLOW)).max()
+        accumulate(res, ev, acc)
+    total_ev, rows, posts, status = acc
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -158,13 +189,18 @@ def main():
     ev_rank = local_ev / world / a.steps
     rows_step = rows_l / a.steps
     posts_step = posts_l / a.steps
-    sweep_bytes = SWEEP_B_PER_WALL_EVENT * (ev_rank - posts_step) + SWEEP_B_PER_ROW * rows_step
+    # the fused sweep (variant >= 10) generates its arrivals in LDS: no arrival reads
+    fused = plan["variant"] >= 10
+    sweep_bytes = (0 if fused else SWEEP_B_PER_WALL_EVENT * (ev_rank - posts_step)) + \
+        SWEEP_B_PER_ROW * rows_step
     achieved = sweep_bytes / (sweep_ms * 1e-3) / 1e9
     scan_ms = ms[2] / max(1, int(nl[2]))
     gen_ms = ms[0] / max(1, int(nl[0]))
     scan_gbs = SCAN_B_PER_ROW * rows_step / (scan_ms * 1e-3) / 1e9 if scan_ms > 0 else None
     gen_gbs = GEN_B_PER_WALL_EVENT * (ev_rank - posts_step) / (gen_ms * 1e-3) / 1e9 \
         if gen_ms > 0 else None
+
+    traffic, traffic_src = pmc_traffic(a.workload, R, plan)
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
@@ -198,9 +234,11 @@ def main():
             "sweep_plan": plan,
             "roofline": {"bound": "hbm", "kernel": "rq_sweep", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": None,
-                         "note": "sweep is latency-bound (serial event chain per replica); "
-                                 "algorithmic bytes = 8 B/wall event + 24 B/pivot row"},
+                         "traffic": traffic,
+                         "traffic_source": traffic_src,
+                         "note": "sweep is latency/issue-bound (serial event chain per replica); "
+                                 "algorithmic bytes = 24 B/pivot row written%s" %
+                                 ("" if fused else " + 8 B/wall event read")},
             "scan_gbs": scan_gbs,
             "gen_gbs": gen_gbs,
             "cpu_baseline": cpu,

@@ -10,7 +10,7 @@ import os
 import torch  # noqa: F401  -- load torch's HIP runtime first so librq.so binds to it
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-SO_PATH = os.path.join(_HERE, "librq.so")
+SO_PATH = os.environ.get("RQ_SO_PATH") or os.path.join(_HERE, "librq.so")   # env: A/B builds only
 
 RQ_OK, RQ_EINVAL, RQ_EOVERFLOW, RQ_EHIP, RQ_ENOMEM, RQ_EUNSORTED, RQ_EUNSUPPORTED = (
     0, -1, -2, -3, -4, -5, -6)

@@ -648,17 +648,23 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
         std::lock_guard<std::mutex> lk(g->stage_mu);
         Stage& st = g->stage[g->stage_next];
         g->stage_next = (g->stage_next + 1) % kStages;
-        if (st.done && hipEventSynchronize(st.done) != hipSuccess) return RQ_EHIP;
         if (st.bytes < p.tables_bytes) {
-            if (st.buf) (void)hipHostFree(st.buf);
-            st.buf = nullptr;
-            st.bytes = 0;
-            if (hipHostMalloc(&st.buf, p.tables_bytes, hipHostMallocDefault) != hipSuccess)
-                return RQ_ENOMEM;
-            st.bytes = p.tables_bytes;
+            // grow the whole ring at once (pinned allocation is slow: never leave a stage
+            // to be allocated by a later, possibly timed, call); round up to 64 KiB
+            const size_t want = align_up(p.tables_bytes, (size_t)65536);
+            for (Stage& x : g->stage) {
+                if (x.done && hipEventSynchronize(x.done) != hipSuccess) return RQ_EHIP;
+                if (x.bytes >= want) continue;
+                if (x.buf) (void)hipHostFree(x.buf);
+                x.buf = nullptr;
+                x.bytes = 0;
+                if (hipHostMalloc(&x.buf, want, hipHostMallocDefault) != hipSuccess) return RQ_ENOMEM;
+                x.bytes = want;
+                if (!x.done && hipEventCreateWithFlags(&x.done, hipEventDisableTiming) != hipSuccess)
+                    return RQ_EHIP;
+            }
         }
-        if (!st.done && hipEventCreateWithFlags(&st.done, hipEventDisableTiming) != hipSuccess)
-            return RQ_EHIP;
+        if (st.done && hipEventSynchronize(st.done) != hipSuccess) return RQ_EHIP;
         char* tab = (char*)st.buf;
         std::memcpy(tab + p.off_invc, invc.data(), invc.size() * sizeof(double));
         std::memcpy(tab + p.off_stoff, p.st_off.data(), p.st_off.size() * sizeof(int64_t));

@@ -504,7 +504,10 @@ __global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
 //     posts) give each event's top-1 set, plain prefix ORs its valid set.
 // ============================================================================
 template <int NK, class COL, int W, int H, bool BITS>
-__global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
+#ifndef RQ_FW_WPE
+#define RQ_FW_WPE 4
+#endif
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(RQ_FW_WPE))) void rq_sweep_fw(SweepArgs a)
 {
     static_assert((W & (W - 1)) == 0 && H <= W, "ring");
     extern __shared__ double lds_g[];

@@ -1,0 +1,24 @@
+#!/bin/bash
+# PMC passes on the bench workload (one counter group per rocprofv3 run, as the
+# gfx950 slot limits require) + a kernel-trace pass; summary -> gpurun_out/pmc_TAG/summary.json
+# usage: scripts/gpu_pmc.sh TAG [bench args...]
+set -o pipefail
+TAG=${1:-run}; shift
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out/pmc_$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+cd "$ROOT"
+B="bench.py --steps 3 --warmup 1 --no-cpu $*"
+P="--output-format csv"
+timeout -k 10 -s KILL 200 rocprofv3 --kernel-trace --stats $P -d "$OUT/kt" -o kt -- python3 $B > "$OUT/kt.log" 2>&1 || { echo kt failed; tail -5 "$OUT/kt.log"; exit 1; }
+echo "kt ok"
+timeout -k 10 -s KILL 120 rocprofv3 --pmc FETCH_SIZE $P -d "$OUT/p3" -o p3 -- python3 $B > "$OUT/p3.log" 2>&1 || { echo p3 failed; tail -5 "$OUT/p3.log"; exit 1; }
+echo "fetch ok"
+timeout -k 10 -s KILL 120 rocprofv3 --pmc WRITE_SIZE $P -d "$OUT/p4" -o p4 -- python3 $B > "$OUT/p4.log" 2>&1 || { echo p4 failed; tail -5 "$OUT/p4.log"; exit 1; }
+echo "write ok"
+timeout -k 10 -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU $P -d "$OUT/p1" -o p1 -- python3 $B > "$OUT/p1.log" 2>&1 || { echo p1 failed; tail -5 "$OUT/p1.log"; exit 1; }
+echo "sq1 ok"
+timeout -k 10 -s KILL 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT $P -d "$OUT/p2" -o p2 -- python3 $B > "$OUT/p2.log" 2>&1 || { echo p2 failed; tail -5 "$OUT/p2.log"; exit 1; }
+echo "sq2 ok"
+python3 scripts/pmc_summary.py "$OUT" > "$OUT/summary.txt" && cat "$OUT/summary.txt"

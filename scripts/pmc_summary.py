@@ -1,12 +1,50 @@
-"""Summarise rocprofv3 counter_collection CSVs: mean per dispatch for each kernel."""
-import csv, glob, sys, collections
+"""Summarise rocprofv3 counter_collection CSVs for the bench's full-size launches.
+
+For each kernel, keeps only the dispatches with the largest grid (the bench's
+timed launches; the small check launch is dropped) and reports the mean of
+each counter per dispatch, plus VGPR/SGPR/LDS of the code object and the
+corrected HBM bytes (FETCH_SIZE is in KiB and counts a 128-B read as 64 B on
+gfx950 -> x2; WRITE_SIZE in KiB, exact for wide stores; MI355X_MICROARCH.md
+'HBM / rocprofv3').  Writes summary.json beside the CSVs.
+usage: python scripts/pmc_summary.py DIR
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
 root = sys.argv[1]
-agg = collections.defaultdict(lambda: collections.defaultdict(list))
+rows = collections.defaultdict(list)
 for f in glob.glob(root + "/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"].split("(")[0][:40]
-        agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
-for k, d in agg.items():
-    print(k)
-    for c, v in sorted(d.items()):
-        print("   %-22s %.4g" % (c, sum(v) / len(v)))
+        rows[r["Kernel_Name"].split("(")[0].replace("void ", "")].append(r)
+out = {}
+for k, rs in rows.items():
+    gmax = max(int(r["Grid_Size"]) for r in rs)
+    big = [r for r in rs if int(r["Grid_Size"]) == gmax]
+    agg = collections.defaultdict(list)
+    for r in big:
+        agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    d = {c: sum(v) / len(v) for c, v in agg.items()}
+    r0 = big[0]
+    info = {"grid": gmax, "wg": int(r0["Workgroup_Size"]), "vgpr": int(r0.get("VGPR_Count", 0) or 0),
+            "agpr": int(r0.get("Accum_VGPR_Count", 0) or 0), "sgpr": int(r0.get("SGPR_Count", 0) or 0),
+            "lds": int(r0.get("LDS_Block_Size", 0) or 0), "counters": d}
+    if "FETCH_SIZE" in d:
+        info["hbm_read_bytes"] = d["FETCH_SIZE"] * 1024 * 2
+    if "WRITE_SIZE" in d:
+        info["hbm_write_bytes"] = d["WRITE_SIZE"] * 1024
+    if "SQ_WAVE_CYCLES" in d and d["SQ_WAVE_CYCLES"] > 0:
+        wc = d["SQ_WAVE_CYCLES"]
+        info["frac_active_inst"] = d.get("SQ_ACTIVE_INST_ANY", 0) / wc
+        info["frac_wait_any"] = d.get("SQ_WAIT_ANY", 0) / wc
+        info["frac_wait_inst"] = d.get("SQ_WAIT_INST_ANY", 0) / wc
+    out[k] = info
+json.dump(out, open(os.path.join(root, "summary.json"), "w"), indent=1)
+for k, v in out.items():
+    if k.startswith("rq_"):
+        print(k, json.dumps({a: b for a, b in v.items() if a != "counters"}))
+        for c, x in sorted(v["counters"].items()):
+            print("   %-22s %.6g" % (c, x))
