@@ -24,6 +24,12 @@
  *                       utils.int_r_2(df, ...)              utils.py:117-121
  *                       utils.num_tweets_of(df, ...)        utils.py:170-176
  *                       on a dataframe in the reference's row layout.
+ *   rq_oracle_dp        utils.oracle_ranking(df, sim_opts)  utils.py:181-245
+ *                       (batched over walls / q values: the loops of
+ *                       find_opt_oracle :260-340 and opt_runs.worker_oracle
+ *                       opt_runs.py:129-155)
+ *   rq_rank_table       utils.rank_of_src_in_df(df, src)    utils.py:38-56
+ *   rq_u_int            utils.u_int_opt(df, ...)            utils.py:59-81
  *
  * Conventions
  *   - every function returns 0 (RQ_OK) or a negative rq_status; no C++
@@ -199,6 +205,36 @@ int rq_metrics_replay(const double* t, const int64_t* src, const int32_t* sink_c
                       int64_t src_id, double end_time, const int32_t* Ks, int32_t nK,
                       double* out, int64_t* counts, void* workspace, size_t workspace_bytes,
                       void* hip_stream);
+
+/* Offline oracle (utils.oracle_ranking) for n_inst single-follower walls at once.
+ * Instance i: n_i wall events, w_i[0..n_i+2) = np.diff([0, 0, event_times..., end_time])
+ * (utils.py:207), q_i, s_i.  Device arrays: w (instances concatenated), w_off[n_inst+1]
+ * (prefix of n_i + 2), q[n_inst], s[n_inst], out_off[n_inst+1] (prefix of n_i + 1).
+ * Outputs (device): cost[i] = J[0, 0]; events / ranks [out_off[i] .. + n_i + 1) = the
+ * oracle_df 'events' and 'ranks' columns.  n_max >= every n_i (<= 1e6, the reference's
+ * own limit); workspace: rq_oracle_workspace_size (n_inst (n_max+1)^2 / 8 bytes of
+ * decision bits). */
+int rq_oracle_workspace_size(int32_t n_inst, int64_t n_max, size_t* bytes);
+int rq_oracle_dp(const double* w, const int64_t* w_off, const double* q, const double* s,
+                 int32_t n_inst, int64_t n_max, double* cost, int32_t* events, int32_t* ranks,
+                 const int64_t* out_off, void* workspace, size_t workspace_bytes, void* hip_stream);
+
+/* rank_of_src_in_df: table[n_t][n_cols] (device) of the rank of src_id in every sink's
+ * feed at every unique t (index[n_t], device); cells = mean of the (t, sink) ranks, then
+ * forward-filled per column when fill != 0 (NaN before a sink's first row / without fill).
+ * Rows in df order, t non-decreasing; n_t = number of unique t.  err (device int32[1]):
+ * 0 ok, bit 0 t not sorted, bit 1 n_t wrong. */
+int rq_rank_table(const double* t, const int64_t* src, const int32_t* sink_col, int64_t n_rows,
+                  int32_t n_cols, int64_t src_id, int32_t fill, int64_t n_t, double* table,
+                  double* index, int32_t* err, void* hip_stream);
+
+/* u_int_opt from a filled rank table: sum_k (sum_f table[k, fcol[f]] * wts[f]) * dt_k with
+ * dt_k = index[k+1] - index[k] (end_time - index[n_t-1] last), numpy pairwise sum.
+ * wts = sqrt(s / q) per follower (device), fcol their table columns (device).
+ * out: device double[1]; workspace >= n_t * 8 bytes. */
+int rq_u_int(const double* table, const double* index, int64_t n_t, int32_t n_cols,
+             const int32_t* fcol, const double* wts, int32_t n_f, double end_time, double* out,
+             void* workspace, size_t workspace_bytes, void* hip_stream);
 
 /* Per-kernel timing for benchmarks: rq_timing(1) starts recording HIP events
  * around every kernel this library launches (on the caller's stream);

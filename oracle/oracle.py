@@ -78,6 +78,11 @@ def lib():
         L.rqo_engine_batch.restype = C.c_int64
         L.rqo_engine_batch.argtypes = [C.POINTER(_Scenario), C.c_int64, C.c_uint32, C.c_int32,
                                        i32, C.c_int32, C.c_int32, d, C.c_uint32, d, i64]
+        L.rqo_oracle_dp.restype = C.c_int
+        L.rqo_oracle_dp.argtypes = [d, C.c_int64, C.c_double, C.c_double, d, i64, i64]
+        L.rqo_rank_table.restype = C.c_int
+        L.rqo_rank_table.argtypes = [d, i64, i32, C.c_int64, C.c_int32, C.c_int64, C.c_int32,
+                                     C.c_int64, d, d]
         L.rqo_spec_log.restype = C.c_double
         L.rqo_spec_log.argtypes = [C.c_double]
         L.rqo_spec_exp.restype = C.c_double
@@ -111,6 +116,38 @@ def metrics_df(t, src, sink, event_id, src_id, end_time, Ks=(1,), row_mode=0):
     if rc:
         raise ValueError("rqo_metrics_df failed: %d" % rc)
     return list(out[:len(Ks)]), out[len(Ks)], out[len(Ks) + 1], cnt
+
+
+def oracle_dp(w, q, s):
+    """utils.oracle_ranking's DP on w = np.diff([0, 0, times..., end]) (n = len(w) - 2).
+    Returns (cost, events[n+1], ranks[n+1])."""
+    w = np.ascontiguousarray(w, dtype=np.float64)
+    n = w.size - 2
+    ev = np.zeros(n + 1, dtype=np.int64)
+    rk = np.zeros(n + 1, dtype=np.int64)
+    cost = C.c_double()
+    rc = lib().rqo_oracle_dp(_p(w, C.c_double), n, float(q), float(s), C.byref(cost),
+                             _p(ev, C.c_int64), _p(rk, C.c_int64))
+    if rc:
+        raise ValueError("rqo_oracle_dp failed: %d" % rc)
+    return cost.value, ev, rk
+
+
+def rank_table(t, src, sink, src_id, fill=True):
+    """utils.rank_of_src_in_df -> (table [n_t][S], index [n_t], sorted sink ids)."""
+    t = np.ascontiguousarray(t, dtype=np.float64)
+    src = np.ascontiguousarray(src, dtype=np.int64)
+    sinks, col = np.unique(np.asarray(sink), return_inverse=True)
+    col = np.ascontiguousarray(col, dtype=np.int32)
+    n_t = int(np.unique(t).size)
+    tab = np.zeros((n_t, sinks.size))
+    idx = np.zeros(n_t)
+    rc = lib().rqo_rank_table(_p(t, C.c_double), _p(src, C.c_int64), _p(col, C.c_int32), t.size,
+                              sinks.size, int(src_id), int(bool(fill)), n_t, _p(tab, C.c_double),
+                              _p(idx, C.c_double))
+    if rc:
+        raise ValueError("rqo_rank_table failed: %d" % rc)
+    return tab, idx, sinks
 
 
 def mt_draws(seed, kind, p=0.0, q=0.0, n=16):

@@ -123,6 +123,15 @@ int64_t rqo_engine_batch(const rqo_scenario* sc, int64_t n_rep, uint32_t seed0,
                          int32_t n_threads, const double* ctrl_rates, uint32_t ctrl_seed_offset,
                          double* out, int64_t* counts);
 
+/* rq_oracle_analysis.c: utils.oracle_ranking (utils.py:181-245) on w[0..n+2)
+ * = np.diff([0, 0, event_times..., end_time]); events/ranks [n+1]. */
+int rqo_oracle_dp(const double* w, int64_t n, double q, double s, double* cost,
+                  int64_t* events, int64_t* ranks);
+/* utils.rank_of_src_in_df (utils.py:38-56): table [n_t][n_cols], index [n_t] */
+int rqo_rank_table(const double* t, const int64_t* src, const int32_t* col, int64_t n_rows,
+                   int32_t n_cols, int64_t src_id, int32_t fill, int64_t n_t, double* table,
+                   double* index);
+
 /* the engine's arithmetic spec (redqueen_amd/csrc/rq_spec.h), exported for tests */
 double rqo_spec_log(double x);
 double rqo_spec_exp(double x);

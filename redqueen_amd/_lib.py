@@ -88,11 +88,19 @@ def lib():
     L.rq_replay_workspace_size.argtypes = [C.c_int64, C.c_int32, C.POINTER(C.c_size_t)]
     L.rq_metrics_replay.argtypes = [_P, _P, _P, _P, C.c_int64, C.c_int32, C.c_int64, C.c_double,
                                     _pi32, C.c_int32, _P, _P, _P, C.c_size_t, _P]
+    L.rq_oracle_workspace_size.argtypes = [C.c_int32, C.c_int64, C.POINTER(C.c_size_t)]
+    L.rq_oracle_dp.argtypes = [_P, _P, _P, _P, C.c_int32, C.c_int64, _P, _P, _P, _P, _P,
+                               C.c_size_t, _P]
+    L.rq_rank_table.argtypes = [_P, _P, _P, C.c_int64, C.c_int32, C.c_int64, C.c_int32,
+                                C.c_int64, _P, _P, _P, _P]
+    L.rq_u_int.argtypes = [_P, _P, C.c_int64, C.c_int32, _P, _P, C.c_int32, C.c_double, _P, _P,
+                           C.c_size_t, _P]
     L.rq_timing.argtypes = [C.c_int]
     L.rq_timing_read.argtypes = [_pd, _pi64]
     for fn in ("rq_timing", "rq_timing_read", "rq_graph_build", "rq_graph_free", "rq_graph_info", "rq_graph_source_ids",
                "rq_graph_followers", "rq_workspace_size", "rq_event_capacity", "rq_run_batch",
-               "rq_replay_workspace_size", "rq_metrics_replay"):
+               "rq_replay_workspace_size", "rq_metrics_replay", "rq_oracle_workspace_size",
+               "rq_oracle_dp", "rq_rank_table", "rq_u_int"):
         getattr(L, fn).restype = C.c_int
     if L.rq_abi_version() != 1:
         raise ImportError("librq.so ABI version mismatch")
@@ -115,4 +123,5 @@ def check(fn, code):
 EXPORTED = ["rq_abi_version", "rq_strerror", "rq_graph_build", "rq_graph_free", "rq_graph_info",
             "rq_graph_source_ids", "rq_graph_followers", "rq_workspace_size",
             "rq_event_capacity", "rq_plan_info", "rq_run_batch", "rq_replay_workspace_size",
-            "rq_metrics_replay", "rq_timing", "rq_timing_read"]
+            "rq_metrics_replay", "rq_oracle_workspace_size", "rq_oracle_dp", "rq_rank_table",
+            "rq_u_int", "rq_timing", "rq_timing_read"]

@@ -1,0 +1,231 @@
+// rq_analysis.hip -- gfx950 kernels for the analysis side of the hot path:
+//
+//   rq_oracle_dp    utils.oracle_ranking (utils.py:181-245): the offline
+//                   oracle's backward dynamic program over a single-follower
+//                   wall, J[r,k] = min(q/2 + J[0,k+1], s/2 w[k+1] (r+1)^2 +
+//                   J[r+1,k+1]), then its forward policy walk.
+//   rq_rank_table   utils.rank_of_src_in_df (utils.py:38-56): per-sink rank
+//                   scan, pivot on unique t with the mean of duplicate
+//                   (t, sink) cells, optional per-column forward fill.
+//   rq_u_int        utils.u_int_opt (utils.py:59-81): rows of the rank table
+//                   dotted with sqrt(s/q) over the followers, times dt,
+//                   summed in numpy's pairwise order.
+//
+// None of these is a dense contraction (no MFMA); they are latency / HBM bound
+// and laid out so that every global access of a wavefront is contiguous.
+#include <hip/hip_runtime.h>
+
+#include "rq_device.h"
+#include "rq_internal.h"
+
+#pragma clang fp contract(off)
+
+using namespace rq;
+
+// ============================================================================
+// 1. oracle DP.  One workgroup per instance (a wall of n events, its own q, s).
+//    Column k of J depends only on column k+1, so the columns run from k = n
+//    down to 0 with one barrier each; rows r < min(k+1, n) are spread over the
+//    threads.  Two column buffers (LDS when they fit, else global) alternate.
+//    The decision lhs < rhs of every (r, k) is kept as one bit (ballot of a
+//    wavefront's 64 consecutive rows), so the forward walk
+//    (utils.py:230-238) needs no second pass over J:  n^2/8 bytes per instance.
+//    Exactness: the reference evaluates 0.5*q + J[0,k+1] and
+//    ((0.5*s)*w[k+1])*float((r+1)**2) + J[r+1,k+1] and keeps the first
+//    argument of min() unless the second is strictly smaller -- restated
+//    literally (no FMA: contract(off)).
+//    Quirk kept: J is zero-initialised and row n of column n is never written,
+//    so column n-1 reads J[n, n] = 0 (not n^2/2).
+// ============================================================================
+template <bool LDS>
+__global__ __launch_bounds__(1024) void rq_oracle_dp_k(OracleArgs a)
+{
+    extern __shared__ double lds_od[];
+    const int inst = blockIdx.x;
+    const int64_t w0 = a.w_off[inst];
+    const int64_t n = a.w_off[inst + 1] - w0 - 2;
+    const double* w = a.w + w0;
+    const double q = a.q[inst];
+    const double s = a.s[inst];
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const int64_t wpc = (n + 1 + 63) / 64;                    // 64-bit words per column
+    uint64_t* bits = a.bits + (size_t)inst * a.bits_stride;   // [n+1 columns][wpc]
+    double* c0 = LDS ? lds_od : a.gcol + (size_t)inst * 2 * (a.n_max + 2);
+    double* c1 = c0 + (n + 2);
+    if (n < 0) return;
+
+    // column n+1: J[r, n+1] = r**2 / 2 (np.arange(n + 1) ** 2 / 2)
+    for (int64_t r = tid; r <= n; r += nt) c0[r] = (double)(r * r) / 2.0;
+    __syncthreads();
+    double* cur = c0;   // column k+1
+    double* nxt = c1;   // column k
+    const double hq = 0.5 * q;
+    const double hs = 0.5 * s;
+    for (int64_t k = n; k >= 0; --k) {
+        const int64_t m = (k + 1 < n) ? k + 1 : n;   // rows written in column k
+        const double lhs = hq + cur[0];
+        const double ck = hs * w[k + 1];
+        // rows are swept by whole wavefronts so each ballot covers 64 consecutive rows
+        for (int64_t rb = (int64_t)(tid & ~63); rb < m; rb += nt) {
+            const int64_t r = rb + (tid & 63);
+            bool post = false;
+            if (r < m) {
+                const double r1 = (double)((r + 1) * (r + 1));
+                const double rhs = ck * r1 + cur[r + 1];
+                post = lhs < rhs;
+                nxt[r] = (rhs < lhs) ? rhs : lhs;     // Python min(lhs, rhs)
+            }
+            const uint64_t b = __ballot(post);
+            if ((tid & 63) == 0) bits[k * wpc + (rb >> 6)] = b;
+        }
+        // row n of column n: J[n, n] = 0, never written by the reference (column n-1
+        // reads it); the other rows >= m of a column are never read again
+        if (tid == 0 && k == n) nxt[n] = 0.0;
+        __syncthreads();
+        double* tmp = cur;
+        cur = nxt;
+        nxt = tmp;
+    }
+    // forward policy walk (utils.py:230-238): one lane, decisions from the bits
+    if (tid == 0) {
+        const int64_t o = a.out_off[inst];
+        a.cost[inst] = cur[0];   // J[0, 0]
+        int64_t rk = 0;
+        a.ranks[o] = 0;
+        for (int64_t k = 0; k < n; ++k) {
+            const uint64_t word = bits[k * wpc + (rk >> 6)];
+            const bool post = (word >> (rk & 63)) & 1ull;
+            a.events[o + k] = post ? 1 : 0;
+            rk = post ? 0 : rk + 1;
+            a.ranks[o + k + 1] = (int32_t)rk;
+        }
+        a.events[o + n] = 0;
+    }
+}
+
+hipError_t rq_launch_oracle_dp(const OracleArgs& a, bool lds, hipStream_t s)
+{
+    if (a.n_inst <= 0) return hipSuccess;
+    const int nt = a.n_max + 1 >= 4096 ? 1024 : 256;
+    if (lds) {
+        const size_t bytes = 2 * (size_t)(a.n_max + 2) * sizeof(double);
+        hipLaunchKernelGGL(rq_oracle_dp_k<true>, dim3(a.n_inst), dim3(nt), bytes, s, a);
+    } else {
+        hipLaunchKernelGGL(rq_oracle_dp_k<false>, dim3(a.n_inst), dim3(nt), 0, s, a);
+    }
+    return hipGetLastError();
+}
+
+// ============================================================================
+// 2. rank table.  One wavefront per 64 sink columns; lane c owns column
+//    blockIdx*64 + c.  The rows (df order, t non-decreasing) are read 64 at a
+//    time, coalesced, and walked in order with register broadcasts: the owning
+//    lane advances its column's position / last-own-post counters
+//    (steps_to, utils.py:43-46) and accumulates the (t, sink) cell; when t
+//    changes every lane emits its cell for the finished t -- the mean of the
+//    cell's ranks, else (fill) the column's previous value, else NaN -- so a
+//    table row is one 8*64-byte contiguous store per wavefront.
+// ============================================================================
+__global__ __launch_bounds__(64) void rq_rank_table_k(RankTableArgs a)
+{
+    const int lane = lane_id();
+    const int64_t c = (int64_t)blockIdx.x * 64 + lane;
+    const bool own_col = c < a.n_cols;
+    const double NaN = __builtin_nan("");
+    int64_t pos = 0, last = 0;
+    double csum = 0.0;
+    int ccnt = 0;
+    double prev = NaN;           // the column's last value (ffill)
+    int64_t row = -1;            // table row of the current t
+    double cur_t = 0.0;
+    int err = 0;
+    auto emit = [&]() {
+        double v;
+        if (ccnt > 0) {
+            v = csum / (double)ccnt;
+            prev = v;
+        } else {
+            v = a.fill ? prev : NaN;
+        }
+        if (own_col && row < a.n_t) a.table[row * a.n_cols + c] = v;
+        if (lane == 0 && row < a.n_t && blockIdx.x == 0) a.index[row] = cur_t;
+        csum = 0.0;
+        ccnt = 0;
+    };
+    for (int64_t i0 = 0; i0 < a.n_rows; i0 += 64) {
+        const int64_t i = i0 + lane;
+        double ti = 0.0;
+        int key = -1;   // col * 2 + (src == src_id)
+        if (i < a.n_rows) {
+            ti = a.t[i];
+            key = a.col[i] * 2 + (a.src[i] == a.src_id ? 1 : 0);
+        }
+        const int cnt = (int)((a.n_rows - i0) < 64 ? (a.n_rows - i0) : 64);
+        for (int j = 0; j < cnt; ++j) {
+            const double tj = __shfl(ti, j, 64);
+            const int kj = __shfl(key, j, 64);
+            if (row < 0 || tj != cur_t) {
+                if (row >= 0) {
+                    if (tj < cur_t) err = 1;   // df not sorted by t
+                    emit();
+                }
+                ++row;
+                cur_t = tj;
+            }
+            if ((int64_t)(kj >> 1) == c) {
+                ++pos;
+                if (kj & 1) last = pos;
+                csum += (double)(pos - last);
+                ++ccnt;
+            }
+        }
+    }
+    if (row >= 0) emit();
+    if (lane == 0 && blockIdx.x == 0) {
+        if (row + 1 != a.n_t) err |= 2;
+        a.err[0] = err;
+    }
+}
+
+hipError_t rq_launch_rank_table(const RankTableArgs& a, hipStream_t s)
+{
+    const unsigned blocks = (unsigned)((a.n_cols + 63) / 64);
+    hipLaunchKernelGGL(rq_rank_table_k, dim3(blocks), dim3(64), 0, s, a);
+    return hipGetLastError();
+}
+
+// ============================================================================
+// 3. u_int_opt.  Row k of the rank table: u_k = sum_f table[k, col_f] * w_f
+//    (follower order), x_k = u_k * dt_k with dt_k = t_{k+1} - t_k and the last
+//    one end_time - t_last (np.diff(concatenate([index, [end_time]]))); the
+//    result is numpy's pairwise np.sum of x (one wavefront, wave_npsum).
+//    NaN ranks (a follower with no row yet) propagate exactly as in numpy.
+// ============================================================================
+__global__ __launch_bounds__(256) void rq_u_int_rows_k(UIntArgs a)
+{
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= a.n_t) return;
+    double u = 0.0;
+    for (int f = 0; f < a.n_f; ++f) u = u + a.table[k * a.n_cols + a.fcol[f]] * a.wts[f];
+    const double dt = (k + 1 < a.n_t ? a.index[k + 1] : a.end) - a.index[k];
+    a.x[k] = u * dt;
+}
+
+__global__ __launch_bounds__(64) void rq_u_int_sum_k(UIntArgs a)
+{
+    extern __shared__ double lds_ui[];
+    double out[1];
+    const double* x = a.x;
+    wave_npsum<1>(a.n_t, [&](int64_t k, double v[1]) { v[0] = x[k]; }, lds_ui, out);
+    if (lane_id() == 0) a.out[0] = out[0];
+}
+
+hipError_t rq_launch_u_int(const UIntArgs& a, hipStream_t s)
+{
+    if (a.n_t > 0) {
+        hipLaunchKernelGGL(rq_u_int_rows_k, dim3((unsigned)((a.n_t + 255) / 256)), dim3(256), 0, s, a);
+        if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
+    }
+    hipLaunchKernelGGL(rq_u_int_sum_k, dim3(1), dim3(64), npsum_lds_doubles<1>() * sizeof(double), s, a);
+    return hipGetLastError();
+}

@@ -933,3 +933,102 @@ int rq_metrics_replay(const double* t, const int64_t* src, const int32_t* sink_c
 }
 
 }  // extern "C"
+
+// ============================================================================
+// analysis entry points (rq_analysis.hip)
+// ============================================================================
+namespace {
+constexpr size_t kOracleLdsMax = 128 * 1024;
+size_t oracle_bits_stride(int64_t n_max) { return (size_t)(n_max + 1) * (size_t)((n_max + 1 + 63) / 64); }
+bool oracle_lds(int64_t n_max) { return 2 * (size_t)(n_max + 2) * sizeof(double) <= kOracleLdsMax; }
+}  // namespace
+
+extern "C" {
+
+int rq_oracle_workspace_size(int32_t n_inst, int64_t n_max, size_t* bytes)
+{
+    if (!bytes || n_inst < 0 || n_max < 0 || n_max > 1000000) return RQ_EINVAL;
+    size_t b = align_up((size_t)n_inst * oracle_bits_stride(n_max) * sizeof(uint64_t), 256);
+    if (!oracle_lds(n_max)) b += (size_t)n_inst * 2 * (size_t)(n_max + 2) * sizeof(double);
+    *bytes = std::max<size_t>(b, 256);
+    return RQ_OK;
+}
+
+int rq_oracle_dp(const double* w, const int64_t* w_off, const double* q, const double* s,
+                 int32_t n_inst, int64_t n_max, double* cost, int32_t* events, int32_t* ranks,
+                 const int64_t* out_off, void* workspace, size_t workspace_bytes, void* hip_stream)
+{
+    if (n_inst < 0) return RQ_EINVAL;
+    if (n_inst == 0) return RQ_OK;
+    if (!w || !w_off || !q || !s || !cost || !events || !ranks || !out_off || !workspace) return RQ_EINVAL;
+    size_t need = 0;
+    const int rc = rq_oracle_workspace_size(n_inst, n_max, &need);
+    if (rc != RQ_OK) return rc;
+    if (workspace_bytes < need) return RQ_EINVAL;
+    OracleArgs a{};
+    a.w = w;
+    a.w_off = w_off;
+    a.q = q;
+    a.s = s;
+    a.n_inst = n_inst;
+    a.n_max = n_max;
+    a.cost = cost;
+    a.events = events;
+    a.ranks = ranks;
+    a.out_off = out_off;
+    a.bits = (uint64_t*)workspace;
+    a.bits_stride = (int64_t)oracle_bits_stride(n_max);
+    a.gcol = (double*)((char*)workspace +
+                       align_up((size_t)n_inst * oracle_bits_stride(n_max) * sizeof(uint64_t), 256));
+    hipStream_t st = (hipStream_t)hip_stream;
+    TimedLaunch tl(K_REPLAY, st);
+    return rq_launch_oracle_dp(a, oracle_lds(n_max), st) == hipSuccess ? RQ_OK : RQ_EHIP;
+}
+
+int rq_rank_table(const double* t, const int64_t* src, const int32_t* sink_col, int64_t n_rows,
+                  int32_t n_cols, int64_t src_id, int32_t fill, int64_t n_t, double* table,
+                  double* index, int32_t* err, void* hip_stream)
+{
+    if (!t || !src || !sink_col || !table || !index || !err) return RQ_EINVAL;
+    if (n_rows < 1 || n_cols < 1 || n_t < 1 || n_t > n_rows) return RQ_EINVAL;
+    RankTableArgs a{};
+    a.t = t;
+    a.src = src;
+    a.col = sink_col;
+    a.n_rows = n_rows;
+    a.n_cols = n_cols;
+    a.src_id = src_id;
+    a.fill = fill ? 1 : 0;
+    a.n_t = n_t;
+    a.table = table;
+    a.index = index;
+    a.err = err;
+    hipStream_t st = (hipStream_t)hip_stream;
+    TimedLaunch tl(K_REPLAY, st);
+    return rq_launch_rank_table(a, st) == hipSuccess ? RQ_OK : RQ_EHIP;
+}
+
+int rq_u_int(const double* table, const double* index, int64_t n_t, int32_t n_cols,
+             const int32_t* fcol, const double* wts, int32_t n_f, double end_time, double* out,
+             void* workspace, size_t workspace_bytes, void* hip_stream)
+{
+    if (!table || !index || !out || !workspace || n_t < 1 || n_cols < 1 || n_f < 0) return RQ_EINVAL;
+    if (n_f > 0 && (!fcol || !wts)) return RQ_EINVAL;
+    if (workspace_bytes < (size_t)n_t * sizeof(double)) return RQ_EINVAL;
+    UIntArgs a{};
+    a.table = table;
+    a.index = index;
+    a.n_t = n_t;
+    a.n_cols = n_cols;
+    a.fcol = fcol;
+    a.wts = wts;
+    a.n_f = n_f;
+    a.end = end_time;
+    a.x = (double*)workspace;
+    a.out = out;
+    hipStream_t st = (hipStream_t)hip_stream;
+    TimedLaunch tl(K_SCAN, st);
+    return rq_launch_u_int(a, st) == hipSuccess ? RQ_OK : RQ_EHIP;
+}
+
+}  // extern "C"

@@ -125,3 +125,50 @@ struct ReplayArgs {
     int32_t* err;           // out [1]: 0 ok, 1 unsorted t
 };
 hipError_t rq_launch_replay(const ReplayArgs& a, int nK, hipStream_t s);
+
+// ---- analysis kernels (rq_analysis.hip) ----
+struct OracleArgs {
+    const double* w;          // device, concatenated per instance: w[n_i + 2]
+    const int64_t* w_off;     // device [n_inst + 1]
+    const double* q;          // device [n_inst]
+    const double* s;          // device [n_inst]
+    int n_inst;
+    int64_t n_max;
+    double* cost;             // device [n_inst]
+    int32_t* events;          // device, concatenated [n_i + 1]
+    int32_t* ranks;           // device, concatenated [n_i + 1]
+    const int64_t* out_off;   // device [n_inst + 1]
+    uint64_t* bits;           // workspace [n_inst][bits_stride]
+    int64_t bits_stride;
+    double* gcol;             // workspace [n_inst][2][n_max + 2] (global-column mode)
+};
+hipError_t rq_launch_oracle_dp(const OracleArgs& a, bool lds, hipStream_t s);
+
+struct RankTableArgs {
+    const double* t;
+    const int64_t* src;
+    const int32_t* col;
+    int64_t n_rows;
+    int n_cols;
+    int64_t src_id;
+    int fill;
+    int64_t n_t;
+    double* table;            // [n_t][n_cols]
+    double* index;            // [n_t]
+    int32_t* err;             // [1]: 1 unsorted t, 2 n_t mismatch
+};
+hipError_t rq_launch_rank_table(const RankTableArgs& a, hipStream_t s);
+
+struct UIntArgs {
+    const double* table;
+    const double* index;
+    int64_t n_t;
+    int n_cols;
+    const int32_t* fcol;
+    const double* wts;
+    int n_f;
+    double end;
+    double* x;                // workspace [n_t]
+    double* out;              // [1]
+};
+hipError_t rq_launch_u_int(const UIntArgs& a, hipStream_t s);

@@ -8,9 +8,17 @@ pairwise sums).  The only host work is handing the
 columns over: the df's sink ids are factorised into pivot-column indices
 (np.unique) and the columns are copied to device memory.
 ``calc_q_capacity_iter`` (utils.py:447-470) runs its seeds as one GPU batch.
+
+Analysis helpers on the same footing: ``rank_of_src_in_df`` (utils.py:38-56)
+and ``u_int_opt`` (:59-81) run ``rq_rank_table`` / ``rq_u_int``;
+``oracle_ranking`` (:181-245) runs the oracle's O(n^2) dynamic program as
+``rq_oracle_dp`` (one workgroup per wall, batched over walls / q values), and
+``get_oracle_df`` / ``find_opt_oracle`` (:248-340) and ``sweep_q`` (:521-607)
+keep the reference's control flow around GPU batches.
 """
 import ctypes as C
 import datetime as D
+import logging
 import sys
 
 import numpy as np
@@ -135,3 +143,355 @@ def calc_q_capacity_iter(sim_opts, q, seeds=None, parallel=True, dynamic=True, m
     res = g.run("opt", q=float(q), s=sim_opts.s, n_rep=len(seeds),
                 ctrl_seed=torch.as_tensor(seeds), max_events=max_events)
     return res.num_events.double().cpu().numpy()
+
+
+# ------------------------------------------------------------- rank table / u_int
+def _dev():
+    import torch
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _put(a, dtype):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=dtype)).to(_dev())
+
+
+def _rank_table_dev(df, src_id, fill=True, with_time=True):
+    """rq_rank_table on the df columns; returns (table, index) device tensors + sink ids."""
+    import torch
+    from . import _lib as L
+    if len(df) == 0:
+        raise ValueError("No objects to concatenate")   # pandas' pivot of an empty df
+    key = df["t"].values if with_time else df["event_id"].values
+    t = np.ascontiguousarray(key, dtype=np.float64)
+    sinks, col = np.unique(df["sink_id"].values, return_inverse=True)
+    n_t = int(np.unique(t).size)
+    S = int(sinks.size)
+    dev = _dev()
+    tab = torch.empty((n_t, S), dtype=torch.float64, device=dev)
+    idx = torch.empty(n_t, dtype=torch.float64, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    tt, ts, tc = _put(t, np.float64), _put(df["src_id"].values, np.int64), _put(col, np.int32)
+    st = torch.cuda.current_stream().cuda_stream
+    L.check("rq_rank_table", L.lib().rq_rank_table(
+        tt.data_ptr(), ts.data_ptr(), tc.data_ptr(), t.size, S, int(src_id), int(bool(fill)), n_t,
+        tab.data_ptr(), idx.data_ptr(), err.data_ptr(), st))
+    if int(err.item()) & 1:
+        raise L.RQError("rq_rank_table (df must be sorted by its pivot index)", L.RQ_EUNSORTED)
+    return tab, idx, sinks
+
+
+def rank_of_src_in_df(df, src_id, fill=True, with_time=True):
+    """Calculates the rank of the src_id at each time instant in the list of events
+    (utils.py:38-56): a DataFrame indexed by the unique t (or event_id), one column
+    per sink_id, computed by rq_rank_table."""
+    import pandas as pd
+    tab, idx, sinks = _rank_table_dev(df, src_id, fill, with_time)
+    index = idx.cpu().numpy()
+    if not with_time:
+        index = index.astype(np.int64)
+    return pd.DataFrame(tab.cpu().numpy(), index=pd.Index(index, name="t" if with_time else "event_id"),
+                        columns=pd.Index(sinks, name="sink_id"))
+
+
+def u_int_opt(df, src_id=None, end_time=None, s=None, q=None, follower_ids=None, sim_opts=None):
+    """Calculate the integral of u(t) for the given src_id assuming that the
+    broadcaster was following the optimal strategy (utils.py:59-81):
+    sum_k (r_k[followers] . sqrt(s/q)) * dt_k on the GPU rank table.  The row dot
+    runs in follower order (the reference's BLAS dgemv may associate differently:
+    equal to ~1e-15 relative, not bit for bit)."""
+    import torch
+    from . import _lib as L
+    if sim_opts is not None:
+        src_id = mb(src_id, sim_opts.src_id)
+        end_time = mb(end_time, sim_opts.end_time)
+        s = mb(s, sim_opts.s)
+        q = mb(q, sim_opts.q)
+        follower_ids = mb(follower_ids, sim_opts.sink_ids)
+    if follower_ids is None:
+        follower_ids = sorted(df.sink_id[df.src_id == src_id].unique())
+    tab, idx, sinks = _rank_table_dev(df, src_id)
+    pos = {int(x): i for i, x in enumerate(sinks)}
+    missing = [f for f in follower_ids if int(f) not in pos]
+    if missing:
+        raise KeyError("{} not in index".format(missing))
+    fcol = np.asarray([pos[int(f)] for f in follower_ids], dtype=np.int32)
+    wts = np.sqrt(np.asarray(s, dtype=np.float64) / q) * np.ones(len(fcol))
+    n_t = tab.shape[0]
+    ws = torch.empty(max(1, n_t), dtype=torch.float64, device=_dev())
+    out = torch.empty(1, dtype=torch.float64, device=_dev())
+    tf, tw = _put(fcol, np.int32), _put(wts, np.float64)
+    st = torch.cuda.current_stream().cuda_stream
+    L.check("rq_u_int", L.lib().rq_u_int(tab.data_ptr(), idx.data_ptr(), n_t, tab.shape[1],
+                                         tf.data_ptr(), tw.data_ptr(), len(fcol), float(end_time),
+                                         out.data_ptr(), ws.data_ptr(), ws.numel() * 8, st))
+    return np.float64(out.item())
+
+
+# -------------------------------------------------------------------- the oracle
+def _oracle_w(df, end_time):
+    """event_times = df.groupby('event_id').t.mean(); w = np.diff([0, 0, times, end])
+    (utils.py:200-207)."""
+    event_times = df.groupby('event_id').t.mean()
+    w = np.diff(np.concatenate([[0.0], [0.0], event_times.values, [end_time]]))
+    return event_times, w
+
+
+def oracle_dp_batch(ws, qs, ss):
+    """rq_oracle_dp over several walls at once: ws[i] = w of wall i (len n_i + 2),
+    qs[i], ss[i] its q and s.  Returns [(cost, events, ranks)] (numpy)."""
+    import torch
+    from . import _lib as L
+    n = np.asarray([len(w) - 2 for w in ws], dtype=np.int64)
+    if np.any(n < 0):
+        raise ValueError("w needs n + 2 >= 2 entries")
+    if len(ws) == 0:
+        return []
+    w_off = np.concatenate([[0], np.cumsum(n + 2)]).astype(np.int64)
+    o_off = np.concatenate([[0], np.cumsum(n + 1)]).astype(np.int64)
+    n_max = int(n.max())
+    nbytes = C.c_size_t()
+    L.check("rq_oracle_workspace_size", L.lib().rq_oracle_workspace_size(len(ws), n_max, C.byref(nbytes)))
+    dev = _dev()
+    wsp = torch.empty(nbytes.value, dtype=torch.uint8, device=dev)
+    tw = _put(np.concatenate([np.asarray(w, dtype=np.float64) for w in ws]), np.float64)
+    twoff, tooff = _put(w_off, np.int64), _put(o_off, np.int64)
+    tq, tsv = _put(qs, np.float64), _put(ss, np.float64)
+    cost = torch.empty(len(ws), dtype=torch.float64, device=dev)
+    ev = torch.empty(int(o_off[-1]), dtype=torch.int32, device=dev)
+    rk = torch.empty(int(o_off[-1]), dtype=torch.int32, device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+    L.check("rq_oracle_dp", L.lib().rq_oracle_dp(
+        tw.data_ptr(), twoff.data_ptr(), tq.data_ptr(), tsv.data_ptr(), len(ws), n_max,
+        cost.data_ptr(), ev.data_ptr(), rk.data_ptr(), tooff.data_ptr(), wsp.data_ptr(),
+        wsp.numel(), st))
+    c, e, r = cost.cpu().numpy(), ev.cpu().numpy(), rk.cpu().numpy()
+    return [(np.float64(c[i]), e[o_off[i]:o_off[i + 1]].astype(np.int64),
+             r[o_off[i]:o_off[i + 1]].astype(np.int64)) for i in range(len(ws))]
+
+
+def _scalar_s(s):
+    if isinstance(s, dict):
+        raise TypeError("unsupported operand type(s) for *: 'float' and 'dict'")
+    a = np.asarray(s, dtype=np.float64).ravel()
+    if a.size != 1:
+        raise ValueError("oracle_ranking is implemented for one follower (s must be a scalar)")
+    return float(a[0])
+
+
+def oracle_ranking(df, sim_opts, omit_src_ids=None, follower_ids=None):
+    """Returns the best places the oracle would have put events (utils.py:181-245).
+    Optionally, it can remove sources, use a custom weight vector and have a
+    custom list of followers.  The DP runs on the GPU (rq_oracle_dp)."""
+    import pandas as pd
+    if omit_src_ids is not None:
+        df = df[~df.src_id.isin(omit_src_ids)]
+
+    if follower_ids is not None:
+        df = sorted(df[df.sink_id.isin(follower_ids)])   # sic (utils.py:190)
+    else:
+        follower_ids = sorted(df.sink_id.unique())
+
+    assert len(follower_ids) == 1, "Oracle has been implemented only for 1 follower."
+
+    q = sim_opts.q
+    s = sim_opts.s
+    event_times, w = _oracle_w(df, sim_opts.end_time)
+    n = event_times.shape[0]
+    if n > 1e6:
+        logging.error('Not running for n > 1e6 events')
+        return []
+    (cost, u_star, oracle_ranks), = oracle_dp_batch([w], [float(q)], [_scalar_s(s)])
+    oracle_df = pd.DataFrame.from_dict({
+        'ranks': oracle_ranks,
+        'events': u_star,
+        'at': np.concatenate([[0.0], event_times.values]),
+        't': np.concatenate([[0.0], event_times.values]),
+        't_delta': w[1:]
+    })
+    return oracle_df, cost
+
+
+def _wall_df(sim_opts):
+    wall_mgr = sim_opts.create_manager_for_wall()
+    wall_mgr.run_dynamic()
+    return wall_mgr.state.get_dataframe()
+
+
+def get_oracle_df(sim_opts, with_cost=False):
+    """utils.py:248-257: oracle on the wall of sim_opts' other sources."""
+    oracle_df, cost = oracle_ranking(df=_wall_df(sim_opts), sim_opts=sim_opts)
+    if with_cost:
+        return oracle_df, cost
+    else:
+        return oracle_df
+
+
+def find_opt_oracle(target_events, sim_opts, max_events=None, tol=1e-2, verbose=False):
+    """Sweep q and get the best run of the oracle (utils.py:260-340): the
+    reference's exponential search + bisection, each step one GPU DP on the
+    (deterministic) wall, which is simulated once."""
+    q_hi, q_init, q_lo = 1.0 * 2, 1.0, 1.0 / 2
+    wall = _wall_df(sim_opts)
+
+    def oracle(q):
+        return oracle_ranking(df=wall, sim_opts=sim_opts.update({'q': q}))
+
+    def terminate_cond(opt_events):
+        return np.abs(opt_events - target_events) / (target_events * 1.0) < tol or \
+            (opt_events == np.ceil(target_events)) or \
+            (opt_events == np.floor(target_events))
+
+    oracle_df, cost = oracle(q_init)
+    num_events = oracle_df.events.sum()
+    if terminate_cond(num_events):
+        return {'q': q_init, 'cost': cost, 'oracle_df': oracle_df}   # sic: key (utils.py:277)
+
+    if num_events > target_events:
+        while True:
+            q_lo = q_init
+            q_init *= 2
+            q_hi = q_init
+            oracle_df, cost = oracle(q_init)
+            num_events = oracle_df.events.sum()
+            if verbose:
+                logTime('q_lo = {}, q_hi = {}, num_events = {} '.format(q_lo, q_hi, num_events))
+            if terminate_cond(num_events):
+                return {'q': q_init, 'cost': cost, 'df': oracle_df}
+            if num_events <= target_events:
+                break
+    elif num_events < target_events:
+        while True:
+            q_hi = q_init
+            q_init /= 2
+            q_lo = q_init
+            oracle_df, cost = oracle(q_init)
+            num_events = oracle_df.events.sum()
+            if verbose:
+                logTime('q_lo = {}, q_hi = {}, num_events = {} '.format(q_lo, q_hi, num_events))
+            if terminate_cond(num_events):
+                return {'q': q_init, 'cost': cost, 'df': oracle_df}
+            if num_events >= target_events or num_events == max_events:
+                break
+
+    if verbose:
+        logTime('q_lo = {}, q_hi = {}'.format(q_lo, q_hi))
+
+    while True:
+        q_try = (q_lo + q_hi) / 2.0
+        oracle_df, cost = oracle(q_try)
+        opt_events = oracle_df.events.sum()
+        if verbose:
+            logTime('q_try = {}, events = {}, cost = {}'.format(q_try, opt_events, cost))
+        if terminate_cond(opt_events):
+            return {'q': q_try, 'cost': cost, 'df': oracle_df}
+        elif opt_events < target_events:
+            q_hi = q_try
+        else:
+            q_lo = q_try
+
+
+def find_opt_oracle_q(target_events, sim_opts, tol=1e-1, verbose=False):
+    res = find_opt_oracle(target_events, sim_opts, tol, verbose)   # sic: tol -> max_events
+    return res['q']
+
+
+def find_opt_oracle_time_top_k(target_events, K, sim_opts, tol=1e-1, verbose=False):
+    logTime('This method is incorrect.')
+    res = find_opt_oracle(target_events, sim_opts, tol, verbose)
+    df = res['df']
+    return np.sum(df.t_delta[df.ranks <= K - 1])
+
+
+# --------------------------------------------------------------------- sweep_q
+def q_int_worker(params):
+    sim_opts, seed, dynamic, max_events = params
+    return calc_q_capacity_iter(sim_opts, sim_opts.q, seeds=[seed], max_events=max_events)[0]
+
+
+def sweep_q(sim_opts, capacity_cap, tol=1e-2, verbose=False, q_init=None, parallel=True,
+            dynamic=True, max_events=None, max_iters=float('inf'), only_tol=False):
+    """Find q whose mean RedQueen capacity over seeds 100..119 meets capacity_cap
+    (utils.py:521-607): the reference's exponential bracket + bisection; every
+    capacity estimate is one GPU batch (calc_q_capacity_iter)."""
+    # We know that on average, the integral of u(t) decreases with increasing 'q'
+
+    def terminate_cond(new_capacity):
+        return abs(new_capacity - capacity_cap) / capacity_cap < tol or \
+            (not only_tol and np.ceil(capacity_cap - 1) <= new_capacity <= np.ceil(capacity_cap + 1))
+
+    def cap_at(q):
+        return calc_q_capacity_iter(sim_opts, q, dynamic=dynamic, parallel=parallel,
+                                    max_events=max_events).mean()
+
+    if q_init is None:
+        r_t = rank_of_src_in_df(_wall_df(sim_opts), -1)
+        q_init = (4 * (r_t.iloc[-1].mean() ** 2) * (sim_opts.end_time) ** 2) / \
+            (np.pi * np.pi * (capacity_cap + 1) ** 4)
+        if verbose:
+            logTime('q_init = {}'.format(q_init))
+
+    # Step 1: Find the upper/lower bound by exponential increase/decrease
+    init_cap = cap_at(q_init)
+    if terminate_cond(init_cap):
+        return q_init
+    if verbose:
+        logTime('Initial capacity = {}, target capacity = {}, q_init = {}'
+                .format(init_cap, capacity_cap, q_init))
+
+    q = q_init
+    if init_cap < capacity_cap:
+        iters = 0
+        while True:
+            iters += 1
+            q_hi = q
+            q /= 2.0
+            q_lo = q
+            capacity = cap_at(q)
+            if verbose:
+                logTime('q = {}, capacity = {}'.format(q, capacity))
+            if terminate_cond(capacity):
+                return q
+            if capacity >= capacity_cap:
+                break
+            if iters > max_iters:
+                if verbose:
+                    logTime('Breaking because of max-iters: {}.'.format(max_iters))
+                return q
+    else:
+        iters = 0
+        while True:
+            iters += 1
+            q_lo = q
+            q *= 2.0
+            q_hi = q
+            capacity = cap_at(q)
+            if verbose:
+                logTime('q = {}, capacity = {}'.format(q, capacity))
+            if terminate_cond(capacity):
+                return q
+            if capacity <= capacity_cap:
+                break
+            if iters > max_iters:
+                if verbose:
+                    logTime('Breaking because of max-iters: {}.'.format(max_iters))
+                return q
+
+    if verbose:
+        logTime('q_hi = {}, q_lo = {}'.format(q_hi, q_lo))
+
+    # Step 2: Keep bisecting on 's' until we arrive at a close enough solution.
+    while True:
+        q = (q_hi + q_lo) / 2.0
+        new_capacity = cap_at(q)
+        if verbose:
+            logTime('new_capacity = {}, q = {}'.format(new_capacity, q))
+        if terminate_cond(new_capacity):
+            break
+        elif new_capacity > capacity_cap:
+            q_lo = q
+        else:
+            q_hi = q
+
+    # Step 3: Return
+    return q

@@ -18,6 +18,14 @@ installed and there is no network) and records, as plain data:
   adversarial.npz  hand-made tie-heavy / duplicate (t, sink) / many-sink dfs
                    with the reference's time_in_top_k / average_rank / int_r_2
   frac.npz         dfs whose pivot has fractional (k/3) cells on 8-130 columns
+  oracle.npz       utils.oracle_ranking on single-follower wall dfs (Poisson2 / Hawkes
+                   walls, duplicated edges, omitted sources, n = 0 / 1), the
+                   find_opt_oracle bisection and opt_runs.worker_oracle's outputs
+  sweepq.npz       utils.sweep_q (sequential) on std_poisson(1, 100): q_init, the
+                   returned q and calc_q_capacity_iter per (q, seed);
+                   rank_of_src_in_df tables and u_int_opt values
+  sig_runs.npz     OptPWSignificance runs (notebook "Testing out significance",
+                   opt_broadcast.ipynb:5469, :5569): events + metrics
   graphs.npz       opt_runs.make_edge_list networks (C3 parameters) and a
                    prepare_multiple_followers_sim_opts network
   dist_c2.npz      (--dist N) N-replica C2 ensemble: RedQueen vs Poisson stats
@@ -293,6 +301,153 @@ def gen_frac():
     np.savez_compressed(os.path.join(HERE, "frac.npz"), cases=np.asarray(cases), **rec)
 
 
+def _df_cols(rec, key, df):
+    for col in ["event_id", "time_delta", "src_id", "t", "sink_id"]:
+        rec[key + "_" + col] = df[col].values
+
+
+def gen_oracle():
+    """utils.oracle_ranking (utils.py:181-245) on reference wall dfs; find_opt_oracle
+    (:260-340) and opt_runs.worker_oracle (opt_runs.py:129-155)."""
+    import redqueen.opt_runs as R
+    rec, cases = {}, []
+
+    def case(key, df, so, qs, omit=None):
+        _df_cols(rec, key, df)
+        rec[key + "_end"] = np.asarray([so.end_time])
+        rec[key + "_s"] = np.asarray([float(np.asarray(so.s).ravel()[0])])
+        rec[key + "_omit"] = np.asarray(omit if omit else [], dtype=np.int64)
+        rec[key + "_q"] = np.asarray(qs, dtype=np.float64)
+        for i, q in enumerate(qs):
+            odf, cost = U.oracle_ranking(df=df, sim_opts=so.update({"q": q}), omit_src_ids=omit)
+            rec["%s_%d_cost" % (key, i)] = np.asarray([cost])
+            rec["%s_%d_ranks" % (key, i)] = odf.ranks.values.astype(np.int64)
+            rec["%s_%d_events" % (key, i)] = odf.events.values.astype(np.int64)
+            rec["%s_%d_t" % (key, i)] = odf.t.values
+            rec["%s_%d_tdelta" % (key, i)] = odf.t_delta.values
+        cases.append(key)
+
+    def wall(so):
+        m = so.create_manager_for_wall()
+        m.run_dynamic()
+        return m.state.get_dataframe()
+
+    so = SimOpts.std_poisson(world_seed=42, world_rate=1000.0)
+    case("p1000", wall(so), so, [1.0, 0.01, 100.0, 1e-6, 1e6])
+    so = SimOpts.std_hawkes(world_seed=7, world_lambda_0=100.0, world_alpha=1.0, world_beta=10.0)
+    case("hawkes", wall(so), so, [1.0, 0.1, 3.0])
+    so10 = SimOpts.std_poisson(world_seed=1, world_rate=100.0).update({"end_time": 10.0})
+    case("p100", wall(so10), so10, [38.5, 1.0])
+    # duplicated edge: every wall event reaches the follower twice (groupby mean of t)
+    sod = SimOpts.std_poisson(world_seed=5, world_rate=200.0).update(
+        {"edge_list": [(1, 1001), (2, 1001), (2, 1001)], "s": 2.5})
+    case("dup", wall(sod), sod, [0.5, 4.0])
+    # a df with the broadcaster's own posts, omitted by omit_src_ids
+    som = SimOpts.std_poisson(world_seed=9, world_rate=300.0)
+    m = som.create_manager_with_opt(3)
+    m.run_dynamic()
+    case("omit", m.state.get_dataframe(), som, [1.0, 0.05], omit=[1])
+    # degenerate walls: one event, and one event exactly at end_time's neighbourhood
+    so1 = SimOpts.std_poisson(world_seed=0, world_rate=1.0).update({"end_time": 0.9})
+    d1 = wall(so1)
+    case("n%d" % d1.event_id.nunique(), d1, so1, [1.0, 0.001])
+    cases_arr = cases
+    # find_opt_oracle on the p100 world, and worker_oracle
+    res = U.find_opt_oracle(50, so10)
+    rec["fo_q"] = np.asarray([res["q"]])
+    rec["fo_cost"] = np.asarray([res["cost"]])
+    rec["fo_events"] = np.asarray([res["df"].events.sum()])
+    op = R.worker_oracle((1, 50, None, so10, None))
+    for k in ["r0_num_events", "num_events", "top_1", "avg_rank", "r_2", "world_events"]:
+        rec["wo_" + k] = np.asarray([float(op[k])])
+    # the df worker_oracle scores (RealData oracle posts + the same world)
+    odf = res["df"]
+    mm = so10.create_manager_with_times(odf.t[odf.events == 1] + R.perf_opts.oracle_eps)
+    mm.run_dynamic()
+    _df_cols(rec, "wo_df", mm.state.get_dataframe())
+    np.savez_compressed(os.path.join(HERE, "oracle.npz"), cases=np.asarray(cases_arr), **rec)
+
+
+def gen_sweepq():
+    """utils.sweep_q (utils.py:521-607) with parallel=False, its q_init from
+    rank_of_src_in_df(wall, -1) (:38-56), calc_q_capacity_iter (:447-470); u_int_opt
+    (:59-81) on README / K1 dfs."""
+    rec = {}
+    so = SimOpts.std_poisson(world_seed=1, world_rate=100.0)
+    qs = []
+    orig = U.calc_q_capacity_iter
+
+    def spy(sim_opts, q, **kw):
+        c = orig(sim_opts, q, **kw)
+        qs.append((q, c))
+        return c
+    U.calc_q_capacity_iter = spy
+    try:
+        rec["sq_q"] = np.asarray([U.sweep_q(so, capacity_cap=50.0, parallel=False)])
+        rec["sq_q2"] = np.asarray([U.sweep_q(so, capacity_cap=20.0, parallel=False, tol=1e-3,
+                                             only_tol=True, max_iters=6)])
+    finally:
+        U.calc_q_capacity_iter = orig
+    rec["sq_trace_q"] = np.asarray([q for q, _ in qs])
+    rec["sq_trace_cap"] = np.asarray([c for _, c in qs])
+    w = so.create_manager_for_wall()
+    w.run_dynamic()
+    r_t = U.rank_of_src_in_df(w.state.get_dataframe(), -1)
+    rec["sq_rlast_mean"] = np.asarray([r_t.iloc[-1].mean()])
+    # rank tables: README run (3 sinks) and K3 df, with and without ffill
+    rd = SimOpts(**README)
+    m = rd.create_manager_with_opt(seed=101)
+    m.run_dynamic()
+    df = m.state.get_dataframe()
+    _df_cols(rec, "rt_readme", df)
+    for src in (1, 2, -1):
+        tab = U.rank_of_src_in_df(df, src)
+        rec["rt_readme_%d" % (src + 1)] = tab.values
+        rec["rt_readme_%d_nofill" % (src + 1)] = U.rank_of_src_in_df(df, src, fill=False).values
+    rec["rt_readme_index"] = tab.index.values
+    rec["rt_readme_cols"] = tab.columns.values.astype(np.int64)
+    rec["rt_readme_uint"] = np.asarray([U.u_int_opt(df, sim_opts=rd.update({"s": np.asarray([1.0, 1.0])}),
+                                                    follower_ids=[1, 3])])
+    so3 = SimOpts(s=np.asarray([0.5, 1.5]), **KAT_BASE)
+    m = so3.create_manager_with_opt(1)
+    m.run_dynamic()
+    df3 = m.state.get_dataframe()
+    _df_cols(rec, "rt_k5", df3)
+    rec["rt_k5_uint"] = np.asarray([U.u_int_opt(df3, sim_opts=so3)])
+    rec["rt_k5_tab"] = U.rank_of_src_in_df(df3, 1).values
+    np.savez_compressed(os.path.join(HERE, "sweepq.npz"), **rec)
+
+
+def gen_sig():
+    """OptPWSignificance (opt_model.py:547-623) via create_manager_with_significance
+    (:850-884): the notebook cells opt_broadcast.ipynb:5469 and :5569 plus variants."""
+    rec = {}
+    so3 = SimOpts(s=np.asarray([1.0, 1.0]), **KAT_BASE)
+    so5 = SimOpts(s=np.asarray([0.5, 1.5]), **KAT_BASE)
+    runs = {"s1": (so3, 1, 10.0, 24, None), "s41": (so5, 41, 10.0, 24, None),
+            "s7": (so5, 7, 25.0, 5, None)}
+    num_segs = 24
+    sig = np.square(np.sin(np.arange(0, num_segs, step=1.0) * 4 * np.pi / num_segs))
+    sig = (sig / sig.sum()).reshape((1, -1))
+    so_sig = SimOpts(src_id=1, s=1.0, q=1.0, end_time=20.0,
+                     other_sources=[("Poisson2", {"src_id": 1000, "seed": 42, "rate": 50.0})],
+                     sink_ids=[5001], edge_list=[(1, 5001), (1000, 5001)])
+    runs["sig"] = (so_sig, 10, so_sig.end_time, None, sig)
+    for key, (so_, seed, period, nseg, signif) in runs.items():
+        m = so_.create_manager_with_significance(seed, time_period=period, significance=signif,
+                                                 num_segments=nseg)
+        sig_used = np.asarray(m.sources[0].s_pw, dtype=np.float64)
+        m.run_dynamic()
+        df = m.state.get_dataframe()
+        rec[key + "_t"], rec[key + "_dt"], rec[key + "_src"] = events_of(df)
+        met, own, world = metrics(df, so_)
+        rec[key + "_met"] = met
+        rec[key + "_cnt"] = np.asarray([own, world, len(df), df.shape[1]])
+        rec[key + "_sig"] = sig_used
+        rec[key + "_par"] = np.asarray([seed, period, float(so_.q)])
+    np.savez_compressed(os.path.join(HERE, "sig_runs.npz"), **rec)
+
+
 # ---------------------------------------------------------------- ensembles
 def _c2_worker(r):
     so = SimOpts(**README)
@@ -384,7 +539,8 @@ if __name__ == "__main__":
     ap.add_argument("--worlds", action="store_true", help="only dist_world.npz")
     a = ap.parse_args()
     steps = {"npsum": gen_npsum, "draws": gen_draws, "readme": gen_readme, "kats": gen_kats,
-             "adv": gen_adversarial, "graphs": gen_graphs, "frac": gen_frac}
+             "adv": gen_adversarial, "graphs": gen_graphs, "frac": gen_frac,
+             "oracle": gen_oracle, "sweepq": gen_sweepq, "sig": gen_sig}
     if a.worlds:
         gen_worlds()
         print("done worlds", flush=True)
