@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define RQ_ABI_VERSION 1
+#define RQ_ABI_VERSION 2
 #define RQ_MAX_K 4 /* at most 4 K values (perf_opts.Ks, opt_runs.py:31-38) per run */
 
 typedef enum {
@@ -74,7 +74,8 @@ typedef enum {
     RQ_SRC_HAWKES = 3,    /* Hawkes         opt_model.py:458-490                    */
     RQ_SRC_PWCONST = 4,   /* PiecewiseConst opt_model.py:626-689                    */
     RQ_SRC_REALDATA = 5,  /* RealData       opt_model.py:711-750                    */
-    RQ_SRC_OPT = 6        /* Opt = RedQueen opt_model.py:493-544 (controlled only)  */
+    RQ_SRC_OPT = 6,       /* Opt = RedQueen opt_model.py:493-544 (controlled only)  */
+    RQ_SRC_OPTPW = 7      /* OptPWSignificance opt_model.py:547-623 (controlled only) */
 } rq_src_kind;
 
 typedef struct rq_source_desc {
@@ -120,7 +121,7 @@ typedef struct rq_graph* rq_graph_t;
 #define RQ_RUN_EVENT_LOG 1       /* also write the (t, source) event log (for get_dataframe)    */
 
 typedef struct rq_batch_desc {
-    int32_t ctrl_kind;           /* RQ_SRC_OPT / POISSON2 / PWCONST / REALDATA / NONE           */
+    int32_t ctrl_kind;           /* RQ_SRC_OPT / OPTPW / POISSON2 / PWCONST / REALDATA / NONE   */
     int32_t n_grid;              /* grid points                                                  */
     const double* q;             /* host [n_grid] (OPT)                                          */
     const double* s;             /* host [n_grid * n_followers], sorted-follower order (OPT)     */
@@ -152,6 +153,12 @@ typedef struct rq_batch_desc {
                                     pre-generated into HBM by rq_gen_streams, serial wave-min
                                     merge) -- kept for A/B parity checks of the fused sweep  */
                                  /* sweep; both are bit-identical, auto picks the faster one    */
+    /* RQ_SRC_OPTPW (create_manager_with_significance, opt_model.py:850-884): the follower
+       significance s_pw[g][f][k] over n_seg equal segments of time_period, rows in the
+       order of rq_graph_followers (sorted follower ids), q from q[g] */
+    int32_t n_seg;
+    double period;
+    const double* s_pw;          /* host [n_grid][n_followers][n_seg]                            */
 } rq_batch_desc;
 
 typedef struct rq_outputs {

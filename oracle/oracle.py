@@ -19,7 +19,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = os.path.join(_HERE, "librq_oracle.so")
 
-POISSON, POISSON2, HAWKES, PWCONST, REALDATA, OPT = 1, 2, 3, 4, 5, 6
+POISSON, POISSON2, HAWKES, PWCONST, REALDATA, OPT, OPTPW = 1, 2, 3, 4, 5, 6, 7
 KIND = {"Poisson": POISSON, "Poisson2": POISSON2, "Hawkes": HAWKES,
         "PiecewiseConst": PWCONST, "RealData": REALDATA, "Opt": OPT}
 
@@ -190,6 +190,13 @@ class Scenario:
             srcs.append(self._src(PWCONST, src_id, ctrl[1], a=ctrl[2], b=ctrl[3]))
         elif kind == "times":
             srcs.append(self._src(REALDATA, src_id, 0, a=ctrl[1]))
+        elif kind == "sig":
+            # ("sig", seed, s_pw [sorted followers][S], time_period): OptPWSignificance
+            spw = np.atleast_2d(np.asarray(ctrl[2], dtype=np.float64))
+            src = self._src(OPTPW, src_id, ctrl[1], q=so["q"], a=spw.ravel())
+            src.n_arr = spw.shape[1]
+            src.p1 = float(ctrl[3])
+            srcs.append(src)
         elif kind == "wall":
             srcs.append(self._src(0, src_id, 0))
         else:
@@ -229,7 +236,7 @@ class Scenario:
             s.p0 = float(rate)
         elif kind == HAWKES:
             s.p0, s.p1, s.p2 = float(l0), float(alpha), float(beta)
-        elif kind == OPT:
+        elif kind in (OPT, OPTPW):
             s.p0 = float(q)
         if a is not None:
             a = np.ascontiguousarray(a, dtype=np.float64)

@@ -435,6 +435,8 @@ typedef struct {
     dvec prev;                           /* Hawkes prev_excitations          */
     /* Opt */
     int opt_init; int64_t n_fol; int64_t* fol; int64_t* trk; double* w; double old_rate;
+    /* OptPWSignificance: old_ranks, sqrt(s_pw / q) [n_fol][S], pw_intensity [S] */
+    int64_t* old; double* sq; double* pw; int err;
 } refsrc;
 
 static void vexp_libm(const double* x, int64_t n, double* out)
@@ -517,6 +519,57 @@ static int ref_next_interval(refsrc* b, const refevent* ev, rqo_vexp_fn vexp, in
         }
         return 0;
     }
+    case RQO_OPTPW: {
+        /* OptPWSignificance.get_next_interval, opt_model.py:580-623 */
+        const int64_t S = s->n_arr;
+        const double T = s->p1;
+        if (!b->opt_init) {
+            b->opt_init = 1;
+            for (int64_t i = 0; i < b->n_fol; i++) b->trk[i] = 0;
+            for (int64_t i = 0; i < b->n_fol * S; i++) b->sq[i] = sqrt(s->a[i] / s->p0);
+        }
+        if (ev) {   /* state.apply_event (tracked ranks, :70-76) */
+            if (ev->src_id == s->src_id) {
+                for (int64_t i = 0; i < b->n_fol; i++) b->trk[i] = 0;
+            } else {
+                for (int k = 0; k < ev->n_sinks; k++)
+                    for (int64_t i = 0; i < b->n_fol; i++)
+                        if (b->fol[i] == ev->sinks[k]) { b->trk[i] += 1; break; }
+            }
+        }
+        if (ev == NULL || ev->src_id == s->src_id) {   /* :597-605 */
+            for (int64_t i = 0; i < b->n_fol; i++) b->old[i] = 0;
+            *out = ev == NULL ? 0.0 : INFINITY;
+            return 1;
+        }
+        /* pw_intensity = (sqrt(s_pw / q) * rank_diff[:, None]).sum(0)   :613-614 */
+        for (int64_t k = 0; k < S; k++) {
+            double acc = 0.0;
+            for (int64_t i = 0; i < b->n_fol; i++) {
+                const double x = b->sq[i * S + k] * (double)(b->trk[i] - b->old[i]);
+                acc = i == 0 ? x : acc + x;
+            }
+            b->pw[k] = acc;
+        }
+        /* take_one_sample (:560-573) */
+        double smax = b->pw[0];
+        for (int64_t k = 1; k < S; k++) if (b->pw[k] > smax) smax = b->pw[k];
+        if (!(smax > 0.0)) { b->err = 1; return 0; }   /* reference: int(nan) ValueError */
+        const double phase = fmod(ev->cur_time, T);
+        double ns = 0.0;
+        for (;;) {
+            ns += rqo_mt_exponential(&b->rs, 1.0 / smax);
+            const int64_t idx = (int64_t)(((double)S * fmod(ns + phase, T)) / T);
+            if (idx < 0 || idx >= S) { b->err = 1; return 0; }   /* IndexError */
+            if (rqo_mt_double(&b->rs) < b->pw[idx] / smax) break;
+        }
+        for (int64_t i = 0; i < b->n_fol; i++) b->old[i] = b->trk[i];
+        if (b->last_self + b->t_delta > ev->cur_time + ns) {
+            *out = ev->cur_time + ns - b->last_self;
+            return 1;
+        }
+        return 0;
+    }
     default:
         return 0;
     }
@@ -593,13 +646,14 @@ int rqo_ref_run(const rqo_scenario* sc, rqo_vexp_fn vexp, int32_t dot_fma, rqo_e
     for (int i = 0; i < ns; i++) {
         refsrc* b = &B[i];
         b->s = &sc->sources[i];
-        b->dynamic = b->s->kind == RQO_POISSON || b->s->kind == RQO_HAWKES || b->s->kind == RQO_OPT;
+        b->dynamic = b->s->kind == RQO_POISSON || b->s->kind == RQO_HAWKES ||
+                     b->s->kind == RQO_OPT || b->s->kind == RQO_OPTPW;
         rqo_mt_seed(&b->rs, b->s->seed);
         b->start_time = sc->start_time;
         b->end_time = sc->end_time;
         b->sinks = all_sinks + (int64_t)i * (sc->n_edges + 1);
         b->n_sinks = sinks_of(sc, b->s->src_id, b->sinks);
-        if (b->s->kind == RQO_OPT) {
+        if (b->s->kind == RQO_OPT || b->s->kind == RQO_OPTPW) {
             /* followers: sorted(follower_sink_ids), opt_model.py:341 */
             b->n_fol = b->n_sinks;
             b->fol = malloc(sizeof(int64_t) * (b->n_fol + 1));
@@ -608,6 +662,13 @@ int rqo_ref_run(const rqo_scenario* sc, rqo_vexp_fn vexp, int32_t dot_fma, rqo_e
             if (!b->fol || !b->trk || !b->w) goto done;
             memcpy(b->fol, b->sinks, sizeof(int64_t) * b->n_fol);
             qsort(b->fol, (size_t)b->n_fol, sizeof(int64_t), cmp_i64);
+            if (b->s->kind == RQO_OPTPW) {
+                const int64_t S = b->s->n_arr;
+                b->old = malloc(sizeof(int64_t) * (b->n_fol + 1));
+                b->sq = malloc(sizeof(double) * (b->n_fol * S + 1));
+                b->pw = malloc(sizeof(double) * (S + 1));
+                if (!b->old || !b->sq || !b->pw || S < 1) goto done;
+            }
         }
         if (!b->dynamic) {
             if (ref_initialize_static(b)) goto done;
@@ -641,6 +702,7 @@ int rqo_ref_run(const rqo_scenario* sc, rqo_vexp_fn vexp, int32_t dot_fma, rqo_e
             for (int i = 0; i < ns; i++) {
                 if (!B[i].dynamic) continue;
                 double r = ref_next_event_time(&B[i], lastp, vexp, dot_fma, &tmp, &tmp2);
+                if (B[i].err) { rc = -7; goto done; }
                 int64_t id = B[i].s->src_id;
                 if (!have || r < td || (r == td && id < nsrc)) { td = r; nsrc = id; have = 1; }
             }
@@ -677,6 +739,7 @@ done:
         for (int i = 0; i < ns; i++) {
             free(B[i].times.v); free(B[i].prev.v);
             free(B[i].fol); free(B[i].trk); free(B[i].w);
+            free(B[i].old); free(B[i].sq); free(B[i].pw);
         }
     }
     free(B); free(all_sinks); free(tmp.v); free(tmp2.v); free(st);
@@ -756,9 +819,33 @@ static int engine_stream(const rqo_source* s, uint32_t salt, double start, doubl
     }
 }
 
+/* engine OptPWSignificance draw for wall event number e (rq_sweep_core.h optpw_sample):
+   thinning at smax from the phase t mod T, Philox call (e, iteration) per candidate */
+static double optpw_sample(double tt, const double* row, double smax, int64_t S, double T,
+                           uint64_t e, uint32_t seed)
+{
+    if (!(smax > 0.0)) return INFINITY;
+    const double inv = 1.0 / smax;
+    const double ph = fmod(tt, T);
+    double ns = 0.0;
+    const uint32_t key[2] = {seed, rqo_kind_salt(RQO_OPTPW) | 0x100u};
+    for (uint32_t it = 1; it < (1u << 20); ++it) {
+        const uint32_t ctr[4] = {(uint32_t)e, (uint32_t)(e >> 32), it, 0u};
+        uint32_t w4[4];
+        rqo_philox4x32_10(ctr, key, w4);
+        ns = ns + rq_std_exponential(rq_uniform53(w4[0], w4[1])) * inv;
+        int64_t idx = (int64_t)(((double)S * fmod(ns + ph, T)) / T);
+        idx = idx < S ? idx : S - 1;
+        if (rq_uniform53(w4[2], w4[3]) < row[idx] / smax) return tt + ns;
+    }
+    return INFINITY;
+}
+
 int rqo_engine_run(const rqo_scenario* sc, rqo_events* ev)
 {
     int rc = -4;
+    double* pwc = NULL;
+    double* pwmax = NULL;
     int ns = sc->n_sources;
     dvec* st = calloc((size_t)ns, sizeof(dvec));
     int64_t* head = calloc((size_t)ns, sizeof(int64_t));
@@ -768,9 +855,34 @@ int rqo_engine_run(const rqo_scenario* sc, rqo_events* ev)
     if (!st || !head || !invc || !fol || !w) goto done;
 
     const rqo_source* ctrl = &sc->sources[0];
-    int opt = ctrl->kind == RQO_OPT;
+    const int optpw = ctrl->kind == RQO_OPTPW;
+    int opt = ctrl->kind == RQO_OPT || optpw;   /* a controller that reacts to the wall */
     int64_t nf = 0;
-    if (opt) {
+    const int64_t S = optpw ? ctrl->n_arr : 0;
+    uint64_t nwall = 0;
+    if (optpw) {
+        /* engine semantics of OptPWSignificance: pw_j[k] = sum over edges (j, i), i a
+           follower, of sqrt(s_pw[i][k] / q), edge-list order; bound max_k pw_j[k] */
+        nf = sinks_of(sc, ctrl->src_id, fol);
+        qsort(fol, (size_t)nf, sizeof(int64_t), cmp_i64);
+        pwc = calloc((size_t)(ns * S + 1), sizeof(double));
+        pwmax = calloc((size_t)ns + 1, sizeof(double));
+        if (!pwc || !pwmax || S < 1) goto done;
+        for (int j = 1; j < ns; j++) {
+            double* row = pwc + (int64_t)j * S;
+            for (int64_t e = 0; e < sc->n_edges; e++) {
+                if (sc->edge_src[e] != sc->sources[j].src_id) continue;
+                for (int64_t i = 0; i < nf; i++)
+                    if (fol[i] == sc->edge_sink[e]) {
+                        for (int64_t k = 0; k < S; k++) row[k] = row[k] + sqrt(ctrl->a[i * S + k] / ctrl->p0);
+                        break;
+                    }
+            }
+            double m = 0.0;
+            for (int64_t k = 0; k < S; k++) m = row[k] > m ? row[k] : m;
+            pwmax[j] = m;
+        }
+    } else if (opt) {
         nf = sinks_of(sc, ctrl->src_id, fol);
         qsort(fol, (size_t)nf, sizeof(int64_t), cmp_i64);
         for (int64_t i = 0; i < nf; i++) w[i] = sqrt(ctrl->a[i] / ctrl->p0);
@@ -819,7 +931,11 @@ int rqo_engine_run(const rqo_scenario* sc, rqo_events* ev)
                 opt_next = INFINITY;
             } else {
                 head[bj]++;
-                if (opt && bj != 0) {
+                if (optpw && bj != 0) {
+                    double cand = optpw_sample(bt, pwc + (int64_t)bj * S, pwmax[bj], S, ctrl->p1,
+                                               nwall++, ctrl->seed);
+                    if (cand < opt_next) opt_next = cand;
+                } else if (opt && bj != 0) {
                     double x = rq_std_exponential(pnext(&po));
                     double e = invc[bj] > 0.0 ? x * invc[bj] : INFINITY;
                     double cand = bt + e;
@@ -831,7 +947,7 @@ int rqo_engine_run(const rqo_scenario* sc, rqo_events* ev)
     rc = 0;
 done:
     if (st) for (int j = 0; j < ns; j++) free(st[j].v);
-    free(st); free(head); free(invc); free(fol); free(w);
+    free(st); free(head); free(invc); free(fol); free(w); free(pwc); free(pwmax);
     return rc;
 }
 

@@ -43,16 +43,19 @@ enum {
     RQO_HAWKES = 3,    /* dynamic Hawkes       opt_model.py:458 */
     RQO_PWCONST = 4,   /* static piecewise     opt_model.py:626 */
     RQO_REALDATA = 5,  /* static fixed times   opt_model.py:711 */
-    RQO_OPT = 6        /* RedQueen controller  opt_model.py:493 */
+    RQO_OPT = 6,       /* RedQueen controller  opt_model.py:493 */
+    RQO_OPTPW = 7      /* OptPWSignificance    opt_model.py:547 */
 };
 
 typedef struct {
     int32_t kind;
-    int32_t n_arr;      /* PWCONST: #segments; REALDATA: #times; OPT: #followers */
+    int32_t n_arr;      /* PWCONST: #segments; REALDATA: #times; OPT: #followers;
+                           OPTPW: #significance segments S */
     int64_t src_id;
     uint32_t seed;
-    double p0, p1, p2;  /* POISSON*: rate; HAWKES: l_0, alpha, beta; OPT: q */
-    const double* a;    /* PWCONST change_times; REALDATA times; OPT s (sorted followers) */
+    double p0, p1, p2;  /* POISSON*: rate; HAWKES: l_0, alpha, beta; OPT: q; OPTPW: q, period */
+    const double* a;    /* PWCONST change_times; REALDATA times; OPT s (sorted followers);
+                           OPTPW s_pw [sorted followers][S] */
     const double* b;    /* PWCONST rates */
 } rqo_source;
 

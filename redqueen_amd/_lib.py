@@ -14,9 +14,10 @@ SO_PATH = os.environ.get("RQ_SO_PATH") or os.path.join(_HERE, "librq.so")   # en
 
 RQ_OK, RQ_EINVAL, RQ_EOVERFLOW, RQ_EHIP, RQ_ENOMEM, RQ_EUNSORTED, RQ_EUNSUPPORTED = (
     0, -1, -2, -3, -4, -5, -6)
-SRC_NONE, SRC_POISSON, SRC_POISSON2, SRC_HAWKES, SRC_PWCONST, SRC_REALDATA, SRC_OPT = range(7)
+SRC_NONE, SRC_POISSON, SRC_POISSON2, SRC_HAWKES, SRC_PWCONST, SRC_REALDATA, SRC_OPT, SRC_OPTPW = range(8)
 ST_ROWS_OVERFLOW, ST_STREAM_OVERFLOW, ST_TIE, ST_EMPTY = 1, 2, 4, 8
 RUN_EVENT_LOG = 1
+ABI_VERSION = 2
 MAX_K = 4
 
 _P = C.c_void_p
@@ -47,7 +48,8 @@ class BatchDesc(C.Structure):
                 ("seed_mod", C.c_int64), ("ctrl_rate", _P), ("ctrl_rate_max", C.c_double),
                 ("Ks", _pi32), ("nK", C.c_int32), ("max_events", C.c_int64),
                 ("flags", C.c_int32), ("cap_scale", C.c_double), ("chunk", C.c_int64),
-                ("replica0", C.c_int64), ("n_local", C.c_int64), ("sweep_mode", C.c_int32)]
+                ("replica0", C.c_int64), ("n_local", C.c_int64), ("sweep_mode", C.c_int32),
+                ("n_seg", C.c_int32), ("period", C.c_double), ("s_pw", _pd)]
 
 
 class Outputs(C.Structure):
@@ -102,7 +104,7 @@ def lib():
                "rq_replay_workspace_size", "rq_metrics_replay", "rq_oracle_workspace_size",
                "rq_oracle_dp", "rq_rank_table", "rq_u_int"):
         getattr(L, fn).restype = C.c_int
-    if L.rq_abi_version() != 1:
+    if L.rq_abi_version() != ABI_VERSION:
         raise ImportError("librq.so ABI version mismatch")
     _lib = L
     return L

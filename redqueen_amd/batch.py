@@ -104,3 +104,21 @@ def run_opt_vs_poisson(sim_opts, seeds=range(10), randomize=True, Ks=(1,), max_e
     b = _frame(rp, seeds, np.full(len(seeds), float(sim_opts.q)), "Poisson", Ks)
     b["capacity"] = a["capacity"].values
     return pd.concat([a, b], ignore_index=True)
+
+
+def run_significance(sim_opts, significance, time_period, seeds=range(10), randomize=True,
+                     Ks=(1,), max_events=None, qs=None):
+    """OptPWSignificance (create_manager_with_significance, opt_model.py:850-884) for
+    every seed (x every q in qs): significance [sinks x segments] (or one row of
+    segments for all followers); seed u runs world randomize_other_sources(u)."""
+    from .opt_model import OptPWSignificance
+    g = compiled_graph(sim_opts)
+    qs = [sim_opts.q] if qs is None else list(qs)
+    seeds = np.asarray(list(seeds), dtype=np.int64)
+    spw = OptPWSignificance(sim_opts.src_id, 0, significance, time_period)._s_pw_for(g.n_followers)
+    qv = np.asarray(qs, dtype=np.float64)
+    R = len(seeds)
+    seed_t = torch.as_tensor(np.tile(seeds, len(qv)))
+    res = g.run("sig", q=qv, s_pw=spw, period=float(time_period), n_rep=R, ctrl_seed=seed_t,
+                world_seed=seed_t, randomize=randomize, Ks=Ks, max_events=max_events)
+    return _frame(res, np.tile(seeds, len(qv)), np.repeat(qv, R), "OptPW", Ks)

@@ -132,6 +132,7 @@ struct Plan {
     size_t g_col = 0, g_ptr = 0, g_odf = 0, g_cbf = 0, g_wave = 0, g_wave_stride = 0, g_rank_off = 0,
            g_win_off = 0, g_x_off = 0, g_total = 0, g_stage_off = 0;
     size_t tables_bytes = 0;
+    size_t off_pwc = 0, off_pwmax = 0;
     size_t off_invc = 0, off_streams = 0, off_slen = 0, off_rt = 0, off_rs = 0, off_rv = 0,
            off_rc = 0, off_sall = 0, off_stoff = 0, off_cap = 0,
            total = 0;
@@ -191,10 +192,13 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     if (b->nK < 1 || b->nK > RQ_MAX_K || !b->Ks) return RQ_EINVAL;
     if (b->n_grid < 1 || b->n_rep < 1) return RQ_EINVAL;
     const int ck = b->ctrl_kind;
-    if (ck != RQ_SRC_OPT && ck != RQ_SRC_POISSON2 && ck != RQ_SRC_PWCONST &&
+    if (ck != RQ_SRC_OPT && ck != RQ_SRC_OPTPW && ck != RQ_SRC_POISSON2 && ck != RQ_SRC_PWCONST &&
         ck != RQ_SRC_REALDATA && ck != RQ_SRC_NONE)
         return RQ_EINVAL;
     if (ck == RQ_SRC_OPT && (!b->q || (g->n_fol > 0 && !b->s))) return RQ_EINVAL;
+    if (ck == RQ_SRC_OPTPW &&
+        (!b->q || b->n_seg < 1 || b->n_seg > 4096 || !(b->period > 0.0) || (g->n_fol > 0 && !b->s_pw)))
+        return RQ_EINVAL;
     if (ck == RQ_SRC_POISSON2 && !b->ctrl_rate) return RQ_EINVAL;
     if ((ck == RQ_SRC_PWCONST) && g->ctrl_arr_n < 1) return RQ_EINVAL;
     const double scale = b->cap_scale >= 1.0 ? b->cap_scale : 1.0;
@@ -210,7 +214,8 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     int64_t ctrl_cap = 0;
     for (int j = 0; j < g->n_str; ++j) {
         int kind = g->kind[j];
-        if (j == g->ctrl_idx) kind = (ck == RQ_SRC_OPT || ck == RQ_SRC_NONE) ? RQ_SRC_NONE : ck;
+        if (j == g->ctrl_idx)
+            kind = (ck == RQ_SRC_OPT || ck == RQ_SRC_OPTPW || ck == RQ_SRC_NONE) ? RQ_SRC_NONE : ck;
         double var;
         const double m = stream_mean_var(g, j, kind, b, &var);
         m_total += m;
@@ -227,7 +232,7 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
         if (j == g->ctrl_idx) ctrl_cap = c;
         else wall_caps += (double)c;
     }
-    double rows = wall_caps + (ck == RQ_SRC_OPT ? wall_caps + 1.0 : (double)ctrl_cap) + 8.0;
+    double rows = wall_caps + ((ck == RQ_SRC_OPT || ck == RQ_SRC_OPTPW) ? wall_caps + 1.0 : (double)ctrl_cap) + 8.0;
     if (b->max_events >= 0) rows = std::min(rows, (double)b->max_events + 1.0);
     p->cap_rows = std::max<int64_t>(64, (int64_t)rows);
     p->spl = g->n_str <= 64 ? 1 : g->n_str <= 128 ? 2 : g->n_str <= 256 ? 4 : 8;
@@ -347,6 +352,10 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     p->off_invc = o;    o = o + sizeof(double) * (size_t)b->n_grid * g->n_str;
     p->off_stoff = o;   o = o + sizeof(int64_t) * g->n_str;
     p->off_cap = o;     o = o + sizeof(int) * g->n_str;
+    const size_t nseg = b->ctrl_kind == RQ_SRC_OPTPW ? (size_t)b->n_seg : 0;
+    o = align_up(o, 8);
+    p->off_pwc = o;     o = o + sizeof(double) * (size_t)b->n_grid * g->n_str * nseg;
+    p->off_pwmax = o;   o = o + sizeof(double) * (nseg ? (size_t)b->n_grid * g->n_str : 0);
     p->tables_bytes = o;
     o = align_up(o, A);
     const int64_t strm = p->fw ? 0 : C;   // the fused sweep keeps its arrivals in LDS
@@ -642,7 +651,31 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             }
         }
     }
-    // parameter tables [inv_c | st_off | cap]: staged in one of the graph's pinned host
+    // OptPWSignificance: per (grid point, stream) the intensity increment of one event
+    // of stream j per significance segment, pw[k] = sum over edges (j, i), i a follower,
+    // of sqrt(s_pw[i, k] / q) (opt_model.py:613-614 with rank_diff_i = edge multiplicity),
+    // edge-list order; and its max over k (the thinning bound, :563)
+    std::vector<double> pwc, pwmax;
+    if (b->ctrl_kind == RQ_SRC_OPTPW) {
+        const int S = b->n_seg;
+        pwc.assign((size_t)b->n_grid * g->n_str * S, 0.0);
+        pwmax.assign((size_t)b->n_grid * g->n_str, 0.0);
+        for (int gi = 0; gi < b->n_grid; ++gi)
+            for (int j = 0; j < g->n_str; ++j) {
+                if (j == g->ctrl_idx) continue;
+                double* row = &pwc[((size_t)gi * g->n_str + j) * S];
+                for (int e = g->csr_ptr[j]; e < g->csr_ptr[j + 1]; ++e) {
+                    const int f = g->col_to_fol[g->csr_col[e]];
+                    if (f < 0) continue;
+                    const double* sp = b->s_pw + ((size_t)gi * g->n_fol + f) * S;
+                    for (int k = 0; k < S; ++k) row[k] = row[k] + std::sqrt(sp[k] / b->q[gi]);
+                }
+                double m = 0.0;
+                for (int k = 0; k < S; ++k) m = row[k] > m ? row[k] : m;
+                pwmax[(size_t)gi * g->n_str + j] = m;
+            }
+    }
+    // parameter tables [inv_c | st_off | cap | pw_c | pw_max]: staged in one of the graph's pinned host
     // buffers so the copy is truly asynchronous (a pageable copy would stall the host)
     {
         std::lock_guard<std::mutex> lk(g->stage_mu);
@@ -669,6 +702,10 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
         std::memcpy(tab + p.off_invc, invc.data(), invc.size() * sizeof(double));
         std::memcpy(tab + p.off_stoff, p.st_off.data(), p.st_off.size() * sizeof(int64_t));
         std::memcpy(tab + p.off_cap, p.cap.data(), p.cap.size() * sizeof(int));
+        if (!pwc.empty()) {
+            std::memcpy(tab + p.off_pwc, pwc.data(), pwc.size() * sizeof(double));
+            std::memcpy(tab + p.off_pwmax, pwmax.data(), pwmax.size() * sizeof(double));
+        }
         if (hipMemcpyAsync(ws, tab, p.tables_bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
             hipEventRecord(st.done, s) != hipSuccess)
             return RQ_EHIP;
@@ -676,7 +713,8 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
     if (hipMemsetAsync(out->status, 0, sizeof(int32_t) * p.R, s) != hipSuccess) return RQ_EHIP;
 
     const int ctrl_stream_kind =
-        (b->ctrl_kind == RQ_SRC_OPT || b->ctrl_kind == RQ_SRC_NONE) ? RQ_SRC_NONE : b->ctrl_kind;
+        (b->ctrl_kind == RQ_SRC_OPT || b->ctrl_kind == RQ_SRC_OPTPW || b->ctrl_kind == RQ_SRC_NONE)
+            ? RQ_SRC_NONE : b->ctrl_kind;
     for (int64_t c0 = 0; c0 < p.R; c0 += p.chunk) {
         const int64_t C = std::min(p.chunk, p.R - c0);
         GenArgs ga{};
@@ -735,6 +773,12 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
         sa.ctrl_seed0 = b->ctrl_seed0;
         sa.src_id = g->d_src_id.p;
         sa.inv_c = (const double*)(ws + p.off_invc);
+        if (b->ctrl_kind == RQ_SRC_OPTPW) {
+            sa.pw_c = (const double*)(ws + p.off_pwc);
+            sa.pw_max = (const double*)(ws + p.off_pwmax);
+            sa.n_seg = b->n_seg;
+            sa.period = b->period;
+        }
         sa.csr_ptr = g->d_csr_ptr.p;
         sa.csr_col = g->d_csr_col.p;
         sa.outdeg_f = g->d_outdeg_f.p;

@@ -41,6 +41,10 @@ struct SweepArgs {
     uint32_t ctrl_seed0;
     const int64_t* src_id;     // [n_str]
     const double* inv_c;       // [n_grid][n_str]
+    const double* pw_c;        // OptPWSignificance: [n_grid][n_str][n_seg] (else null)
+    const double* pw_max;      // [n_grid][n_str]
+    int n_seg;
+    double period;
     const int* csr_ptr;        // [n_str + 1]
     const int* csr_col;        // sink columns, edge-list order per source
     const int* outdeg_f;       // [n_str] edges into the controlled source's followers

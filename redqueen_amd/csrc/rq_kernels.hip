@@ -197,7 +197,9 @@ __global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
         }
     }
 
-    const bool opt = a.ctrl_kind == RQ_SRC_OPT;
+    const bool opt = a.ctrl_kind == RQ_SRC_OPT || a.ctrl_kind == RQ_SRC_OPTPW;
+    const double* pwc = a.pw_c ? a.pw_c + (size_t)g * a.n_str * a.n_seg : nullptr;
+    const double* pwm = a.pw_c ? a.pw_max + (size_t)g * a.n_str : nullptr;
     double opt_next = opt ? a.start : RQ_INF;
     const int64_t k = a.seed_mod > 0 ? i % a.seed_mod : i;
     const uint32_t oseed = a.ctrl_seed ? a.ctrl_seed[i] : a.ctrl_seed0 + (uint32_t)k;
@@ -321,7 +323,8 @@ __global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
         uint64_t ownm = 0;
         double ot = RQ_INF;
         if (opt && a.dbg != 3)
-            controller_tile(n, act, tt, tj, invc, cbf, oseed, ndraw, opt_next, ownm, ot);
+            controller_tile(n, act, tt, tj, invc, cbf, oseed, ndraw, opt_next, ownm, ot, pwc, pwm, a.n_seg,
+                            a.period);
         // ---- C: apply the tile's events in order ----
         if (LOG) {
             for (int q = 0; q < n; ++q) {
@@ -556,7 +559,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(RQ_FW_WPE)
     else gen.none();
     int pos = 0, fil = 0;   // arrivals consumed / generated by this lane's source
 
-    const bool opt = a.ctrl_kind == RQ_SRC_OPT;
+    const bool opt = a.ctrl_kind == RQ_SRC_OPT || a.ctrl_kind == RQ_SRC_OPTPW;
+    const double* pwc = a.pw_c ? a.pw_c + (size_t)g * a.n_str * a.n_seg : nullptr;
+    const double* pwm = a.pw_c ? a.pw_max + (size_t)g * a.n_str : nullptr;
     double opt_next = opt ? a.start : RQ_INF;
     const int64_t k = a.seed_mod > 0 ? i % a.seed_mod : i;
     const uint32_t oseed = a.ctrl_seed ? a.ctrl_seed[i] : a.ctrl_seed0 + (uint32_t)k;
@@ -678,7 +683,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(RQ_FW_WPE)
         // ---- B: RedQueen controller over the tile ----
         uint64_t ownm = 0;
         double ot = RQ_INF;
-        if (opt) controller_tile(n, act, tt, tj, invc, cbf, oseed, ndraw, opt_next, ownm, ot);
+        if (opt) controller_tile(n, act, tt, tj, invc, cbf, oseed, ndraw, opt_next, ownm, ot, pwc, pwm, a.n_seg,
+                            a.period);
 
         // ---- C: aggregates after each event ----
         const bool own_b = act && ((ownm >> lane) & 1ull);       // controller post before #lane

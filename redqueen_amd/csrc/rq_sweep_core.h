@@ -331,14 +331,43 @@ struct RowStage {
 //  post fires before wall event q when the running min beats t_q (ties: lower
 //  src_id first, cbf); a post resets the min.  One prefix-min per post.
 //  Out: ownm bit q = a post right before wall event q, at time ot (lane q).
+//  OptPWSignificance (pwc != null, opt_model.py:547-623): the candidate is the first
+//  point after t_q of a Poisson process whose intensity is the event's increment
+//  pw_j[k] over the periodic significance segments k of T, drawn by thinning at
+//  the bound max_k pw_j[k] from the phase t_q mod T (take_one_sample, :558-573);
+//  event q's draws are Philox calls (event index, iteration) -- any count per lane.
+__device__ __forceinline__ double optpw_sample(double tt, const double* row, double smax, int S,
+                                               double T, uint64_t e, uint32_t oseed)
+{
+    if (!(smax > 0.0)) return RQ_INF;
+    const double inv = 1.0 / smax;
+    const double ph = fmod(tt, T);
+    double ns = 0.0;
+    for (uint32_t it = 1; it < (1u << 20); ++it) {
+        uint32_t w4[4] = {(uint32_t)e, (uint32_t)(e >> 32), it, 0u};
+        philox4x32_10(w4, oseed, kind_salt(RQ_SRC_OPTPW, true));
+        ns = ns + rq_std_exponential(rq_uniform53(w4[0], w4[1])) * inv;
+        int idx = (int)(((double)S * fmod(ns + ph, T)) / T);
+        idx = idx < S ? idx : S - 1;
+        if (rq_uniform53(w4[2], w4[3]) < row[idx] / smax) return tt + ns;
+    }
+    return RQ_INF;
+}
+
 __device__ __forceinline__ void controller_tile(int n, bool act, double tt, int tj, const double* invc,
                                                 const int* cbf, uint32_t oseed, uint64_t& ndraw,
-                                                double& opt_next, uint64_t& ownm, double& ot)
+                                                double& opt_next, uint64_t& ownm, double& ot,
+                                                const double* pwc = nullptr,
+                                                const double* pwmax = nullptr, int S = 0,
+                                                double T = 0.0)
 {
     const int lane = lane_id();
     double c = RQ_INF;
     bool cb = false;
-    if (act) {
+    if (act && pwc) {
+        c = optpw_sample(tt, pwc + (size_t)tj * S, pwmax[tj], S, T, ndraw + (uint64_t)lane, oseed);
+        cb = cbf[tj] != 0;
+    } else if (act) {
         const uint64_t d = ndraw + (uint64_t)lane;   // draw d: Philox call d>>1, half d&1
         const uint64_t call = d >> 1;
         uint32_t w4[4] = {(uint32_t)call, (uint32_t)(call >> 32), 0u, 0u};

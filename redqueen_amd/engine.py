@@ -17,7 +17,7 @@ from . import _lib as L
 KIND_BY_NAME = {"Poisson": L.SRC_POISSON, "Poisson2": L.SRC_POISSON2, "Hawkes": L.SRC_HAWKES,
                 "PiecewiseConst": L.SRC_PWCONST, "RealData": L.SRC_REALDATA, "Opt": L.SRC_OPT}
 CTRL_BY_NAME = {"opt": L.SRC_OPT, "poisson": L.SRC_POISSON2, "pwconst": L.SRC_PWCONST,
-                "times": L.SRC_REALDATA, "wall": L.SRC_NONE}
+                "times": L.SRC_REALDATA, "wall": L.SRC_NONE, "sig": L.SRC_OPTPW}
 
 
 def _arr(x, dt):
@@ -136,10 +136,12 @@ class Graph:
     def run(self, ctrl="opt", q=1.0, s=None, n_rep=1, ctrl_seed=0, world_seed=0,
             randomize=False, seed_mod=0, ctrl_rate=None, Ks=(1,), max_events=None,
             event_log=False, cap_scale=1.0, chunk=0, stream=None, check=True, sweep_mode=0, replica0=0, n_local=0,
-            plan_only=False):
+            plan_only=False, s_pw=None, period=None):
         """Enqueue one batch.  ``q``: scalar or [n_grid]; ``s``: per grid point
         row(s) over the sorted followers ([n_grid, F]) or anything ``s_matrix``
-        takes.  Seeds: int base (seed + replica id) or a device uint32 tensor."""
+        takes.  Seeds: int base (seed + replica id) or a device uint32 tensor.
+        ``ctrl="sig"`` (OptPWSignificance): ``s_pw`` [F, S] or [n_grid, F, S] over the
+        sorted followers and ``period`` T."""
         dev = torch.device("cuda", torch.cuda.current_device())
         ck = CTRL_BY_NAME[ctrl] if isinstance(ctrl, str) else int(ctrl)
         qv = _arr(np.atleast_1d(q), np.float64)
@@ -154,6 +156,16 @@ class Graph:
                 raise ValueError("s must be [n_grid, n_followers]")
         else:
             sm = np.zeros((n_grid, max(1, self.n_followers)))
+        spw = None
+        if ck == L.SRC_OPTPW:
+            if s_pw is None or period is None:
+                raise ValueError("s_pw and period required for OptPWSignificance")
+            spw = np.asarray(s_pw, dtype=np.float64)
+            if spw.ndim == 2:
+                spw = np.broadcast_to(spw, (n_grid,) + spw.shape)
+            spw = np.ascontiguousarray(spw)
+            if spw.ndim != 3 or spw.shape[:2] != (n_grid, self.n_followers) or spw.shape[2] < 1:
+                raise ValueError("s_pw must be [n_grid, n_followers, n_segments]")
         R_all = n_grid * int(n_rep)
         R = int(n_local) if n_local else R_all - int(replica0)
         Ks = _arr(Ks, np.int32)
@@ -199,6 +211,10 @@ class Graph:
         b.sweep_mode = int(sweep_mode)
         b.replica0 = int(replica0)
         b.n_local = int(n_local)
+        if spw is not None:
+            b.n_seg = spw.shape[2]
+            b.period = float(period)
+            b.s_pw = spw.ctypes.data_as(L._pd)
         lib = L.lib()
         if plan_only:
             info = (C.c_int64 * 8)()

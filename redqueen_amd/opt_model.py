@@ -208,13 +208,28 @@ class Opt(Broadcaster):
 
 
 class OptPWSignificance(Broadcaster):
-    """opt_model.py:547-623 -- SURVEY 8(f) 'next'; no kernel in this round."""
+    """RedQueen with a piecewise-constant periodic significance (opt_model.py:547-623):
+    s_vec is [followers x segments] (or one row of segments spread to every follower,
+    :590-604) over time_period; run by the sweep kernels' OptPWSignificance controller."""
+    _rq_kind = L.SRC_OPTPW
 
     def __init__(self, src_id, seed, s_vec, time_period, q=1.0):
         super().__init__(src_id, seed)
         self.s_pw = np.asarray(s_vec)
         self.q = q
+        self.old_ranks = 0
         self.time_period = time_period
+        self.init = False
+
+    def _s_pw_for(self, n_followers):
+        s_pw = np.asarray(self.s_pw, dtype=np.float64)
+        if s_pw.ndim == 1:
+            # Spread the same s_pw to all the followers (opt_model.py:590-602)
+            s_pw = s_pw.repeat(n_followers).reshape((n_followers, -1), order='F')
+        if s_pw.ndim != 2 or s_pw.shape[0] != n_followers:
+            raise ValueError("operands could not be broadcast together: significance rows {} vs "
+                             "{} followers".format(s_pw.shape[0] if s_pw.ndim else 0, n_followers))
+        return s_pw
 
 
 # ----------------------------------------------------------------------- Manager
@@ -261,11 +276,11 @@ class Manager:
         ctrl = None
         if self.sim_opts is not None:
             for s in self.sources:
-                if s.src_id == self.sim_opts.src_id and isinstance(s, (Opt, Poisson2,
+                if s.src_id == self.sim_opts.src_id and isinstance(s, (Opt, OptPWSignificance, Poisson2,
                                                                        PiecewiseConst, RealData)):
                     ctrl = s
         if ctrl is None:
-            opts = [s for s in self.sources if isinstance(s, Opt)]
+            opts = [s for s in self.sources if isinstance(s, (Opt, OptPWSignificance))]
             if len(opts) > 1:
                 raise NotImplementedError("more than one Opt broadcaster in one run")
             ctrl = opts[0] if opts else None
@@ -281,7 +296,7 @@ class Manager:
         ctrl = self._controlled()
         others = [s for s in self.sources if s is not ctrl]
         for s in others:
-            if s._rq_kind is None or s._rq_kind == L.SRC_OPT:
+            if s._rq_kind is None or s._rq_kind in (L.SRC_OPT, L.SRC_OPTPW):
                 raise NotImplementedError("broadcaster %s has no engine kernel" %
                                           type(s).__name__)
         if ctrl is None:
@@ -305,6 +320,10 @@ class Manager:
             else:
                 s = np.ones(g.n_followers) * np.asarray(ctrl.s, dtype=float)
             res = g.run("opt", q=ctrl.q, s=s, ctrl_seed=seed, max_events=maxev, event_log=True)
+        elif isinstance(ctrl, OptPWSignificance):
+            res = g.run("sig", q=ctrl.q, s_pw=ctrl._s_pw_for(g.n_followers),
+                        period=float(ctrl.time_period), ctrl_seed=seed, max_events=maxev,
+                        event_log=True)
         elif isinstance(ctrl, Poisson2):
             res = g.run("poisson", ctrl_seed=seed, ctrl_rate=[float(ctrl.rate)], max_events=maxev,
                         event_log=True)
@@ -398,7 +417,26 @@ class SimOpts:
 
     def create_manager_with_significance(self, seed, time_period, significance=None,
                                          num_segments=None):
-        raise NotImplementedError("OptPWSignificance is SURVEY 8(f) 'next' -- not in this round")
+        """Manager with an OptPWSignificance broadcaster (opt_model.py:850-884): the
+        significance, or s extended to num_segments per follower."""
+        num_followers = len(self.sink_ids)
+        if significance is not None:
+            significance = np.asarray(significance).astype(float)
+        else:
+            s_vec = np.asarray(self.s)
+            if s_vec.shape[0] == 1 and num_segments is not None:
+                s_vec = np.ones((num_followers, num_segments), dtype=float) * s_vec[:, None]
+            if num_segments is not None:
+                s_vec = np.ones((num_followers, num_segments)) * s_vec[:, None]
+            significance = s_vec
+        assert len(significance.shape) == 2, "Significance must be 2 dimensional."
+        assert significance.shape[1] == num_segments or num_segments is None, \
+            "Number of segments in significance do not match"
+        assert significance.shape[0] == len(self.sink_ids), \
+            "Number of sink_ids is not the same as size of significance."
+        opt_pw = OptPWSignificance(src_id=self.src_id, seed=seed, s_vec=significance,
+                                   time_period=time_period, q=self.q)
+        return Manager(sim_opts=self, sources=[opt_pw] + self.create_other_sources())
 
     def create_manager_for_wall(self):
         edge_list = [x for x in self.edge_list if x[0] != self.src_id]

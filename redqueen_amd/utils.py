@@ -495,3 +495,114 @@ def sweep_q(sim_opts, capacity_cap, tol=1e-2, verbose=False, q_init=None, parall
 
     # Step 3: Return
     return q
+
+
+# ------------------------------------------------------------ significance sweeps
+def significance_q_int_worker(params):
+    sim_opts, seed, time_period = params
+    m = sim_opts.create_manager_with_significance(seed, significance=sim_opts.s,
+                                                  time_period=time_period)
+    m.run_dynamic()
+    return num_tweets_of(m.state.get_dataframe(), sim_opts=sim_opts)
+
+
+def calc_significance_capacity_iter(sim_opts, q, time_period, seeds=None, parallel=True,
+                                    max_events=None):
+    """OptPWSignificance capacities per seed at this q (utils.py:496-518), with
+    sim_opts.s as the [sinks x segments] significance.  parallel=True (the
+    reference's pool path: posts per replica) is one GPU batch over the seeds;
+    parallel=False keeps the reference's sequential path, which scores u_int_opt."""
+    from .batch import compiled_graph
+    import torch
+    if seeds is None:
+        seeds = range(1000, 1025)
+    sim_opts = sim_opts.update({'q': q})
+    seeds = np.asarray(list(seeds), dtype=np.int64)
+    if not parallel:
+        capacities = np.zeros(len(seeds), dtype=float)
+        for idx, seed in enumerate(seeds):
+            m = sim_opts.create_manager_with_significance(seed=int(seed), significance=sim_opts.s,
+                                                          time_period=time_period)
+            m.run_dynamic()
+            capacities[idx] = u_int_opt(m.state.get_dataframe(), sim_opts=sim_opts)
+        return capacities
+    from .opt_model import OptPWSignificance
+    g = compiled_graph(sim_opts)
+    sig = np.asarray(sim_opts.s, dtype=float)
+    assert sig.ndim == 2 and sig.shape[0] == len(sim_opts.sink_ids), \
+        "Number of sink_ids is not the same as size of significance."
+    spw = OptPWSignificance(sim_opts.src_id, 0, sig, time_period, q)._s_pw_for(g.n_followers)
+    res = g.run("sig", q=float(q), s_pw=spw, period=float(time_period), n_rep=len(seeds),
+                ctrl_seed=torch.as_tensor(seeds), max_events=max_events)
+    return res.num_events.double().cpu().numpy()
+
+
+def sweep_q_with_significance(sim_opts, capacity_cap, time_period, tol=1e-2, parallel=True,
+                              verbose=False, q_init=None):
+    """utils.py:610-700: sweep_q for the OptPWSignificance broadcaster; every
+    capacity estimate is one GPU batch (calc_significance_capacity_iter)."""
+
+    def terminate_cond(new_capacity):
+        return abs(new_capacity - capacity_cap) / capacity_cap < tol or \
+            np.ceil(capacity_cap - 1) <= new_capacity <= np.ceil(capacity_cap + 1)
+
+    def cap_at(q):
+        return calc_significance_capacity_iter(sim_opts=sim_opts, q=q, time_period=time_period,
+                                               parallel=parallel).mean()
+
+    if q_init is None:
+        r_t = rank_of_src_in_df(_wall_df(sim_opts), -1)
+        q_init = (4 * (r_t.iloc[-1].mean() ** 2) * (sim_opts.end_time) ** 2) / \
+            (np.pi * np.pi * (capacity_cap + 1) ** 4)
+        if verbose:
+            logTime('q_init = {}'.format(q_init))
+
+    init_cap = cap_at(q_init)
+    if terminate_cond(init_cap):
+        logTime('q_init meets the conditions.')
+        return q_init
+    if verbose:
+        logTime('Initial capacity = {}, target capacity = {}, q_init = {}'
+                .format(init_cap, capacity_cap, q_init))
+
+    q = q_init
+    if init_cap < capacity_cap:
+        while True:
+            q_hi = q
+            q /= 2.0
+            q_lo = q
+            capacity = cap_at(q)
+            if verbose:
+                logTime('q = {}, capacity = {}'.format(q, capacity))
+            if terminate_cond(capacity):
+                return q
+            if capacity >= capacity_cap:
+                break
+    else:
+        while True:
+            q_lo = q
+            q *= 2.0
+            q_hi = q
+            capacity = cap_at(q)
+            if verbose:
+                logTime('q = {}, capacity = {}'.format(q, capacity))
+            if terminate_cond(capacity):
+                return q
+            if capacity <= capacity_cap:
+                break
+
+    if verbose:
+        logTime('q_hi = {}, q_lo = {}'.format(q_hi, q_lo))
+
+    while True:
+        q = (q_hi + q_lo) / 2.0
+        new_capacity = cap_at(q)
+        if verbose:
+            logTime('new_capacity = {}, q = {}'.format(new_capacity, q))
+        if terminate_cond(new_capacity):
+            break
+        elif new_capacity > capacity_cap:
+            q_lo = q
+        else:
+            q_hi = q
+    return q

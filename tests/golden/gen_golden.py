@@ -24,6 +24,8 @@ installed and there is no network) and records, as plain data:
   sweepq.npz       utils.sweep_q (sequential) on std_poisson(1, 100): q_init, the
                    returned q and calc_q_capacity_iter per (q, seed);
                    rank_of_src_in_df tables and u_int_opt values
+  dist_sig.npz     (--sig-dist N) N-replica OptPWSignificance ensemble (K3 network,
+                   24-segment follower significance, randomized worlds)
   sig_runs.npz     OptPWSignificance runs (notebook "Testing out significance",
                    opt_broadcast.ipynb:5469, :5569): events + metrics
   graphs.npz       opt_runs.make_edge_list networks (C3 parameters) and a
@@ -448,6 +450,35 @@ def gen_sig():
     np.savez_compressed(os.path.join(HERE, "sig_runs.npz"), **rec)
 
 
+# OptPWSignificance ensemble: the K3 network with a follower- and phase-dependent
+# significance (24 segments of a period 10), worlds randomize_other_sources(r), seed r
+SIG_SEGS = 24
+
+
+def sig_matrix():
+    k = np.arange(SIG_SEGS)
+    return np.stack([0.2 + np.sin(np.pi * k / SIG_SEGS) ** 2,
+                     1.5 * (0.1 + np.cos(2 * np.pi * k / SIG_SEGS) ** 2)])
+
+
+def _sig_worker(r):
+    so = SimOpts(s=np.asarray([1.0, 1.0]), **KAT_BASE)
+    w = so.randomize_other_sources(r)
+    m = w.create_manager_with_significance(r, time_period=10.0, significance=sig_matrix())
+    m.run_dynamic()
+    df = m.state.get_dataframe()
+    met, own, world = metrics(df, so)
+    return np.concatenate([[own, world, m.state.get_num_events()], met])
+
+
+def gen_sig_dist(n):
+    with mp.Pool(os.cpu_count()) as pool:
+        res = np.asarray(pool.map(_sig_worker, range(n), chunksize=16))
+    cols = ["posts", "world", "events"] + ["top%d" % k for k in KS] + ["avg", "r2"]
+    np.savez_compressed(os.path.join(HERE, "dist_sig.npz"), data=res, cols=np.asarray(cols),
+                        sig=sig_matrix())
+
+
 # ---------------------------------------------------------------- ensembles
 def _c2_worker(r):
     so = SimOpts(**README)
@@ -537,11 +568,16 @@ if __name__ == "__main__":
     ap.add_argument("--only", default="")
     ap.add_argument("--no-worlds", action="store_true")
     ap.add_argument("--worlds", action="store_true", help="only dist_world.npz")
+    ap.add_argument("--sig-dist", type=int, default=0, help="only dist_sig.npz with N replicas")
     a = ap.parse_args()
     steps = {"npsum": gen_npsum, "draws": gen_draws, "readme": gen_readme, "kats": gen_kats,
              "adv": gen_adversarial, "graphs": gen_graphs, "frac": gen_frac,
              "oracle": gen_oracle, "sweepq": gen_sweepq, "sig": gen_sig}
-    if a.worlds:
+    if a.sig_dist:
+        gen_sig_dist(a.sig_dist)
+        print("done sig dist", flush=True)
+        a.worlds = True   # nothing else
+    elif a.worlds:
         gen_worlds()
         print("done worlds", flush=True)
     for k, f in steps.items():

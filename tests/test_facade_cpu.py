@@ -62,8 +62,11 @@ def test_factories_and_validation():
         PiecewiseConst(2, 0, change_times=[0, 5, 3], rates=[1, 2, 3])
     m = Manager([Opt(1, 0), Poisson(2, 0)], sink_ids=[1, 2], end_time=1.0)
     assert m.edge_list == [(1, 1), (1, 2), (2, 1), (2, 2)]
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(IndexError):   # scalar s: the reference indexes s.shape[0] too
         so.create_manager_with_significance(1, 10.0)
+    m = so.update({"s": np.asarray([1.0, 2.0, 3.0])}).create_manager_with_significance(
+        1, 10.0, num_segments=4)
+    assert m.sources[0].s_pw.shape == (3, 4) and m.sources[0].time_period == 10.0
 
 
 def test_dataframe_layout_matches_reference_expansion():

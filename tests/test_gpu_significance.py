@@ -1,0 +1,104 @@
+"""OptPWSignificance on the GPU (controller of every sweep variant) against the CPU
+engine oracle bit for bit, the facade's create_manager_with_significance, the
+batched grid, and the reference's 8k-replica ensemble (99% CI)."""
+import math
+
+import numpy as np
+import pytest
+
+from tests.test_gpu_engine import MODES, _cmp_replica, _ctx, _graph, _mode_kw, _world_with_seeds
+from tests.test_significance_cpu import KAT_BASE, KS
+
+pytestmark = pytest.mark.gpu
+
+
+def _sig(S=24, F=2):
+    k = np.arange(S)
+    return np.stack([0.2 + np.sin(np.pi * k / S + f) ** 2 for f in range(F)])
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("seed", [1, 41])
+def test_kat_graph_bit_exact(seed, mode):
+    torch, engine, graphs, O = _ctx()
+    so = dict(KAT_BASE, s=[1.0, 1.0])
+    g = _graph(engine, so)
+    sig = _sig()
+    Ks = (1, 2, 5)
+    res = g.run("sig", q=1.0, s_pw=sig, period=10.0, n_rep=1, ctrl_seed=seed, Ks=Ks,
+                **_mode_kw(mode))
+    sc = O.Scenario(so, ("sig", seed, sig, 10.0))
+    met, (t, dt, s) = O.engine_metrics(sc, Ks)
+    _cmp_replica(res, 0, met, t, s, Ks)
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_c3_world_randomized_bit_exact(mode):
+    """1000-follower network: per-(stream, segment) intensity tables, 50 sources."""
+    torch, engine, graphs, O = _ctx()
+    so = graphs.c3()
+    g = _graph(engine, so)
+    S = 7
+    rs = np.random.RandomState(3)
+    sig = rs.uniform(0.0, 2.0, (g.n_followers, S)) * (rs.uniform(size=(g.n_followers, 1)) < 0.8)
+    R = 16
+    res = g.run("sig", q=so["q"], s_pw=sig, period=13.0, n_rep=R, ctrl_seed=500, world_seed=500,
+                randomize=True, Ks=(1,), **_mode_kw(mode))
+    for r in range(0, R, 5):
+        u = 500 + r
+        sc = O.Scenario(_world_with_seeds(so, u), ("sig", u, sig, 13.0))
+        met, (t, dt, s) = O.engine_metrics(sc, (1,))
+        _cmp_replica(res, r, met, t, s, (1,))
+
+
+def test_facade_manager_and_grid():
+    torch, engine, graphs, O = _ctx()
+    from redqueen_amd import batch
+    from redqueen_amd import utils as U
+    from redqueen_amd.opt_model import SimOpts
+    so = SimOpts(s=np.asarray([1.0, 1.0]), **KAT_BASE)
+    m = so.create_manager_with_significance(1, time_period=10.0, num_segments=24)
+    m.run_dynamic()
+    df = m.state.get_dataframe()
+    sc = O.Scenario(so.get_dict(), ("sig", 1, np.ones((2, 24)), 10.0))
+    met, (t, dt, s) = O.engine_metrics(sc, (1,))
+    assert U.num_tweets_of(df, sim_opts=so) == np.sum(s == 1)
+    assert U.time_in_top_k(df, K=1, sim_opts=so) == met[0][0]
+    with pytest.raises(AssertionError):
+        so.create_manager_with_significance(1, time_period=10.0, significance=np.ones((3, 4)))
+    # the grid: seeds x q in one launch == the oracle replica by replica
+    sig = _sig()
+    out = batch.run_significance(so, sig, 10.0, seeds=range(20), qs=[0.5, 2.0], Ks=(1,))
+    assert len(out) == 40 and (out.status == 0).all()
+    for i in (0, 7, 25, 39):
+        u, q = int(out.seed[i]), float(out.q[i])
+        sc = O.Scenario(_world_with_seeds(so.update({"q": q}).get_dict(), u), ("sig", u, sig, 10.0))
+        (top, avg, r2, cnt), _ = O.engine_metrics(sc, (1,))
+        assert out.top_1[i] == top[0] and out.avg_rank[i] == avg and out.num_events[i] == cnt[0]
+    # capacity iteration: one batch over seeds 1000..1024 == the oracle
+    so2 = so.update({"s": sig})
+    caps = U.calc_significance_capacity_iter(so2, 0.7, 10.0)
+    sc = O.Scenario(so2.update({"q": 0.7}).get_dict(), ("sig", 0, sig, 10.0))
+    _, cnt, _ = O.engine_batch(sc, 25, 1000, False, (1,), 4)
+    assert np.array_equal(caps, cnt[:, 0].astype(float))
+
+
+def test_ensemble_vs_reference(golden):
+    torch, engine, graphs, O = _ctx()
+    from redqueen_amd import batch
+    from redqueen_amd.opt_model import SimOpts
+    d = golden("dist_sig.npz")
+    cols = [str(c) for c in d["cols"]]
+    ref = {c: d["data"][:, i] for i, c in enumerate(cols)}
+    n = d["data"].shape[0]
+    so = SimOpts(s=np.asarray([1.0, 1.0]), **KAT_BASE)
+    out = batch.run_significance(so, d["sig"], 10.0, seeds=range(n), Ks=KS)
+    assert (out.status == 0).all()
+    eng = {"posts": out.num_events.values, "world": out.world_events.values,
+           "events": out.events.values, "avg": out.avg_rank.values, "r2": out.r_2.values}
+    for k in KS:
+        eng["top%d" % k] = out["top_%d" % k].values
+    for k, v in eng.items():
+        r = ref[k]
+        z = (v.mean() - r.mean()) / math.sqrt(v.var() / len(v) + r.var() / len(r))
+        assert abs(z) < 2.576, (k, r.mean(), v.mean(), z)
