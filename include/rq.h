@@ -30,6 +30,8 @@
  *                       opt_runs.py:129-155)
  *   rq_rank_table       utils.rank_of_src_in_df(df, src)    utils.py:38-56
  *   rq_u_int            utils.u_int_opt(df, ...)            utils.py:59-81
+ *   rq_log_rows /       State.get_dataframe()               opt_model.py:85-97
+ *   rq_log_expand       for every replica of an RQ_RUN_EVENT_LOG batch at once
  *
  * Conventions
  *   - every function returns 0 (RQ_OK) or a negative rq_status; no C++
@@ -242,6 +244,21 @@ int rq_rank_table(const double* t, const int64_t* src, const int32_t* sink_col, 
 int rq_u_int(const double* table, const double* index, int64_t n_t, int32_t n_cols,
              const int32_t* fcol, const double* wts, int32_t n_f, double end_time, double* out,
              void* workspace, size_t workspace_bytes, void* hip_stream);
+
+/* Dataframe rows of a batch's event logs (State.get_dataframe, opt_model.py:85-97):
+ * one row per (event, sink of an edge of the event's source), event order then
+ * edge-list order.  ev_t / ev_src / counts are rq_run_batch's outputs (RQ_RUN_EVENT_LOG,
+ * counts[i][2] = events of replica i), ev_cap their row stride.
+ * rq_log_rows writes row_off[n_rep + 1] (device): replica i owns rows
+ * [row_off[i], row_off[i+1]).  rq_log_expand then fills the five reference columns
+ * (device, row_off[n_rep] rows each): event_id (100 + event index), time_delta
+ * (t_k - t_{k-1}, t_{-1} = start_time), src_id, t, sink_id. */
+int rq_log_rows(rq_graph_t g, const int32_t* ev_src, const int64_t* counts, int64_t n_rep,
+                int64_t ev_cap, int64_t* row_off, void* hip_stream);
+int rq_log_expand(rq_graph_t g, const double* ev_t, const int32_t* ev_src, const int64_t* counts,
+                  int64_t n_rep, int64_t ev_cap, const int64_t* row_off, int64_t* event_id,
+                  double* time_delta, int64_t* src_id, double* t, int64_t* sink_id,
+                  void* hip_stream);
 
 /* Per-kernel timing for benchmarks: rq_timing(1) starts recording HIP events
  * around every kernel this library launches (on the caller's stream);

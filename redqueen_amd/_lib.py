@@ -97,12 +97,14 @@ def lib():
                                 C.c_int64, _P, _P, _P, _P]
     L.rq_u_int.argtypes = [_P, _P, C.c_int64, C.c_int32, _P, _P, C.c_int32, C.c_double, _P, _P,
                            C.c_size_t, _P]
+    L.rq_log_rows.argtypes = [_P, _P, _P, C.c_int64, C.c_int64, _P, _P]
+    L.rq_log_expand.argtypes = [_P, _P, _P, _P, C.c_int64, C.c_int64, _P, _P, _P, _P, _P, _P, _P]
     L.rq_timing.argtypes = [C.c_int]
     L.rq_timing_read.argtypes = [_pd, _pi64]
     for fn in ("rq_timing", "rq_timing_read", "rq_graph_build", "rq_graph_free", "rq_graph_info", "rq_graph_source_ids",
                "rq_graph_followers", "rq_workspace_size", "rq_event_capacity", "rq_run_batch",
                "rq_replay_workspace_size", "rq_metrics_replay", "rq_oracle_workspace_size",
-               "rq_oracle_dp", "rq_rank_table", "rq_u_int"):
+               "rq_oracle_dp", "rq_rank_table", "rq_u_int", "rq_log_rows", "rq_log_expand"):
         getattr(L, fn).restype = C.c_int
     if L.rq_abi_version() != ABI_VERSION:
         raise ImportError("librq.so ABI version mismatch")
@@ -126,4 +128,4 @@ EXPORTED = ["rq_abi_version", "rq_strerror", "rq_graph_build", "rq_graph_free", 
             "rq_graph_source_ids", "rq_graph_followers", "rq_workspace_size",
             "rq_event_capacity", "rq_plan_info", "rq_run_batch", "rq_replay_workspace_size",
             "rq_metrics_replay", "rq_oracle_workspace_size", "rq_oracle_dp", "rq_rank_table",
-            "rq_u_int", "rq_timing", "rq_timing_read"]
+            "rq_u_int", "rq_log_rows", "rq_log_expand", "rq_timing", "rq_timing_read"]

@@ -10,6 +10,9 @@
 //   rq_u_int        utils.u_int_opt (utils.py:59-81): rows of the rank table
 //                   dotted with sqrt(s/q) over the followers, times dt,
 //                   summed in numpy's pairwise order.
+//   rq_log_rows /   State.get_dataframe (opt_model.py:85-97) for a whole batch
+//   rq_log_expand   of event logs: one row per (event, sink of an edge of the
+//                   event's source) in event order then edge-list order.
 //
 // None of these is a dense contraction (no MFMA); they are latency / HBM bound
 // and laid out so that every global access of a wavefront is contiguous.
@@ -227,5 +230,148 @@ hipError_t rq_launch_u_int(const UIntArgs& a, hipStream_t s)
         if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
     }
     hipLaunchKernelGGL(rq_u_int_sum_k, dim3(1), dim3(64), npsum_lds_doubles<1>() * sizeof(double), s, a);
+    return hipGetLastError();
+}
+
+// ============================================================================
+// 4. event-log expansion.  rows: one wavefront per replica sums the out-degrees
+//    of its events; a single block turns the per-replica counts into offsets.
+//    expand: one block per replica walks its events in chunks of 1024: a block
+//    scan of the out-degrees gives each event's first row, then every thread
+//    takes consecutive ROWS (binary search of its event in the chunk's offsets in
+//    LDS), so the 40 bytes per row go out as coalesced column stores.
+// ============================================================================
+__global__ __launch_bounds__(256) void rq_log_rows_k(LogArgs a)
+{
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= a.n_rep) return;
+    const int lane = lane_id();
+    const int64_t n = a.counts[r * 4 + 2];
+    const int32_t* src = a.ev_src + r * a.ev_cap;
+    int64_t sum = 0;
+    for (int64_t k = lane; k < n; k += 64) {
+        const int j = src[k];
+        sum += a.csr_ptr[j + 1] - a.csr_ptr[j];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    if (lane == 0) a.row_off[r + 1] = sum;
+}
+
+__global__ __launch_bounds__(1024) void rq_log_scan_k(LogArgs a)
+{
+    __shared__ int64_t wsum[16];
+    __shared__ int64_t carry;
+    const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+    if (tid == 0) {
+        carry = 0;
+        a.row_off[0] = 0;
+    }
+    __syncthreads();
+    for (int64_t b = 0; b < a.n_rep; b += 1024) {
+        const int64_t i = b + tid;
+        int64_t v = i < a.n_rep ? a.row_off[i + 1] : 0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int64_t u = __shfl_up(v, o, 64);
+            if (lane >= o) v += u;
+        }
+        if (lane == 63) wsum[w] = v;
+        __syncthreads();
+        int64_t pre = carry;
+        for (int q = 0; q < w; ++q) pre += wsum[q];
+        if (i < a.n_rep) a.row_off[i + 1] = pre + v;   // inclusive prefix of counts
+        __syncthreads();
+        if (tid == 1023) carry = pre + v;
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void rq_log_expand_k(LogArgs a)
+{
+    constexpr int CH = 1024, PER = CH / 256;
+    __shared__ int64_t off[CH + 1];
+    __shared__ int32_t sj[CH];
+    __shared__ double stt[CH];
+    __shared__ double std_[CH];
+    __shared__ int64_t wsum[4];
+    const int64_t r = blockIdx.x;
+    const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+    const int64_t n = a.counts[r * 4 + 2];
+    const double* T = a.ev_t + r * a.ev_cap;
+    const int32_t* J = a.ev_src + r * a.ev_cap;
+    int64_t row0 = a.row_off[r];
+    for (int64_t c0 = 0; c0 < n; c0 += CH) {
+        const int m = (int)((n - c0) < CH ? (n - c0) : CH);
+        // this thread's PER consecutive events: degrees + a block exclusive scan
+        int64_t loc[PER];
+        int64_t part = 0;
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const int e = tid * PER + q;
+            int64_t d = 0;
+            if (e < m) {
+                const int j = J[c0 + e];
+                const double tk = T[c0 + e];
+                d = a.csr_ptr[j + 1] - a.csr_ptr[j];
+                sj[e] = j;
+                stt[e] = tk;
+                std_[e] = tk - (c0 + e > 0 ? T[c0 + e - 1] : a.start);
+            }
+            loc[q] = part;
+            part += d;
+        }
+        int64_t v = part;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int64_t u = __shfl_up(v, o, 64);
+            if (lane >= o) v += u;
+        }
+        if (lane == 63) wsum[w] = v;
+        __syncthreads();
+        int64_t pre = 0;
+        for (int q = 0; q < w; ++q) pre += wsum[q];
+        const int64_t excl = pre + v - part;
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const int e = tid * PER + q;
+            if (e < m) off[e] = excl + loc[q];
+        }
+        const int64_t chunk_rows = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        if (tid == 0) off[m] = chunk_rows;
+        __syncthreads();
+        // rows of this chunk, one per thread, coalesced
+        for (int64_t x = tid; x < chunk_rows; x += 256) {
+            int lo = 0, hi = m;   // last e with off[e] <= x
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (off[mid] <= x) lo = mid;
+                else hi = mid;
+            }
+            const int e = lo;
+            const int j = sj[e];
+            const int64_t rr = row0 + x;
+            a.event_id[rr] = 100 + c0 + e;
+            a.time_delta[rr] = std_[e];
+            a.src_id[rr] = a.src_ids[j];
+            a.t[rr] = stt[e];
+            a.sink_id[rr] = a.sink_ids[a.csr_col[a.csr_ptr[j] + (x - off[e])]];
+        }
+        row0 += chunk_rows;
+        __syncthreads();
+    }
+}
+
+hipError_t rq_launch_log_rows(const LogArgs& a, hipStream_t s)
+{
+    hipLaunchKernelGGL(rq_log_rows_k, dim3((unsigned)((a.n_rep + 3) / 4)), dim3(256), 0, s, a);
+    if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
+    hipLaunchKernelGGL(rq_log_scan_k, dim3(1), dim3(1024), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t rq_launch_log_expand(const LogArgs& a, hipStream_t s)
+{
+    hipLaunchKernelGGL(rq_log_expand_k, dim3((unsigned)a.n_rep), dim3(256), 0, s, a);
     return hipGetLastError();
 }

@@ -102,6 +102,10 @@ struct rq_graph {
     std::vector<double> p0, p1, p2, arr_a, arr_b;
     std::vector<int> csr_ptr, csr_col, outdeg_f, fol;
     std::vector<int64_t> fol_ids;
+    std::vector<int64_t> sink_ids;   // sorted: the sink column -> sink id map
+    DevBuf<int64_t> d_sink_ids;
+    std::vector<int> csr_col_el;     // sink columns in edge-list order for every stream
+    DevBuf<int> d_csr_col_el;
     std::vector<int> col_to_fol;     // sink column -> follower position or -1
     // per-stream sink bitsets (32 sinks per word) for the K=1 bitset sweep, n_sinks <= 2048
     int nw = 0;
@@ -410,6 +414,7 @@ int rq_graph_build(const rq_graph_desc* d, rq_graph_t* out)
     std::sort(sinks.begin(), sinks.end());
     if (std::adjacent_find(sinks.begin(), sinks.end()) != sinks.end()) return RQ_EINVAL;
     g->n_sinks = d->n_sinks;
+    g->sink_ids = sinks;
     std::unordered_map<int64_t, int> col;
     for (int c = 0; c < g->n_sinks; ++c) col[sinks[c]] = c;
 
@@ -525,6 +530,9 @@ int rq_graph_build(const rq_graph_desc* d, rq_graph_t* out)
         }
         g->outdeg_f.push_back(of);
         g->csr_ptr.push_back((int)g->csr_col.size());
+        // dataframe export: every stream's sinks in edge-list order (the controlled row
+        // above is the sorted follower list the sweep indexes by follower position)
+        for (int c : rows[j]) g->csr_col_el.push_back(c);
     }
 
     if (g->n_sinks <= kBitsMaxSinks) {
@@ -546,7 +554,8 @@ int rq_graph_build(const rq_graph_desc* d, rq_graph_t* out)
         (rc = g->d_fol.upload(g->fol)) || (rc = g->d_seed.upload(g->seed)) ||
         (rc = g->d_p0.upload(g->p0)) || (rc = g->d_p1.upload(g->p1)) ||
         (rc = g->d_p2.upload(g->p2)) || (rc = g->d_arr_a.upload(g->arr_a)) ||
-        (rc = g->d_arr_b.upload(g->arr_b)))
+        (rc = g->d_arr_b.upload(g->arr_b)) || (rc = g->d_sink_ids.upload(g->sink_ids)) ||
+        (rc = g->d_csr_col_el.upload(g->csr_col_el)))
         return rc;
     *out = guard.release();
     return RQ_OK;
@@ -1073,6 +1082,60 @@ int rq_u_int(const double* table, const double* index, int64_t n_t, int32_t n_co
     hipStream_t st = (hipStream_t)hip_stream;
     TimedLaunch tl(K_SCAN, st);
     return rq_launch_u_int(a, st) == hipSuccess ? RQ_OK : RQ_EHIP;
+}
+
+}  // extern "C"
+
+// ============================================================================
+// event-log export (State.get_dataframe at batch scale)
+// ============================================================================
+extern "C" {
+
+int rq_log_rows(rq_graph_t g, const int32_t* ev_src, const int64_t* counts, int64_t n_rep,
+                int64_t ev_cap, int64_t* row_off, void* hip_stream)
+{
+    if (!g || !ev_src || !counts || !row_off || n_rep < 1 || ev_cap < 1) return RQ_EINVAL;
+    LogArgs a{};
+    a.ev_src = ev_src;
+    a.counts = counts;
+    a.n_rep = n_rep;
+    a.ev_cap = ev_cap;
+    a.csr_ptr = g->d_csr_ptr.p;
+    a.n_str = g->n_str;
+    a.row_off = row_off;
+    hipStream_t st = (hipStream_t)hip_stream;
+    TimedLaunch tl(K_REPLAY, st);
+    return rq_launch_log_rows(a, st) == hipSuccess ? RQ_OK : RQ_EHIP;
+}
+
+int rq_log_expand(rq_graph_t g, const double* ev_t, const int32_t* ev_src, const int64_t* counts,
+                  int64_t n_rep, int64_t ev_cap, const int64_t* row_off, int64_t* event_id,
+                  double* time_delta, int64_t* src_id, double* t, int64_t* sink_id,
+                  void* hip_stream)
+{
+    if (!g || !ev_t || !ev_src || !counts || !row_off || n_rep < 1 || ev_cap < 1) return RQ_EINVAL;
+    if (!event_id || !time_delta || !src_id || !t || !sink_id) return RQ_EINVAL;
+    LogArgs a{};
+    a.ev_t = ev_t;
+    a.ev_src = ev_src;
+    a.counts = counts;
+    a.n_rep = n_rep;
+    a.ev_cap = ev_cap;
+    a.csr_ptr = g->d_csr_ptr.p;
+    a.csr_col = g->d_csr_col_el.p;
+    a.n_str = g->n_str;
+    a.src_ids = g->d_src_id.p;
+    a.sink_ids = g->d_sink_ids.p;
+    a.start = g->start;
+    a.row_off = const_cast<int64_t*>(row_off);
+    a.event_id = event_id;
+    a.time_delta = time_delta;
+    a.src_id = src_id;
+    a.t = t;
+    a.sink_id = sink_id;
+    hipStream_t st = (hipStream_t)hip_stream;
+    TimedLaunch tl(K_REPLAY, st);
+    return rq_launch_log_expand(a, st) == hipSuccess ? RQ_OK : RQ_EHIP;
 }
 
 }  // extern "C"

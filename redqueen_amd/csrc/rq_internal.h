@@ -176,3 +176,24 @@ struct UIntArgs {
     double* out;              // [1]
 };
 hipError_t rq_launch_u_int(const UIntArgs& a, hipStream_t s);
+
+struct LogArgs {
+    const double* ev_t;       // [n_rep][ev_cap]
+    const int32_t* ev_src;    // [n_rep][ev_cap] stream indices
+    const int64_t* counts;    // [n_rep][4], [2] = events
+    int64_t n_rep, ev_cap;
+    const int* csr_ptr;       // [n_str + 1]
+    const int* csr_col;       // sink columns, edge-list order per stream
+    int n_str;
+    const int64_t* src_ids;   // [n_str]
+    const int64_t* sink_ids;  // [n_sinks] sorted
+    double start;
+    int64_t* row_off;         // [n_rep + 1]
+    int64_t* event_id;
+    double* time_delta;
+    int64_t* src_id;
+    double* t;
+    int64_t* sink_id;
+};
+hipError_t rq_launch_log_rows(const LogArgs& a, hipStream_t s);
+hipError_t rq_launch_log_expand(const LogArgs& a, hipStream_t s);

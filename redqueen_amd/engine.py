@@ -296,6 +296,50 @@ class BatchResult:
     def n_events(self):
         return self.counts[:, 2]
 
+    def log_columns(self, stream=None):
+        """The reference dataframe rows of every replica's event log, expanded on the
+        GPU (rq_log_rows + rq_log_expand; State.get_dataframe, opt_model.py:85-97).
+        Returns (row_off [R+1] host int64, {event_id, time_delta, src_id, t, sink_id}
+        device tensors); replica i owns rows [row_off[i], row_off[i+1])."""
+        if self.ev_t is None:
+            raise ValueError("run with event_log=True to export the event log")
+        dev = self.ev_t.device
+        R, cap = self.ev_t.shape
+        st = (stream or torch.cuda.current_stream()).cuda_stream
+        row_off = torch.empty(R + 1, dtype=torch.int64, device=dev)
+        lib = L.lib()
+        L.check("rq_log_rows", lib.rq_log_rows(self.graph._h, self.ev_src.data_ptr(),
+                                               self.counts.data_ptr(), R, cap,
+                                               row_off.data_ptr(), st))
+        ro = row_off.cpu().numpy()
+        n = int(ro[-1])
+        cols = {"event_id": torch.empty(n, dtype=torch.int64, device=dev),
+                "time_delta": torch.empty(n, dtype=torch.float64, device=dev),
+                "src_id": torch.empty(n, dtype=torch.int64, device=dev),
+                "t": torch.empty(n, dtype=torch.float64, device=dev),
+                "sink_id": torch.empty(n, dtype=torch.int64, device=dev)}
+        if n:
+            L.check("rq_log_expand", lib.rq_log_expand(
+                self.graph._h, self.ev_t.data_ptr(), self.ev_src.data_ptr(),
+                self.counts.data_ptr(), R, cap, row_off.data_ptr(),
+                *(cols[k].data_ptr() for k in ("event_id", "time_delta", "src_id", "t", "sink_id")),
+                st))
+        return ro, cols
+
+    def dataframe(self, i=None):
+        """State.get_dataframe() of replica i, or of all replicas with a leading
+        'replica' column (i=None); rows expanded on the GPU."""
+        import pandas as pd
+        ro, cols = self.log_columns()
+        host = {k: v.cpu().numpy() for k, v in cols.items()}
+        if i is not None:
+            a, b = int(ro[i]), int(ro[i + 1])
+            return pd.DataFrame({k: host[k][a:b] for k in
+                                 ("event_id", "time_delta", "src_id", "t", "sink_id")})
+        rep = np.repeat(np.arange(len(ro) - 1, dtype=np.int64) + getattr(self, "replica0", 0),
+                        np.diff(ro))
+        return pd.DataFrame(dict(replica=rep, **host))
+
     def events(self, i):
         """(t, src_id) numpy arrays of replica i (needs event_log=True)."""
         n = int(self.counts[i, 2].item())

@@ -47,8 +47,10 @@ class State:
         self._src = np.zeros(0, dtype=np.int64)
         self._edges = []
         self._events = None
+        self._result = None
 
-    def _set_log(self, t, src, edge_list):
+    def _set_log(self, t, src, edge_list, result=None):
+        self._result = result
         self._t = np.asarray(t, dtype=np.float64)
         self._src = np.asarray(src, dtype=np.int64)
         self._edges = list(edge_list)
@@ -77,32 +79,14 @@ class State:
 
     def get_dataframe(self):
         """One row per (event, sink) in event order then edge-list order, columns
-        event_id, time_delta, src_id, t, sink_id (State.get_dataframe, :85-97)."""
-        n = self._t.size
-        srcs = np.asarray([e[0] for e in self._edges], dtype=np.int64)
-        dsts = np.asarray([e[1] for e in self._edges], dtype=np.int64)
-        order = np.argsort(srcs, kind="stable")
-        srcs_sorted, dsts_sorted = srcs[order], dsts[order]
-        uniq, start = np.unique(srcs_sorted, return_index=True)
-        cnt = np.diff(np.concatenate([start, [srcs_sorted.size]]))
-        if n == 0 or uniq.size == 0:
+        event_id, time_delta, src_id, t, sink_id (State.get_dataframe, :85-97); the
+        rows are expanded on the GPU from the run's event log (rq_log_expand)."""
+        if self._result is None or self._t.size == 0:
             return pd.DataFrame.from_records([])
-        pos = np.searchsorted(uniq, self._src)
-        hit = (pos < uniq.size) & (uniq[np.minimum(pos, uniq.size - 1)] == self._src)
-        k_cnt = np.where(hit, cnt[np.minimum(pos, uniq.size - 1)], 0)
-        k_start = np.where(hit, start[np.minimum(pos, uniq.size - 1)], 0)
-        ev = np.repeat(np.arange(n), k_cnt)
-        if ev.size == 0:
+        df = self._result.dataframe(0)
+        if len(df) == 0:
             return pd.DataFrame.from_records([])
-        first = np.repeat(np.cumsum(k_cnt) - k_cnt, k_cnt)
-        within = np.arange(ev.size) - first
-        sink = dsts_sorted[np.repeat(k_start, k_cnt) + within]
-        td = self._time_delta()
-        return pd.DataFrame({"event_id": (100 + ev).astype(np.int64),
-                             "time_delta": td[ev],
-                             "src_id": self._src[ev],
-                             "t": self._t[ev],
-                             "sink_id": sink.astype(np.int64)})
+        return df
 
 
 # ----------------------------------------------------------------- broadcasters
@@ -336,7 +320,7 @@ class Manager:
         for s in self.sources:
             s.used = True
         t, src = res.events(0)
-        self.state._set_log(t, src, self.edge_list)
+        self.state._set_log(t, src, self.edge_list, res)
         self.result = res
         return self
 

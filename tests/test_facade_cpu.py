@@ -69,21 +69,18 @@ def test_factories_and_validation():
     assert m.sources[0].s_pw.shape == (3, 4) and m.sources[0].time_period == 10.0
 
 
-def test_dataframe_layout_matches_reference_expansion():
+def test_state_log_without_a_run():
+    """The event list of a State (the df rows are expanded on the GPU: test_gpu_export)."""
     so = graphs.readme()
     sc = O.Scenario(so, ("opt", 101))
     t, dt, s = O.engine_run(sc)
     st = State(0.0, so["sink_ids"])
+    assert len(st.get_dataframe()) == 0
     st._set_log(t, s, so["edge_list"])
-    df = st.get_dataframe()
-    ref = sc.expand(t, dt, s)
-    assert list(df.columns) == ["event_id", "time_delta", "src_id", "t", "sink_id"]
-    for c in df.columns:
-        assert np.array_equal(df[c].values, ref[c]), c
-    assert str(df.event_id.dtype) == "int64" and str(df.sink_id.dtype) == "int64"
     assert st.get_num_events() == len(t)
     ev = st.events[3]
     assert ev.event_id == 103 and ev.src_id == s[3] and ev.cur_time == t[3]
+    assert ev.time_delta == t[3] - t[2]
 
 
 def test_graph_generators_reproduce_reference_networks(golden):
