@@ -1,0 +1,80 @@
+"""The BASELINE configs beyond the bench line, as GPU parity cases.
+
+C5 (10k followers, 500 bursty Hawkes sources): bit-exact vs the engine oracle on
+a shortened horizon (T=100, ~5e4 events per replica: the oracle finishes in
+seconds) and, at the full T=1000 (~5e5 events per replica), size-independent
+checks: no overflow, batch == sharded sub-batches, event counts at the Hawkes
+mean.  C4 (README graph x 64 q x 4 s): the full grid at 64 replicas per point,
+sharded as 8 ranks would run it, equal to the unsharded grid; grid means move with
+q as RedQueen's budget law says (posts fall as q grows)."""
+import numpy as np
+import pytest
+
+from tests.test_gpu_engine import _cmp_replica, _ctx, _graph, _world_with_seeds
+
+pytestmark = pytest.mark.gpu
+
+
+def test_c5_short_horizon_bit_exact():
+    torch, engine, graphs, O = _ctx()
+    so = dict(graphs.c5(), end_time=100.0)
+    g = _graph(engine, so)
+    R = 8
+    res = g.run("opt", q=so["q"], s=so["s"], n_rep=R, ctrl_seed=40, world_seed=40, randomize=True,
+                Ks=(1, 5))
+    assert int(res.status.max().item()) == 0
+    for r in (0, 5):
+        u = 40 + r
+        sc = O.Scenario(_world_with_seeds(so, u), ("opt", u))
+        met, (t, dt, s) = O.engine_metrics(sc, (1, 5))
+        _cmp_replica(res, r, met, t, s, (1, 5))
+
+
+def test_c5_full_horizon_properties():
+    torch, engine, graphs, O = _ctx()
+    from redqueen_amd import dist
+    so = graphs.c5()
+    g = _graph(engine, so)
+    R = 96
+    kw = dict(q=so["q"], s=so["s"], ctrl_seed=9, world_seed=9, randomize=True, Ks=(1,))
+    full = g.run("opt", n_rep=R, **kw)
+    assert int(full.status.max().item()) == 0
+    parts = []
+    for rank in range(4):
+        a, b = dist.shard(R, 4, rank)
+        parts.append(g.run("opt", n_rep=R, replica0=a, n_local=b - a, **kw).metrics)
+    assert torch.equal(torch.cat(parts), full.metrics)
+    ev = full.counts[:, 1].double().mean().item()   # world events: 500 x l0 T / (1 - a/b)
+    assert abs(ev - 500 * 0.5 * 1000 / 0.5) < 0.02 * 500000, ev
+    top = full.metrics[:, 0].cpu().numpy()
+    assert np.all((top >= 0) & (top <= 1000.0))
+
+
+def test_c4_grid_sharded():
+    torch, engine, graphs, O = _ctx()
+    from redqueen_amd import dist
+    so = graphs.readme()
+    g = _graph(engine, so)
+    grid = graphs.c4_grid()
+    qs = np.asarray([q for q, _ in grid])
+    sm = np.asarray([[s1, s2] for _, (s1, s2) in grid])
+    n_rep = 64
+    kw = dict(q=qs, s=sm, ctrl_seed=0, world_seed=0, randomize=True, Ks=(1,), seed_mod=n_rep)
+    full = g.run("opt", n_rep=n_rep, **kw)
+    assert int(full.status.max().item()) == 0
+    m8 = []
+    for rank in range(8):
+        a, b = dist.shard(len(grid) * n_rep, 8, rank)
+        m8.append(g.run("opt", n_rep=n_rep, replica0=a, n_local=b - a, **kw).metrics)
+    assert torch.equal(torch.cat(m8), full.metrics)
+    posts = full.counts[:, 0].double().reshape(len(grid), n_rep).mean(1).cpu().numpy()
+    for si in range(4):
+        p = posts[si * 64:(si + 1) * 64]
+        assert p[0] > p[-1] and np.all(np.diff(p) <= 0.05 * p[0] + 5.0)
+    # a replica of the grid == the oracle at its (q, s, seed)
+    for gi in (0, 64 * 1 + 17, 64 * 3 + 63):
+        u = 0   # seed_mod = n_rep: replica 0 of every grid point runs seed 0
+        dd = dict(so, q=float(qs[gi]), s=sm[gi])
+        (top, avg, r2, cnt), _ = O.engine_metrics(O.Scenario(_world_with_seeds(dd, u), ("opt", u)), (1,))
+        row = full.metrics[gi * n_rep].cpu().numpy()
+        assert row[0] == top[0] and row[1] == avg and row[2] == r2
