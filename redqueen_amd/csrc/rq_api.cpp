@@ -253,7 +253,7 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     p->log = (b->flags & RQ_RUN_EVENT_LOG) || b->max_events >= 0 || b->sweep_mode == 2 ||
              (has_rd && b->sweep_mode != 1 && b->sweep_mode != 5);
     for (int q = 0; q < b->nK; ++q) p->log = p->log || b->Ks[q] > 32767;   // int16 ranks
-    if (p->log) p->spl = 8;
+    if (p->log) p->spl = g->n_str <= 64 ? 1 : 8;
 
     p->mstride = g->nw | 1;   // odd row stride: one LDS bank per stream for a given word
     p->bits = !p->log && p->nK == 1 && b->Ks[0] == 1 && g->nw > 0 && b->sweep_mode != 3 &&
@@ -311,10 +311,12 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
 
     // fused windowed sweep: one stream per lane, rings of W arrivals generated in LDS,
     // a window of H per ring in registers; (W, H, waves per block) for the most waves per CU
+    const bool pw = b->ctrl_kind == RQ_SRC_OPTPW;
     p->fw = !p->log && g->n_str <= 64 && b->sweep_mode != 4 && b->sweep_mode != 5;
     if (p->fw) {
         int best = -1;
         const int c16 = p->bits ? 1 : (g->n_sinks <= 65535 ? 1 : 0);
+        if (pw && !c16) p->fw = false;   // OptPWSignificance fused instances: uint16 columns
         const size_t colb = p->bits ? 4 * (size_t)g->n_str * p->mstride
                                     : (c16 ? 2 * g->csr_col.size() : 0);
         size_t sh = 0;
@@ -325,7 +327,9 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
         int only_w = 0;
         if (const char* e = getenv("RQ_FW_W")) only_w = atoi(e);   // tuning only
         for (int W : {16, 8}) {
+            if (!p->fw) break;
             if (only_w && W != only_w) continue;
+            if (pw && W != 16) continue;
             const int H = W / 2;
             const size_t r_off = align_up(8 * (size_t)g->n_str, 16);
             const size_t w_off = align_up(r_off + (p->bits ? 0 : 2 * (size_t)p->n_sinks_pad), 16);
@@ -334,7 +338,7 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
             for (int wpb : {16, 12, 10, 8, 6, 5, 4, 3, 2, 1}) {
                 const size_t tot = sh + wpb * stride;
                 if (tot > kLdsMax) continue;
-                int blocks = rq_fw_blocks_per_cu(p->nK, c16, W, p->bits, wpb, tot);
+                int blocks = rq_fw_blocks_per_cu(p->nK, c16, W, p->bits, wpb, tot, pw);
                 if (blocks <= 0) blocks = (int)std::min<size_t>(kLdsMax / tot, 16 / wpb);
                 const int waves = blocks * wpb;
                 const int score = waves * 4 + (W == 16 ? 1 : 0);
@@ -612,7 +616,8 @@ int rq_plan_info(rq_graph_t g, const rq_batch_desc* b, int64_t* info)
     info[1] = p.spl;
     info[2] = p.gwin;
     info[3] = p.gwpb;
-    info[4] = p.fw ? rq_fw_blocks_per_cu(p.nK, p.gcol16, p.gwin, p.bits, p.gwpb, p.g_total)
+    info[4] = p.fw ? rq_fw_blocks_per_cu(p.nK, p.gcol16, p.gwin, p.bits, p.gwpb, p.g_total,
+                                          b->ctrl_kind == RQ_SRC_OPTPW)
                    : rq_sweep_blocks_per_cu(p.spl, p.nK, p.gcol16, p.gwin, p.log, p.bits, p.gwpb, p.g_total);
     info[5] = p.gcol_lds;
     info[6] = (int64_t)p.g_total;

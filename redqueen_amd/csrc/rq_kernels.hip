@@ -165,7 +165,7 @@ __global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
         fil[q] = 0;
     }
     // refill every ring that is at most half full (and not exhausted)
-    auto refill = [&]() {
+    auto refill = [&]() __attribute__((always_inline)) {
 #pragma unroll
         for (int q = 0; q < SPL; ++q) {
             const int j = lane * SPL + q;
@@ -231,12 +231,12 @@ __global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
         xlds = reinterpret_cast<double*>(wb + a.lds_x_off + 12 * (size_t)a.n_sinks_pad);
         ax.init(a.Ks, reinterpret_cast<int*>(rank), xs, a.n_sinks_pad, a.n_sinks, lane);
     }
-    auto close_row = [&]() -> bool {
+    auto close_row = [&]() __attribute__((always_inline)) -> bool {
         pend = false;
         return rs.put(pend_t, ax.row_sum(a.n_sinks, xlds), ax.nvalid, ax.cnt, lane, status);
     };
     // LOG: one event of the log (State.apply_event); false = stop the replica
-    auto event = [&](double tev, bool own, int jw, int e0, int e1) -> bool {
+    auto event = [&](double tev, bool own, int jw, int e0, int e1) __attribute__((always_inline)) -> bool {
         if (a.max_events >= 0 && n_events >= a.max_events) return false;
         if (a.ev_t) es.push(tev, own ? a.ctrl_idx : jw, lane, status);
         ++n_events;
@@ -323,7 +323,7 @@ __global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
         uint64_t ownm = 0;
         double ot = RQ_INF;
         if (opt && a.dbg != 3)
-            controller_tile(n, act, tt, tj, invc, cbf, oseed, ndraw, opt_next, ownm, ot, pwc, pwm, a.n_seg,
+            controller_tile<true>(n, act, tt, tj, invc, cbf, oseed, ndraw, opt_next, ownm, ot, pwc, pwm, a.n_seg,
                             a.period);
         // ---- C: apply the tile's events in order ----
         if (LOG) {
@@ -506,11 +506,8 @@ __global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
 //     events: per sink-bitset word, segmented prefix ORs (segments start at the
 //     posts) give each event's top-1 set, plain prefix ORs its valid set.
 // ============================================================================
-template <int NK, class COL, int W, int H, bool BITS>
-#ifndef RQ_FW_WPE
-#define RQ_FW_WPE 4
-#endif
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(RQ_FW_WPE))) void rq_sweep_fw(SweepArgs a)
+template <int NK, class COL, int W, int H, bool BITS, bool PW = false>
+__global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
 {
     static_assert((W & (W - 1)) == 0 && H <= W, "ring");
     extern __shared__ double lds_g[];
@@ -560,8 +557,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(RQ_FW_WPE)
     int pos = 0, fil = 0;   // arrivals consumed / generated by this lane's source
 
     const bool opt = a.ctrl_kind == RQ_SRC_OPT || a.ctrl_kind == RQ_SRC_OPTPW;
-    const double* pwc = a.pw_c ? a.pw_c + (size_t)g * a.n_str * a.n_seg : nullptr;
-    const double* pwm = a.pw_c ? a.pw_max + (size_t)g * a.n_str : nullptr;
+    // OptPWSignificance only in the PW instances: the thinning loop's registers stay out
+    // of the RedQueen controller's allocation
+    const double* pwc = PW ? a.pw_c + (size_t)g * a.n_str * a.n_seg : nullptr;
+    const double* pwm = PW ? a.pw_max + (size_t)g * a.n_str : nullptr;
     double opt_next = opt ? a.start : RQ_INF;
     const int64_t k = a.seed_mod > 0 ? i % a.seed_mod : i;
     const uint32_t oseed = a.ctrl_seed ? a.ctrl_seed[i] : a.ctrl_seed0 + (uint32_t)k;
@@ -683,7 +682,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(RQ_FW_WPE)
         // ---- B: RedQueen controller over the tile ----
         uint64_t ownm = 0;
         double ot = RQ_INF;
-        if (opt) controller_tile(n, act, tt, tj, invc, cbf, oseed, ndraw, opt_next, ownm, ot, pwc, pwm, a.n_seg,
+        if (opt) controller_tile<PW>(n, act, tt, tj, invc, cbf, oseed, ndraw, opt_next, ownm, ot, pwc, pwm, a.n_seg,
                             a.period);
 
         // ---- C: aggregates after each event ----
@@ -1160,7 +1159,11 @@ hipError_t rq_launch_gen(const GenArgs& a, hipStream_t s)
 hipError_t rq_launch_sweep(const SweepArgs& a, int spl, int nK, int col16, int log, int bits, hipStream_t s)
 {
     if (a.n_chunk <= 0) return hipSuccess;
-    // event log / max_events: the sequential variant, eight sources per lane, W = 8
+    // event log / max_events: the sequential variant, W = 8; one source per lane when
+    // they fit (the per-lane ring state of eight sources costs ~200 VGPRs and spills)
+    if (log && spl == 1)
+        return col16 ? launch_sweep_k<1, uint16_t, 8, true>(a, nK, s)
+                     : launch_sweep_k<1, int, 8, true>(a, nK, s);
     if (log)
         return col16 ? launch_sweep_k<8, uint16_t, 8, true>(a, nK, s)
                      : launch_sweep_k<8, int, 8, true>(a, nK, s);
@@ -1204,6 +1207,8 @@ static int occ_c(int nK, int col16, int W, int bits, int wpb, size_t lds)
 }
 int rq_sweep_blocks_per_cu(int spl, int nK, int col16, int W, int log, int bits, int wpb, size_t lds)
 {
+    if (log && spl == 1)
+        return col16 ? occ_k<1, uint16_t, 8, true>(nK, wpb, lds) : occ_k<1, int, 8, true>(nK, wpb, lds);
     if (log) return col16 ? occ_k<8, uint16_t, 8, true>(nK, wpb, lds) : occ_k<8, int, 8, true>(nK, wpb, lds);
     switch (spl) {
     case 1: return occ_c<1>(nK, col16, W, bits, wpb, lds);
@@ -1213,52 +1218,61 @@ int rq_sweep_blocks_per_cu(int spl, int nK, int col16, int W, int log, int bits,
     }
 }
 
-// fused windowed sweep: (W, H) in {(16, 8), (8, 4)}
-template <int NK, class COL, int W, bool BITS>
+// fused windowed sweep: (W, H) in {(16, 8), (8, 4)}; OptPWSignificance (PW) instances
+// exist for uint16 columns and W = 16 only (make_plan keeps other PW runs off this path)
+template <int NK, class COL, int W, bool BITS, bool PW = false>
 static hipError_t launch_fw_t(const SweepArgs& a, hipStream_t s)
 {
     const unsigned blocks = (unsigned)((a.n_chunk + a.wpb - 1) / a.wpb);
-    hipLaunchKernelGGL((rq_sweep_fw<NK, COL, W, W / 2, BITS>), dim3(blocks), dim3(64 * a.wpb), a.lds_total, s, a);
+    hipLaunchKernelGGL((rq_sweep_fw<NK, COL, W, W / 2, BITS, PW>), dim3(blocks), dim3(64 * a.wpb), a.lds_total, s, a);
     return hipGetLastError();
 }
-template <class COL, int W>
+template <class COL, int W, bool PW = false>
 static hipError_t launch_fw_k(const SweepArgs& a, int nK, hipStream_t s)
 {
     switch (nK) {
-    case 1: return launch_fw_t<1, COL, W, false>(a, s);
-    case 2: return launch_fw_t<2, COL, W, false>(a, s);
-    case 3: return launch_fw_t<3, COL, W, false>(a, s);
-    default: return launch_fw_t<4, COL, W, false>(a, s);
+    case 1: return launch_fw_t<1, COL, W, false, PW>(a, s);
+    case 2: return launch_fw_t<2, COL, W, false, PW>(a, s);
+    case 3: return launch_fw_t<3, COL, W, false, PW>(a, s);
+    default: return launch_fw_t<4, COL, W, false, PW>(a, s);
     }
 }
 hipError_t rq_launch_sweep_fw(const SweepArgs& a, int nK, int col16, int W, int bits, hipStream_t s)
 {
     if (a.n_chunk <= 0) return hipSuccess;
+    if (a.pw_c) {
+        if (!col16 || W != 16) return hipErrorInvalidValue;
+        return bits ? launch_fw_t<1, uint16_t, 16, true, true>(a, s) : launch_fw_k<uint16_t, 16, true>(a, nK, s);
+    }
     if (bits) return W == 16 ? launch_fw_t<1, uint16_t, 16, true>(a, s) : launch_fw_t<1, uint16_t, 8, true>(a, s);
     if (W == 16) return col16 ? launch_fw_k<uint16_t, 16>(a, nK, s) : launch_fw_k<int, 16>(a, nK, s);
     return col16 ? launch_fw_k<uint16_t, 8>(a, nK, s) : launch_fw_k<int, 8>(a, nK, s);
 }
-template <int NK, class COL, int W, bool BITS>
+template <int NK, class COL, int W, bool BITS, bool PW = false>
 static int occ_fw_t(int wpb, size_t lds)
 {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rq_sweep_fw<NK, COL, W, W / 2, BITS>, 64 * wpb, lds) !=
-        hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rq_sweep_fw<NK, COL, W, W / 2, BITS, PW>, 64 * wpb,
+                                                      lds) != hipSuccess)
         return 0;
     return nb;
 }
-template <class COL, int W>
+template <class COL, int W, bool PW = false>
 static int occ_fw_k(int nK, int wpb, size_t lds)
 {
     switch (nK) {
-    case 1: return occ_fw_t<1, COL, W, false>(wpb, lds);
-    case 2: return occ_fw_t<2, COL, W, false>(wpb, lds);
-    case 3: return occ_fw_t<3, COL, W, false>(wpb, lds);
-    default: return occ_fw_t<4, COL, W, false>(wpb, lds);
+    case 1: return occ_fw_t<1, COL, W, false, PW>(wpb, lds);
+    case 2: return occ_fw_t<2, COL, W, false, PW>(wpb, lds);
+    case 3: return occ_fw_t<3, COL, W, false, PW>(wpb, lds);
+    default: return occ_fw_t<4, COL, W, false, PW>(wpb, lds);
     }
 }
-int rq_fw_blocks_per_cu(int nK, int col16, int W, int bits, int wpb, size_t lds)
+int rq_fw_blocks_per_cu(int nK, int col16, int W, int bits, int wpb, size_t lds, int pw)
 {
+    if (pw) {
+        if (!col16 || W != 16) return -1;
+        return bits ? occ_fw_t<1, uint16_t, 16, true, true>(wpb, lds) : occ_fw_k<uint16_t, 16, true>(nK, wpb, lds);
+    }
     if (bits) return W == 16 ? occ_fw_t<1, uint16_t, 16, true>(wpb, lds) : occ_fw_t<1, uint16_t, 8, true>(wpb, lds);
     if (W == 16) return col16 ? occ_fw_k<uint16_t, 16>(nK, wpb, lds) : occ_fw_k<int, 16>(nK, wpb, lds);
     return col16 ? occ_fw_k<uint16_t, 8>(nK, wpb, lds) : occ_fw_k<int, 8>(nK, wpb, lds);

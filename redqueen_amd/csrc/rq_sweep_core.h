@@ -354,6 +354,7 @@ __device__ __forceinline__ double optpw_sample(double tt, const double* row, dou
     return RQ_INF;
 }
 
+template <bool PW>
 __device__ __forceinline__ void controller_tile(int n, bool act, double tt, int tj, const double* invc,
                                                 const int* cbf, uint32_t oseed, uint64_t& ndraw,
                                                 double& opt_next, uint64_t& ownm, double& ot,
@@ -364,7 +365,7 @@ __device__ __forceinline__ void controller_tile(int n, bool act, double tt, int 
     const int lane = lane_id();
     double c = RQ_INF;
     bool cb = false;
-    if (act && pwc) {
+    if (PW && act && pwc) {
         c = optpw_sample(tt, pwc + (size_t)tj * S, pwmax[tj], S, T, ndraw + (uint64_t)lane, oseed);
         cb = cbf[tj] != 0;
     } else if (act) {

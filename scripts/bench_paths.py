@@ -1,0 +1,108 @@
+"""Secondary measurements (not the bench line): the HBM-facing kernels of the path.
+
+  * sweep with the event log on (RQ_RUN_EVENT_LOG, the sequential-exact variant):
+    writes 12 B per event (t f64 + source i32) + 24 B per pivot row
+  * rq_log_rows + rq_log_expand: State.get_dataframe rows for a whole batch,
+    12 B read per event + 40 B written per (event, sink) row
+  * rq_scan: 24 B read per pivot row (timed inside the plain C3 run)
+  * rq_metrics_replay on a reference-layout df: 28 B read per df row
+  * rq_oracle_dp: n = 8000 walls, 64 instances
+Per-kernel times come from the library's HIP events (rq_timing) on the launch stream.
+usage: python scripts/bench_paths.py [--reps N]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from redqueen_amd import _lib as L  # noqa: E402
+from redqueen_amd import engine, graphs, utils  # noqa: E402
+
+PEAK = 8000.0
+
+
+def timed(fn, reps=3):
+    fn()
+    torch.cuda.synchronize()
+    ms = np.zeros(5)
+    nl = np.zeros(5, dtype=np.int64)
+    L.lib().rq_timing(1)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        out = fn()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / reps
+    L.lib().rq_timing_read(ms.ctypes.data_as(L._pd), nl.ctypes.data_as(L._pi64))
+    L.lib().rq_timing(0)
+    return out, ms / reps, wall
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    torch.cuda.set_device(0)
+    so = graphs.c3()
+    g = engine.Graph(so["src_id"], so["other_sources"], so["sink_ids"], so["edge_list"], so["end_time"])
+    res = {}
+
+    # 1. sweep with the event log
+    R = 2048
+    run = lambda: g.run("opt", q=so["q"], s=so["s"], n_rep=R, ctrl_seed=0, world_seed=0,  # noqa: E731
+                        randomize=True, event_log=True, check=False)
+    r, ms, wall = timed(run, a.reps)
+    ev = int(r.counts[:, 2].sum())
+    rows = int(r.counts[:, 3].sum())
+    b = 12 * ev + 24 * rows
+    res["sweep_event_log"] = {"replicas": R, "events": ev, "ms": ms[1], "bytes": b,
+                              "GBps": b / ms[1] / 1e6, "frac": b / ms[1] / 1e6 / PEAK}
+
+    # 2. batch dataframe expansion (64 replicas keeps the output ~2 GB)
+    R2 = 64
+    r2 = g.run("opt", q=so["q"], s=so["s"], n_rep=R2, ctrl_seed=0, world_seed=0, randomize=True,
+               event_log=True)
+    (ro, cols), ms, wall = timed(lambda: r2.log_columns(), a.reps)
+    nrow = int(ro[-1])
+    ev2 = int(r2.counts[:, 2].sum())
+    b = 40 * nrow + 12 * ev2 * 2   # rows written; events read by both passes
+    res["log_expand"] = {"replicas": R2, "rows": nrow, "ms": ms[3], "bytes": b,
+                         "GBps": b / ms[3] / 1e6, "frac": b / ms[3] / 1e6 / PEAK}
+
+    # 3. scan inside the plain (fused) C3 run
+    R3 = 10000
+    run3 = lambda: g.run("opt", q=so["q"], s=so["s"], n_rep=R3, ctrl_seed=0, world_seed=0,  # noqa: E731
+                         randomize=True, check=False)
+    r3, ms, wall = timed(run3, a.reps)
+    rows3 = int(r3.counts[:, 3].sum())
+    res["scan"] = {"replicas": R3, "rows": rows3, "ms": ms[2], "bytes": 24 * rows3,
+                   "GBps": 24 * rows3 / ms[2] / 1e6, "frac": 24 * rows3 / ms[2] / 1e6 / PEAK}
+
+    # 4. replay of one reference-layout df (~7e5 rows)
+    df = r2.dataframe(0)
+    _, ms, wall = timed(lambda: utils.replay_metrics(df, so["src_id"], so["end_time"], (1,)), a.reps)
+    res["replay"] = {"rows": len(df), "ms": ms[3] + ms[2], "wall_ms": wall * 1e3,
+                     "GBps": 28 * len(df) / (ms[3] + ms[2]) / 1e6}
+
+    # 5. oracle DP
+    rs = np.random.RandomState(0)
+    n = 8000
+    ws = []
+    for i in range(64):
+        t = np.cumsum(rs.exponential(0.01, n))
+        ws.append(np.diff(np.concatenate([[0.0, 0.0], t, [t[-1] + 1.0]])))
+    qs, ss = list(rs.uniform(1, 100, 64)), [1.0] * 64
+    _, ms, wall = timed(lambda: utils.oracle_dp_batch(ws, qs, ss), a.reps)
+    cells = 64 * n * n / 2
+    res["oracle_dp"] = {"instances": 64, "n": n, "ms": ms[3], "wall_ms": wall * 1e3,
+                        "Gcells_per_s": cells / ms[3] / 1e6}
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
