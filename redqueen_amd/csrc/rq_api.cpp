@@ -45,6 +45,7 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // stream around every kernel, summed by rq_timing_read.  Off by default.
 enum { K_GEN = 0, K_SWEEP = 1, K_SCAN = 2, K_REPLAY = 3, K_MERGE = 4, K_N = 5 };
 bool g_timing = false;
+unsigned long long* g_clk = nullptr;   // RQ_PHASE_CLOCK builds: the sweep's phase clocks
 
 std::vector<std::pair<hipEvent_t, hipEvent_t>> g_ev[K_N];
 
@@ -836,6 +837,15 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             sa.nw = g->nw;
             sa.mstride = p.mstride;
             if (const char* d = getenv("RQ_SWEEP_DBG")) sa.dbg = atoi(d);   // profiling only
+#ifdef RQ_PHASE_CLOCK
+            {
+                static unsigned long long* clk = nullptr;
+                if (!clk && hipMalloc(&clk, 8 * sizeof(unsigned long long)) == hipSuccess)
+                    (void)hipMemset(clk, 0, 8 * sizeof(unsigned long long));
+                sa.clk = clk;
+                g_clk = clk;
+            }
+#endif
             sa.lds_total = p.g_total;
             sa.lds_stage_off = p.g_stage_off;
             sa.gen = ga;
@@ -1144,3 +1154,17 @@ int rq_log_expand(rq_graph_t g, const double* ev_t, const int32_t* ev_src, const
 }
 
 }  // extern "C"
+
+extern "C" int rq_phase_clock(unsigned long long* host8)
+{
+    // RQ_PHASE_CLOCK diagnostic builds only: copy out and clear the per-phase
+    // s_memtime sums of every rq_sweep_fw wave since the last call
+    if (!host8) return RQ_EINVAL;
+    for (int q = 0; q < 8; ++q) host8[q] = 0;
+    if (!g_clk) return RQ_EUNSUPPORTED;
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(host8, g_clk, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemset(g_clk, 0, 8 * sizeof(unsigned long long)) != hipSuccess)
+        return RQ_EHIP;
+    return RQ_OK;
+}

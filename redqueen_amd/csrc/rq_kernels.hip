@@ -551,6 +551,20 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
     __syncthreads();
     if (!live) return;
 
+#ifdef RQ_PHASE_CLOCK
+    unsigned long long ck[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long tk = __builtin_amdgcn_s_memtime();
+#define RQ_CLK(q)                                                   \
+    do {                                                            \
+        const unsigned long long t2 = __builtin_amdgcn_s_memtime(); \
+        ck[q] += t2 - tk;                                           \
+        tk = t2;                                                    \
+    } while (0)
+#else
+#define RQ_CLK(q) \
+    do {          \
+    } while (0)
+#endif
     SrcGen gen;
     if (lane < a.n_str) gen.init(a.gen, lane, i);
     else gen.none();
@@ -595,6 +609,7 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
                 }
             }
         }
+        RQ_CLK(0);   // A1: ring refills (arrival generation)
         const int avail = fil - pos;
         double v[H];
 #pragma unroll
@@ -646,6 +661,7 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
             n = (int)wave_sum_u32((uint32_t)c);
         }
 
+        RQ_CLK(1);   // window + A2 cut
         // ---- A3: stage in stream order, rank-sort into (t, stream) order ----
 #pragma unroll
         for (int q = 0; q < H; ++q)
@@ -658,10 +674,13 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
         const double ti = act ? st_t[lane] : RQ_INF;
         const int ji = act ? st_j[lane] : 0;
         int rnk = 0;
-        for (int q = 0; q < n; ++q) {
-            const double tq = bcast_d(ti, q);
-            rnk += (tq < ti || (tq == ti && q < lane)) ? 1 : 0;
-        }
+        if (a.dbg != 4)   // profiling only: 4 = skip the rank sort
+            for (int q = 0; q < n; ++q) {
+                const double tq = bcast_d(ti, q);
+                rnk += (tq < ti || (tq == ti && q < lane)) ? 1 : 0;
+            }
+        else
+            rnk = lane;
         wave_lds_sync();
         if (act) {
             st_t[rnk] = ti;
@@ -679,12 +698,14 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
             e1 = cptr[tj + 1];
             od = odf[tj];
         }
+        RQ_CLK(2);   // A3 stage + rank sort
         // ---- B: RedQueen controller over the tile ----
         uint64_t ownm = 0;
         double ot = RQ_INF;
-        if (opt) controller_tile<PW>(n, act, tt, tj, invc, cbf, oseed, ndraw, opt_next, ownm, ot, pwc, pwm, a.n_seg,
+        if (opt && a.dbg != 3) controller_tile<PW>(n, act, tt, tj, invc, cbf, oseed, ndraw, opt_next, ownm, ot, pwc, pwm, a.n_seg,
                             a.period);
 
+        RQ_CLK(3);   // B controller
         // ---- C: aggregates after each event ----
         const bool own_b = act && ((ownm >> lane) & 1ull);       // controller post before #lane
         const bool strm_own = act && !opt && tj == a.ctrl_idx;   // controlled stream's arrival
@@ -695,7 +716,9 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
         int ocnt[NK], wcnt[NK];
 #pragma unroll
         for (int kq = 0; kq < NK; ++kq) ocnt[kq] = wcnt[kq] = 0;
-        if (BITS) {
+        if (a.dbg == 1) {
+            // profiling only: skip phase C
+        } else if (BITS) {
             // segments of the tile start at its own events (posts / own-stream arrivals)
             const bool rst = own_b || strm_own;
             const uint64_t rm = __ballot(rst);
@@ -777,14 +800,20 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
                 }
             }
         }
+        RQ_CLK(4);   // C aggregates
         const uint64_t mo = __ballot(has_o), ma = mo | __ballot(has_w);
         n_events += n + __popcll(ownm);
         posts += __popcll(mo) + __popcll(__ballot(has_w && strm_own));
         world += __popcll(__ballot(has_w && !strm_own));
         if (ma && place_rows<NK>(rs, ma, has_o, has_w, ot, tt, osum, oval, ocnt, wsum, wval, wcnt, status))
             stop = true;
+        RQ_CLK(5);   // rows
         if (stop || fin) break;
     }
+#ifdef RQ_PHASE_CLOCK
+    if (lane == 0 && a.clk)
+        for (int q = 0; q < 6; ++q) atomicAdd(&a.clk[q], ck[q]);
+#endif
     // the controller's last post after the final arrival
     if (!stop && opt && opt_next <= a.end) {
         ++n_events;
