@@ -782,7 +782,7 @@ static int engine_stream(const rqo_source* s, uint32_t salt, double start, doubl
                 if (!(tc <= end)) return 0;
                 double decay = rq_exp(nbeta * (tc - tau));
                 double rate = l0 + eta * decay;
-                if (v < rate / B) {
+                if (v * B < rate) {   /* engine: division-free thinning test */
                     eta = eta * decay + alpha;
                     tau = tc;
                     if (dvec_push(out, tc)) return -1;
@@ -803,7 +803,7 @@ static int engine_stream(const rqo_source* s, uint32_t salt, double start, doubl
             double v = pnext(&p);
             int64_t idx = bisect_right(s->a, s->n_arr, t) - 1;
             if (idx < 0) idx += s->n_arr;
-            if (v < s->b[idx] / mx)
+            if (v * mx < s->b[idx])
                 if (dvec_push(out, t)) return -1;
         }
     }
@@ -836,7 +836,7 @@ static double optpw_sample(double tt, const double* row, double smax, int64_t S,
         ns = ns + rq_std_exponential(rq_uniform53(w4[0], w4[1])) * inv;
         int64_t idx = (int64_t)(((double)S * fmod(ns + ph, T)) / T);
         idx = idx < S ? idx : S - 1;
-        if (rq_uniform53(w4[2], w4[3]) < row[idx] / smax) return tt + ns;
+        if (rq_uniform53(w4[2], w4[3]) * smax < row[idx]) return tt + ns;
     }
     return INFINITY;
 }

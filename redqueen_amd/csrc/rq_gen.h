@@ -7,7 +7,8 @@
 //   Hawkes              opt_model.py:466-490 -- Ogata thinning, bound B = lambda at
 //                       the last accepted arrival (not refreshed on rejection), the
 //                       exponential kernel's O(1) recurrence for lambda; two draws
-//                       (Exp, uniform) per candidate
+//                       (Exp, uniform) per candidate; accept when U * B < lambda
+//                       (the reference's U < lambda / B, division-free)
 //   PiecewiseConst      opt_model.py:642-663 -- thinning of exponential gaps at the
 //                       max rate; two draws per candidate
 //   RealData            opt_model.py:722-750 -- the given (host-filtered) times
@@ -142,7 +143,7 @@ struct SrcGen {
         if (kind == RQ_SRC_HAWKES) {
             const double decay = rq_exp(nbeta * (tc - tau));
             const double rate = p0 + eta * decay;
-            if (u2 < rate / B) {
+            if (u2 * B < rate) {   // u2 < rate / B without the f64 division
                 eta = eta * decay + p1;
                 tau = tc;
                 needB = true;
@@ -160,7 +161,7 @@ struct SrcGen {
         }
         int idx = lo - 1;
         if (idx < 0) idx += na;
-        if (u2 < tb[idx] / p0) {
+        if (u2 * p0 < tb[idx]) {
             *out = tc;
             return true;
         }

@@ -349,7 +349,7 @@ __device__ __forceinline__ double optpw_sample(double tt, const double* row, dou
         ns = ns + rq_std_exponential(rq_uniform53(w4[0], w4[1])) * inv;
         int idx = (int)(((double)S * fmod(ns + ph, T)) / T);
         idx = idx < S ? idx : S - 1;
-        if (rq_uniform53(w4[2], w4[3]) < row[idx] / smax) return tt + ns;
+        if (rq_uniform53(w4[2], w4[3]) * smax < row[idx]) return tt + ns;
     }
     return RQ_INF;
 }
