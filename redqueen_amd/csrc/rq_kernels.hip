@@ -673,14 +673,19 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
         const bool act = lane < n;
         const double ti = act ? st_t[lane] : RQ_INF;
         const int ji = act ? st_j[lane] : 0;
+        // rank = #staged arrivals before this one in (t, stream) order; the staged
+        // times are read back from LDS two at a time (a broadcast ds_read_b128: every
+        // lane reads the same address) instead of two v_readlanes per element
         int rnk = 0;
-        if (a.dbg != 4)   // profiling only: 4 = skip the rank sort
-            for (int q = 0; q < n; ++q) {
-                const double tq = bcast_d(ti, q);
-                rnk += (tq < ti || (tq == ti && q < lane)) ? 1 : 0;
+        if (a.dbg != 4) {   // profiling only: 4 = skip the rank sort
+            for (int q = 0; q < n; q += 2) {
+                const double2 tq = *reinterpret_cast<const double2*>(st_t + q);
+                rnk += (tq.x < ti || (tq.x == ti && q < lane)) ? 1 : 0;
+                rnk += (q + 1 < n && (tq.y < ti || (tq.y == ti && q + 1 < lane))) ? 1 : 0;
             }
-        else
+        } else {
             rnk = lane;
+        }
         wave_lds_sync();
         if (act) {
             st_t[rnk] = ti;
