@@ -252,8 +252,8 @@ class Graph:
             if not ovf:
                 # equal event times in the fast tiled sweep: redo with the exact sequential
                 # sweep (never taken by continuous-time worlds; RealData runs are exact already)
-                seq = (event_log or b.max_events >= 0 or b.sweep_mode in (1, 2, 5) or self.has_realdata
-                       or ck == L.SRC_REALDATA)
+                seq = (b.max_events >= 0 or b.sweep_mode in (1, 2, 5) or self.has_realdata
+                       or ck == L.SRC_REALDATA or (event_log and self.n_streams > 64))
                 if not seq and int((status & L.ST_TIE).any().item()):
                     b.sweep_mode = 2
                     continue

@@ -42,16 +42,19 @@ def _oracle(O, so, ctrl, Ks, max_events=None):
     return met, t, s
 
 
-MODES = ["fast", "scatter", "log", "legacy"]
+MODES = ["fast", "scatter", "log", "legacy", "fastlog"]
 
 
 def _mode_kw(mode):
     """fast: the fused windowed sweep (K=1 runs on sink bitsets); scatter: the same
     with per-sink LDS ranks (sweep_mode=3); log: the sequential event-log variant
     (sweep_mode=2), events compared too; legacy: pre-generated streams + serial
-    wave-min merge (sweep_mode=4)."""
+    wave-min merge (sweep_mode=4); fastlog: the fused sweep writing the event log
+    itself (event_log=True, auto mode), events compared too."""
     if mode == "log":
         return dict(event_log=True, sweep_mode=2)
+    if mode == "fastlog":
+        return dict(event_log=True, sweep_mode=0)
     return dict(event_log=False, sweep_mode={"scatter": 3, "legacy": 4}.get(mode, 0))
 
 
