@@ -287,14 +287,14 @@ __global__ __launch_bounds__(1024) void rq_log_scan_k(LogArgs a)
     }
 }
 
-__global__ __launch_bounds__(256) void rq_log_expand_k(LogArgs a)
+__global__ __launch_bounds__(1024) void rq_log_expand_k(LogArgs a)
 {
-    constexpr int CH = 1024, PER = CH / 256;
+    constexpr int NT = 1024, CH = 1024, NW = NT / 64;   // one event per thread per chunk
     __shared__ int64_t off[CH + 1];
     __shared__ int32_t sj[CH];
     __shared__ double stt[CH];
     __shared__ double std_[CH];
-    __shared__ int64_t wsum[4];
+    __shared__ int64_t wsum[NW];
     const int64_t r = blockIdx.x;
     const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
     const int64_t n = a.counts[r * 4 + 2];
@@ -303,25 +303,18 @@ __global__ __launch_bounds__(256) void rq_log_expand_k(LogArgs a)
     int64_t row0 = a.row_off[r];
     for (int64_t c0 = 0; c0 < n; c0 += CH) {
         const int m = (int)((n - c0) < CH ? (n - c0) : CH);
-        // this thread's PER consecutive events: degrees + a block exclusive scan
-        int64_t loc[PER];
-        int64_t part = 0;
-#pragma unroll
-        for (int q = 0; q < PER; ++q) {
-            const int e = tid * PER + q;
-            int64_t d = 0;
-            if (e < m) {
-                const int j = J[c0 + e];
-                const double tk = T[c0 + e];
-                d = a.csr_ptr[j + 1] - a.csr_ptr[j];
-                sj[e] = j;
-                stt[e] = tk;
-                std_[e] = tk - (c0 + e > 0 ? T[c0 + e - 1] : a.start);
-            }
-            loc[q] = part;
-            part += d;
+        // this thread's event: degree + a block exclusive scan
+        const int e = tid;
+        int64_t d = 0;
+        if (e < m) {
+            const int j = J[c0 + e];
+            const double tk = T[c0 + e];
+            d = a.csr_ptr[j + 1] - a.csr_ptr[j];
+            sj[e] = j;
+            stt[e] = tk;
+            std_[e] = tk - (c0 + e > 0 ? T[c0 + e - 1] : a.start);
         }
-        int64_t v = part;
+        int64_t v = d;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const int64_t u = __shfl_up(v, o, 64);
@@ -329,33 +322,30 @@ __global__ __launch_bounds__(256) void rq_log_expand_k(LogArgs a)
         }
         if (lane == 63) wsum[w] = v;
         __syncthreads();
-        int64_t pre = 0;
-        for (int q = 0; q < w; ++q) pre += wsum[q];
-        const int64_t excl = pre + v - part;
-#pragma unroll
-        for (int q = 0; q < PER; ++q) {
-            const int e = tid * PER + q;
-            if (e < m) off[e] = excl + loc[q];
+        int64_t pre = 0, chunk_rows = 0;
+        for (int q = 0; q < NW; ++q) {
+            pre += q < w ? wsum[q] : 0;
+            chunk_rows += wsum[q];
         }
-        const int64_t chunk_rows = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        if (e < m) off[e] = pre + v - d;
         if (tid == 0) off[m] = chunk_rows;
         __syncthreads();
-        // rows of this chunk, one per thread, coalesced
-        for (int64_t x = tid; x < chunk_rows; x += 256) {
+        // rows of this chunk, one per thread, coalesced column stores
+        for (int64_t x = tid; x < chunk_rows; x += NT) {
             int lo = 0, hi = m;   // last e with off[e] <= x
             while (hi - lo > 1) {
                 const int mid = (lo + hi) >> 1;
                 if (off[mid] <= x) lo = mid;
                 else hi = mid;
             }
-            const int e = lo;
-            const int j = sj[e];
+            const int ev = lo;
+            const int j = sj[ev];
             const int64_t rr = row0 + x;
-            a.event_id[rr] = 100 + c0 + e;
-            a.time_delta[rr] = std_[e];
+            a.event_id[rr] = 100 + c0 + ev;
+            a.time_delta[rr] = std_[ev];
             a.src_id[rr] = a.src_ids[j];
-            a.t[rr] = stt[e];
-            a.sink_id[rr] = a.sink_ids[a.csr_col[a.csr_ptr[j] + (x - off[e])]];
+            a.t[rr] = stt[ev];
+            a.sink_id[rr] = a.sink_ids[a.csr_col[a.csr_ptr[j] + (x - off[ev])]];
         }
         row0 += chunk_rows;
         __syncthreads();
@@ -372,6 +362,6 @@ hipError_t rq_launch_log_rows(const LogArgs& a, hipStream_t s)
 
 hipError_t rq_launch_log_expand(const LogArgs& a, hipStream_t s)
 {
-    hipLaunchKernelGGL(rq_log_expand_k, dim3((unsigned)a.n_rep), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(rq_log_expand_k, dim3((unsigned)a.n_rep), dim3(1024), 0, s, a);
     return hipGetLastError();
 }

@@ -63,8 +63,9 @@ def main():
     res["sweep_event_log"] = {"replicas": R, "events": ev, "ms": ms[1], "bytes": b,
                               "GBps": b / ms[1] / 1e6, "frac": b / ms[1] / 1e6 / PEAK}
 
-    # 2. batch dataframe expansion (64 replicas keeps the output ~2 GB)
-    R2 = 64
+    # 2. batch dataframe expansion: 256 replicas (one block each, enough to fill the
+    #    256 CUs; ~7 GB of columns)
+    R2 = 256
     r2 = g.run("opt", q=so["q"], s=so["s"], n_rep=R2, ctrl_seed=0, world_seed=0, randomize=True,
                event_log=True)
     (ro, cols), ms, wall = timed(lambda: r2.log_columns(), a.reps)
