@@ -839,6 +839,8 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             sa.nw = g->nw;
             sa.mstride = p.mstride;
             if (const char* d = getenv("RQ_SWEEP_DBG")) sa.dbg = atoi(d);   // profiling only
+            sa.tile_target = 58.0;   // measured on C3: 40 -> 895k, 48 -> 943k, 58 -> 964k, 62 -> 956k replicas/s
+            if (const char* e = getenv("RQ_FW_TILE")) sa.tile_target = atof(e);   // tuning only
 #ifdef RQ_PHASE_CLOCK
             {
                 static unsigned long long* clk = nullptr;

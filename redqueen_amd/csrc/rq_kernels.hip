@@ -643,7 +643,7 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
                     break;
                 }
             }
-            if (!trunc) span = (cut - tfirst) * (48.0 / (double)(n > 8 ? n : 8));
+            if (!trunc) span = (cut - tfirst) * (a.tile_target / (double)(n > 8 ? n : 8));
         }
         if (trunc) {
             // the arrivals equal to tfirst, in stream order, up to the first ring whose
