@@ -788,7 +788,10 @@ static int engine_stream(const rqo_source* s, uint32_t salt, double start, doubl
                     if (dvec_push(out, tc)) return -1;
                     break;
                 }
+                /* engine: refreshed bound after a rejection (lambda only decays) */
                 t = tc;
+                B = rate;
+                inv = 1.0 / rate;
             }
         }
     }

@@ -8,7 +8,10 @@
 //                       the last accepted arrival (not refreshed on rejection), the
 //                       exponential kernel's O(1) recurrence for lambda; two draws
 //                       (Exp, uniform) per candidate; accept when U * B < lambda
-//                       (the reference's U < lambda / B, division-free)
+//                       (the reference's U < lambda / B, division-free); after a
+//                       rejection the bound is refreshed to lambda at the candidate
+//                       (the reference keeps the stale bound: same law, more
+//                       candidates)
 //   PiecewiseConst      opt_model.py:642-663 -- thinning of exponential gaps at the
 //                       max rate; two draws per candidate
 //   RealData            opt_model.py:722-750 -- the given (host-filtered) times
@@ -150,6 +153,10 @@ struct SrcGen {
                 *out = tc;
                 return true;
             }
+            // rejected: lambda only decays until the next arrival, so lambda(tc) bounds
+            // it from here on -- thinning continues at the refreshed (lower) bound
+            B = rate;
+            inv = 1.0 / rate;
             return false;
         }
         // PiecewiseConst: rate(t) = rates[bisect_right(change_times, t) - 1]
