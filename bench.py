@@ -126,9 +126,11 @@ def main():
         means = m.mean(0)
         return res, means, ev
 
-    # capacity check once (overflow -> the engine reruns with doubled capacities), then
-    # warmup at full size so the timed region starts with every buffer allocated
-    ok = g.run("opt", q=so["q"], s=so["s"], n_rep=min(R, 512), ctrl_seed=0, world_seed=0,
+    # capacity check once at full size (overflow -> the engine reruns with doubled
+    # capacities; every launch of the run has the timed launches' shape, so a rocprofv3
+    # average over the whole command matches the per-launch HIP-event time), then
+    # warmup so the timed region starts with every buffer allocated
+    ok = g.run("opt", q=so["q"], s=so["s"], n_rep=R, ctrl_seed=0, world_seed=0,
                randomize=True, Ks=Ks, check=True)
     del ok
     def accumulate(res, ev, acc):
