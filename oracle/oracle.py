@@ -77,7 +77,7 @@ def lib():
         L.rqo_engine_run.argtypes = [C.POINTER(_Scenario), C.POINTER(_Events)]
         L.rqo_engine_batch.restype = C.c_int64
         L.rqo_engine_batch.argtypes = [C.POINTER(_Scenario), C.c_int64, C.c_uint32, C.c_int32,
-                                       i32, C.c_int32, C.c_int32, d, C.c_uint32, d, i64]
+                                       i32, C.c_int32, C.c_int32, d, C.c_uint32, C.c_uint32, d, i64]
         L.rqo_oracle_dp.restype = C.c_int
         L.rqo_oracle_dp.argtypes = [d, C.c_int64, C.c_double, C.c_double, d, i64, i64]
         L.rqo_rank_table.restype = C.c_int
@@ -313,7 +313,7 @@ def engine_metrics(sc, Ks=(1,)):
 
 
 def engine_batch(sc, n_rep, seed0=0, randomize=True, Ks=(1,), n_threads=1, ctrl_rates=None,
-                 ctrl_seed_offset=0):
+                 ctrl_seed_offset=0, seed_stride=1):
     """n_rep replicas: replica r uses seed u + ctrl_seed_offset (u = seed0 + r) for the
     controlled source and,
     with randomize, u + 99*idx for other source idx.  Returns (metrics [n_rep, nK+2],
@@ -327,7 +327,7 @@ def engine_batch(sc, n_rep, seed0=0, randomize=True, Ks=(1,), n_threads=1, ctrl_
         rp = _p(rates, C.c_double)
     tot = lib().rqo_engine_batch(C.byref(sc.c), n_rep, seed0, int(randomize),
                                  _p(Ks, C.c_int32), len(Ks), n_threads, rp, ctrl_seed_offset,
-                                 _p(out, C.c_double), _p(cnt, C.c_int64))
+                                 seed_stride, _p(out, C.c_double), _p(cnt, C.c_int64))
     if tot < 0:
         raise RuntimeError("rqo_engine_batch failed: %d" % tot)
     return out, cnt, tot

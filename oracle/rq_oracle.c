@@ -962,7 +962,7 @@ double rqo_spec_exp(double x) { return rq_exp(x); }
 
 typedef struct {
     const rqo_scenario* sc; int64_t r0, r1; uint32_t seed0; int randomize; const double* rates;
-    uint32_t ctrl_off;
+    uint32_t ctrl_off, stride;
     const int32_t* Ks; int32_t nK; double* out; int64_t* counts; int64_t events; int rc;
 } batch_job;
 
@@ -987,7 +987,7 @@ static void* batch_worker(void* arg)
         sinkmap_n[i] = sinks_of(sc, sc->sources[i].src_id, sinkmap[i]);
     }
     for (int64_t r = j->r0; r < j->r1; r++) {
-        uint32_t u = j->seed0 + (uint32_t)r;
+        uint32_t u = j->seed0 + j->stride * (uint32_t)r;
         memcpy(srcs, sc->sources, sizeof(rqo_source) * ns);
         srcs[0].seed = u + j->ctrl_off;
         if (j->rates) srcs[0].p0 = j->rates[r];
@@ -1053,7 +1053,7 @@ out:
 
 int64_t rqo_engine_batch(const rqo_scenario* sc, int64_t n_rep, uint32_t seed0,
                          int32_t randomize, const int32_t* Ks, int32_t nK,
-                         int32_t n_threads, const double* ctrl_rates, uint32_t ctrl_seed_offset,
+                         int32_t n_threads, const double* ctrl_rates, uint32_t ctrl_seed_offset, uint32_t seed_stride,
                          double* out, int64_t* counts)
 {
     if (n_threads < 1) n_threads = 1;
@@ -1065,6 +1065,7 @@ int64_t rqo_engine_batch(const rqo_scenario* sc, int64_t n_rep, uint32_t seed0,
         jobs[i].Ks = Ks; jobs[i].nK = nK; jobs[i].out = out; jobs[i].counts = counts;
         jobs[i].rates = ctrl_rates;
         jobs[i].ctrl_off = ctrl_seed_offset;
+        jobs[i].stride = seed_stride ? seed_stride : 1u;
         jobs[i].r0 = n_rep * i / n_threads;
         jobs[i].r1 = n_rep * (i + 1) / n_threads;
         pthread_create(&th[i], NULL, batch_worker, &jobs[i]);

@@ -116,14 +116,15 @@ int rqo_engine_run(const rqo_scenario* sc, rqo_events* ev);
 uint32_t rqo_kind_salt(int32_t kind);
 
 /* Batched CPU baseline: n_rep replicas of the engine model, replica r uses
- * world seeds (u_r + 99*idx) and controlled seed u_r where u_r = seed0 + r,
+ * world seeds (u_r + 99*idx) and controlled seed u_r where u_r = seed0 + stride * r
+ * (seed_stride 0 = 1),
  * metrics with Appendix-B semantics.  out: [n_rep][nK+2], counts [n_rep][3]
  * (posts, world, events).  n_threads pthreads.  ctrl_rates (may be NULL):
  * per-replica rate of a Poisson2 controlled source (sources[0] must be
  * POISSON2).  Returns total events. */
 int64_t rqo_engine_batch(const rqo_scenario* sc, int64_t n_rep, uint32_t seed0,
                          int32_t randomize, const int32_t* Ks, int32_t nK,
-                         int32_t n_threads, const double* ctrl_rates, uint32_t ctrl_seed_offset,
+                         int32_t n_threads, const double* ctrl_rates, uint32_t ctrl_seed_offset, uint32_t seed_stride,
                          double* out, int64_t* counts);
 
 /* rq_oracle_analysis.c: utils.oracle_ranking (utils.py:181-245) on w[0..n+2)

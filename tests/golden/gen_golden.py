@@ -24,6 +24,7 @@ installed and there is no network) and records, as plain data:
   sweepq.npz       utils.sweep_q (sequential) on std_poisson(1, 100): q_init, the
                    returned q and calc_q_capacity_iter per (q, seed);
                    rank_of_src_in_df tables and u_int_opt values
+  dist_c3.npz      (--c3-dist N) N-replica RedQueen ensemble on the C3 bench network
   dist_sig.npz     (--sig-dist N) N-replica OptPWSignificance ensemble (K3 network,
                    24-segment follower significance, randomized worlds)
   sig_runs.npz     OptPWSignificance runs (notebook "Testing out significance",
@@ -479,6 +480,37 @@ def gen_sig_dist(n):
                         sig=sig_matrix())
 
 
+C3_SEED_STRIDE = 5000
+
+
+def _c3_worker(r):
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from redqueen_amd import graphs as G
+    d = G.c3()
+    so = SimOpts(**d)
+    u = C3_SEED_STRIDE * r   # disjoint seed sets per replica (50 sources x 99 < 5000)
+    w = so.randomize_other_sources(u)
+    m = w.create_manager_with_opt(seed=u)
+    m.run_dynamic()
+    df = m.state.get_dataframe()
+    top = U.time_in_top_k(df=df, K=1, sim_opts=so)
+    avg = U.average_rank(df, sim_opts=so)
+    own = len(df.event_id[df.src_id == so.src_id].unique())
+    world = len(df.event_id[df.src_id != so.src_id].unique())
+    return np.asarray([own, world, m.state.get_num_events(), top, avg])
+
+
+def gen_c3_dist(n):
+    """C3 (the bench network) through the reference itself: n replicas, replica r runs
+    world randomize_other_sources(5000 r) and RedQueen seed 5000 r, so no two replicas
+    share a source stream (~41 s per replica per core)."""
+    with mp.Pool(os.cpu_count()) as pool:
+        res = np.asarray(pool.map(_c3_worker, range(n), chunksize=1))
+    np.savez_compressed(os.path.join(HERE, "dist_c3.npz"), data=res,
+                        cols=np.asarray(["posts", "world", "events", "top1", "avg"]),
+                        seed_stride=np.asarray([C3_SEED_STRIDE]))
+
+
 # ---------------------------------------------------------------- ensembles
 def _c2_worker(r):
     so = SimOpts(**README)
@@ -569,11 +601,16 @@ if __name__ == "__main__":
     ap.add_argument("--no-worlds", action="store_true")
     ap.add_argument("--worlds", action="store_true", help="only dist_world.npz")
     ap.add_argument("--sig-dist", type=int, default=0, help="only dist_sig.npz with N replicas")
+    ap.add_argument("--c3-dist", type=int, default=0, help="only dist_c3.npz with N replicas")
     a = ap.parse_args()
     steps = {"npsum": gen_npsum, "draws": gen_draws, "readme": gen_readme, "kats": gen_kats,
              "adv": gen_adversarial, "graphs": gen_graphs, "frac": gen_frac,
              "oracle": gen_oracle, "sweepq": gen_sweepq, "sig": gen_sig}
-    if a.sig_dist:
+    if a.c3_dist:
+        gen_c3_dist(a.c3_dist)
+        print("done c3 dist", flush=True)
+        a.worlds = True   # nothing else
+    elif a.sig_dist:
         gen_sig_dist(a.sig_dist)
         print("done sig dist", flush=True)
         a.worlds = True   # nothing else

@@ -239,3 +239,19 @@ def test_engine_is_deterministic_and_seed_sensitive():
     assert not np.array_equal(a[0], c[0])
     # every event time is within [0, T] and non-decreasing
     assert np.all(np.diff(a[0]) >= 0) and a[0][0] >= 0 and a[0][-1] <= 100.0
+
+
+def test_engine_c3_matches_reference_distribution(golden):
+    """Engine semantics on the C3 bench network vs the reference's replicas of it."""
+    d = golden("dist_c3.npz")
+    cols = [str(c) for c in d["cols"]]
+    ref = {c: d["data"][:, i] for i, c in enumerate(cols)}
+    so = graphs.c3()
+    out, cnt, _ = O.engine_batch(O.Scenario(so, ("opt", 0)), 1024, 500000, True, (1,), 8,
+                                 seed_stride=int(d["seed_stride"][0]))
+    eng = {"posts": cnt[:, 0], "world": cnt[:, 1], "events": cnt[:, 2], "top1": out[:, 0],
+           "avg": out[:, 1]}
+    for k, v in eng.items():
+        r = ref[k]
+        z = (v.mean() - r.mean()) / math.sqrt(v.var() / len(v) + r.var() / len(r))
+        assert abs(z) < 2.576, (k, r.mean(), v.mean(), z)
