@@ -150,7 +150,7 @@ typedef struct rq_batch_desc {
     int32_t sweep_mode;          /* 0 auto: fast tiled sweep unless the run needs the sequential
                                     one (event log, max_events, RealData); 1 fast whenever the
                                     event log / max_events allow; 2 force the sequential sweep;
-                                    3 as 0 but never the K=1 sink-bitset variant;
+                                    3 as 0 but never a K=1 sink-bit variant (per-sink ranks);
                                     4 / 5 as 0 / 1 on the legacy kernels (arrival streams
                                     pre-generated into HBM by rq_gen_streams, serial wave-min
                                     merge) -- kept for A/B parity checks of the fused sweep  */
@@ -191,7 +191,7 @@ int rq_workspace_size(rq_graph_t g, const rq_batch_desc* b, size_t* bytes);
 int rq_event_capacity(rq_graph_t g, const rq_batch_desc* b, int64_t* cap);
 /* how rq_run_batch will run this batch (diagnostics / occupancy reporting):
  * info[0] sweep variant (0 fast tiled, 1 sequential exact, 2 fast tiled on K=1 sink
- * bitsets), [1] sources per lane,
+ * bitsets, 3 fast tiled on K=1 per-wave LDS sink bits; +10 fused), [1] sources per lane,
  * [2] arrival-ring depth W, [3] waves per block, [4] blocks per CU (runtime occupancy,
  * 0 without a device), [5] sink columns in LDS (1) or global (0), [6] dynamic LDS
  * bytes per block, [7] replicas per chunk */

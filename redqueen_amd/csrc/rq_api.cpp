@@ -112,6 +112,8 @@ struct rq_graph {
     int nw = 0;
     std::vector<uint32_t> masks;
     DevBuf<uint32_t> d_mask;
+    std::vector<uint32_t> fbits;   // follower set as a sink bitset (BL sweep)
+    DevBuf<uint32_t> d_fbits;
     // controlled-slot arrays (PiecewiseConst / RealData controlled runs)
     int ctrl_arr_off = 0, ctrl_arr_n = 0;
     DevBuf<int64_t> d_src_id;
@@ -129,6 +131,9 @@ struct Plan {
     std::vector<int64_t> st_off;
     // sequential (event log / max_events) sweep variant; K=1 sink-bitset variant
     bool log = false, bits = false;
+    // K=1 on per-wave LDS sink bits for graphs past the bitset variant (> 64 sources)
+    bool bl = false;
+    size_t g_fb = 0;
     // fused windowed sweep (n_str <= 64): arrivals generated in-kernel, window depth fw_h
     bool fw = false;
     int fw_h = 8, mstride = 1;
@@ -215,7 +220,7 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     p->chunk = b->chunk > 0 ? std::min<int64_t>(b->chunk, p->R) : std::min<int64_t>(p->R, 16384);
     p->cap.assign(g->n_str, 0);
     p->st_off.assign(g->n_str, 0);
-    double wall_caps = 0.0, m_total = 0.0, v_total = 0.0;
+    double wall_caps = 0.0;
     int64_t ctrl_cap = 0;
     for (int j = 0; j < g->n_str; ++j) {
         int kind = g->kind[j];
@@ -223,8 +228,6 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
             kind = (ck == RQ_SRC_OPT || ck == RQ_SRC_OPTPW || ck == RQ_SRC_NONE) ? RQ_SRC_NONE : ck;
         double var;
         const double m = stream_mean_var(g, j, kind, b, &var);
-        m_total += m;
-        v_total += var;
         int64_t c = 0;
         if (kind != RQ_SRC_NONE)
             c = kind == RQ_SRC_REALDATA ? (int64_t)m
@@ -262,13 +265,16 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     p->bits = !p->log && p->nK == 1 && b->Ks[0] == 1 && g->nw > 0 && b->sweep_mode != 3 &&
               (size_t)g->n_str * p->mstride * 4 <= 64 * 1024;
     if (p->bits) p->spl = g->n_str <= 64 ? 1 : g->n_str <= 128 ? 2 : g->n_str <= 256 ? 4 : 8;
+    p->bl = !p->log && !p->bits && p->nK == 1 && b->Ks[0] == 1 && p->spl >= 2 && b->sweep_mode != 3;
+    const int nwl = (g->n_sinks + 31) / 32;
 
     // general sweep: pick (ring depth W, waves per block) for the most waves per CU
     {
         int best = -1;
         // sink columns live in LDS as uint16 when they fit, else they are read from
         // global memory as int (the kernel's COL type selects the path at compile time)
-        for (int col_lds = g->n_sinks <= 65535 ? 1 : 0; col_lds >= 0 && best < 0; --col_lds) {
+        // both placements are scored: LDS columns only win at equal waves per CU
+        for (int col_lds = g->n_sinks <= 65535 ? 1 : 0; col_lds >= 0; --col_lds) {
             const int c16 = col_lds;
             // BITS: sink bitsets [n_str][nw] replace the columns (and the per-wave ranks)
             const size_t colb = p->bits ? 4 * (size_t)g->n_str * p->mstride
@@ -278,12 +284,16 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
             const size_t o_ptr = sh;  sh = align_up(sh + 4 * (g->n_str + 1), 16);
             const size_t o_odf = sh;  sh = align_up(sh + 4 * g->n_str, 16);
             const size_t o_cbf = sh;  sh = align_up(sh + 4 * g->n_str, 16);
+            const size_t o_fb = sh;   if (p->bl) sh = align_up(sh + 4 * (size_t)nwl, 16);
             const int spl = p->spl;
-            for (int W : {16, 8}) {
+            for (int W : {16, 8, 4}) {
                 if (p->log && W != 8) continue;
+                if (p->bl ? W == 16 : W == 4) continue;   // BL instances: W in {8, 4}
                 const size_t r_off = align_up(8 * (size_t)g->n_str, 16);
                 const size_t rank_b = p->log ? 4 : (p->bits ? 0 : 2);   // fast: int16 saturating
-                const size_t w_off = align_up(r_off + rank_b * (size_t)p->n_sinks_pad, 16);
+                // BL: two bits per sink (T, V words) in place of the int16 ranks
+                const size_t w_off = p->bl ? align_up(r_off + 8 * (size_t)nwl, 16)
+                                           : align_up(r_off + rank_b * (size_t)p->n_sinks_pad, 16);
                 // rings: W arrivals for each real source (lanes past n_str own none)
                 size_t stride = align_up(w_off + 8 * (size_t)g->n_str * W, 16);
                 // LOG: per-sink gtag/gcnt/gsum + a wave_npsum<1> scratch (304 doubles)
@@ -295,16 +305,17 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
                     if (tot > kLdsMax) continue;
                     // resident waves per CU: the runtime's occupancy for this instance
                     // (VGPR/SGPR/LDS); without a device, the LDS bound capped at 16
-                    int blocks = rq_sweep_blocks_per_cu(spl, p->nK, c16, W, p->log, p->bits, wpb, tot);
+                    int blocks = rq_sweep_blocks_per_cu(spl, p->nK, c16, W, p->log, p->bl ? 2 : p->bits, wpb, tot);
                     if (blocks <= 0) blocks = (int)std::min<size_t>(kLdsMax / tot, 16 / wpb);
                     const int waves = blocks * wpb;
-                    const int score = waves * 4 + (W == 16 ? 1 : 0);   // W=16 refills half as often
+                    // W=16 refills half as often; LDS columns skip the global latency
+                    const int score = waves * 8 + col_lds * 2 + (W == 16 ? 1 : 0);
                     if (score > best) {
                         best = score;
                         p->gwin = W; p->gwpb = wpb; p->gcol_lds = col_lds; p->gcol16 = c16;
                         p->g_col = o_col; p->g_ptr = o_ptr; p->g_odf = o_odf; p->g_cbf = o_cbf;
                         p->g_wave = sh; p->g_wave_stride = stride; p->g_rank_off = r_off;
-                        p->g_win_off = w_off; p->g_x_off = x_off; p->g_total = tot;
+                        p->g_win_off = w_off; p->g_x_off = x_off; p->g_total = tot; p->g_fb = o_fb;
                     }
                 }
             }
@@ -552,8 +563,12 @@ int rq_graph_build(const rq_graph_desc* d, rq_graph_t* out)
             }
     }
 
+    g->fbits.assign((g->n_sinks + 31) / 32, 0u);
+    for (int c : g->fol) g->fbits[c / 32] |= 1u << (c % 32);
+
     int rc;
     if (g->nw > 0 && (rc = g->d_mask.upload(g->masks))) return rc;
+    if ((rc = g->d_fbits.upload(g->fbits))) return rc;
     if ((rc = g->d_src_id.upload(g->src_id)) || (rc = g->d_kind.upload(g->kind)) ||
         (rc = g->d_orig.upload(g->orig_idx)) || (rc = g->d_arr_off.upload(g->arr_off)) ||
         (rc = g->d_arr_n.upload(g->arr_n)) || (rc = g->d_csr_ptr.upload(g->csr_ptr)) ||
@@ -615,13 +630,14 @@ int rq_plan_info(rq_graph_t g, const rq_batch_desc* b, int64_t* info)
     Plan p;
     const int rc = make_plan(g, b, &p);
     if (rc) return rc;
-    info[0] = (p.log ? 1 : (p.bits ? 2 : 0)) + (p.fw ? 10 : 0);
+    info[0] = (p.log ? 1 : (p.bits ? 2 : (p.bl ? 3 : 0))) + (p.fw ? 10 : 0);
     info[1] = p.spl;
     info[2] = p.gwin;
     info[3] = p.gwpb;
     info[4] = p.fw ? rq_fw_blocks_per_cu(p.nK, p.gcol16, p.gwin, p.bits, p.gwpb, p.g_total,
                                           b->ctrl_kind == RQ_SRC_OPTPW)
-                   : rq_sweep_blocks_per_cu(p.spl, p.nK, p.gcol16, p.gwin, p.log, p.bits, p.gwpb, p.g_total);
+                   : rq_sweep_blocks_per_cu(p.spl, p.nK, p.gcol16, p.gwin, p.log, p.bl ? 2 : p.bits, p.gwpb,
+                                            p.g_total);
     info[5] = p.gcol_lds;
     info[6] = (int64_t)p.g_total;
     info[7] = p.chunk;
@@ -838,6 +854,9 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             sa.masks = g->d_mask.p;
             sa.nw = g->nw;
             sa.mstride = p.mstride;
+            sa.fbits = g->d_fbits.p;
+            sa.nwl = (g->n_sinks + 31) / 32;
+            sa.lds_fbits = p.g_fb;
             if (const char* d = getenv("RQ_SWEEP_DBG")) sa.dbg = atoi(d);   // profiling only
             sa.tile_target = 58.0;   // measured on C3: 40 -> 895k, 48 -> 943k, 58 -> 964k, 62 -> 956k replicas/s
             if (const char* e = getenv("RQ_FW_TILE")) sa.tile_target = atof(e);   // tuning only
@@ -855,7 +874,7 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             sa.gen = ga;
             TimedLaunch tl(K_SWEEP, s);
             const hipError_t e = p.fw ? rq_launch_sweep_fw(sa, p.nK, p.gcol16, p.gwin, p.bits, s)
-                                      : rq_launch_sweep(sa, p.spl, p.nK, p.gcol16, p.log, p.bits, s);
+                                      : rq_launch_sweep(sa, p.spl, p.nK, p.gcol16, p.log, p.bl ? 2 : p.bits, s);
             if (e != hipSuccess) return RQ_EHIP;
         }
 

@@ -69,6 +69,9 @@ struct SweepArgs {
     int n_csr;
     const uint32_t* masks;   // [n_str][nw] sink bitsets (BITS variant)
     int nw, mstride;         // words per bitset; LDS row stride in words (odd: bank spread)
+    const uint32_t* fbits;   // follower set as a sink bitset [nwl] (BL variant)
+    int nwl;                 // BL: words per per-wave T / V bitset = ceil(n_sinks / 32)
+    size_t lds_fbits;        // BL: the follower bitset's place in the block's shared LDS
     int dbg;                 // profiling: 1 skip phase C, 2 skip sink updates, 3 skip phase B
     unsigned long long* clk; // RQ_PHASE_CLOCK builds only: per-phase s_memtime sums [8]
     double tile_target;      // fused sweep: arrivals a tile aims at (the cut adapts to it)

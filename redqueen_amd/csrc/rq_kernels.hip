@@ -104,7 +104,7 @@ __global__ __launch_bounds__(256) void rq_gen_streams(GenArgs a)
 //       (equal-time rows merged) are placed and stored by all lanes at once.
 //    LOG = the event log / max_events variant: phase C goes event by event.
 // ============================================================================
-template <int SPL, int NK, class COL, int W, bool LOG, bool BITS>
+template <int SPL, int NK, class COL, int W, bool LOG, bool BITS, bool BL>
 __global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
 {
     extern __shared__ double lds_g[];
@@ -133,6 +133,10 @@ __global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
         odf[j] = a.outdeg_f[j];
         cbf[j] = a.ctrl_src_id < a.src_id[j];
     }
+    // BL: the follower set as a sink bitset, shared by the block's waves
+    uint32_t* fbl = reinterpret_cast<uint32_t*>(base + a.lds_fbits);
+    if (BL)
+        for (int k = threadIdx.x; k < a.nwl; k += blockDim.x) fbl[k] = a.fbits[k];
     const int64_t rl = (int64_t)blockIdx.x * a.wpb + w;
     const bool live = rl < a.n_chunk;
     const int64_t o = a.chunk0 + (live ? rl : 0);
@@ -140,13 +144,18 @@ __global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
     const int g = (int)(i / a.n_rep);
     char* wb = base + a.lds_wave + (size_t)w * a.lds_wave_stride;
     double* invc = reinterpret_cast<double*>(wb);
+    AggL agl;
+    if (BL) {
+        uint32_t* tb = reinterpret_cast<uint32_t*>(wb + a.lds_rank_off);
+        agl.init(tb, tb + a.nwl, fbl, a.nwl, lane);
+    }
     // ranks: exact int for the LOG variant (pivot cells average them); the fast
     // sweep only compares them with K-1, so int16 saturating at 32767 is exact
     using RT = typename std::conditional<LOG, int, int16_t>::type;
     RT* rank = reinterpret_cast<RT*>(wb + a.lds_rank_off);
     double* win = reinterpret_cast<double*>(wb + a.lds_win_off);
     for (int j = lane; j < a.n_str; j += 64) invc[j] = a.inv_c[(int64_t)g * a.n_str + j];
-    if (!BITS)
+    if (!BITS && !BL)
         for (int c = lane; c < a.n_sinks; c += 64) rank[c] = -1;   // NaN: no row yet
     __syncthreads();
     if (!live) return;
@@ -404,9 +413,25 @@ __global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
                 osum = (int64_t)(((uint64_t)(uint32_t)osh << 32) | (uint32_t)osl);
                 wcnt[0] = wc0;
                 ocnt[0] = oc0;
-            } else for (int q = 0; q < n; ++q) {
+            } else {
+              // event q + 1's first 128 sink columns are loaded while event q runs
+              int pa = 0, pb = 0;
+              if (n > 0) {
+                  const int f0 = bcast_i(e0, 0), f1 = bcast_i(e1, 0);
+                  pa = f0 + lane < f1 ? colat(f0 + lane) : 0;
+                  pb = f0 + 64 + lane < f1 ? colat(f0 + 64 + lane) : 0;
+              }
+              for (int q = 0; q < n; ++q) {
+                const int ca = pa, cb = pb;
+                const int qe0 = bcast_i(e0, q), qe1 = bcast_i(e1, q);
+                if (q + 1 < n) {
+                    const int f0 = bcast_i(e0, q + 1), f1 = bcast_i(e1, q + 1);
+                    pa = f0 + lane < f1 ? colat(f0 + lane) : 0;
+                    pb = f0 + 64 + lane < f1 ? colat(f0 + 64 + lane) : 0;
+                }
                 if ((ownm >> q) & 1ull) {
-                    ag.own(rank, folat, a.n_fol, lane);
+                    if (BL) agl.own(ag, lane);
+                    else ag.own(rank, folat, a.n_fol, lane);
                     if (lane == q) {
                         osum = ag.sumR;
                         oval = ag.nvalid;
@@ -415,16 +440,20 @@ __global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
                     }
                 }
                 const int jw = bcast_i(tj, q);
-                if (!opt && jw == a.ctrl_idx)
-                    ag.own(rank, folat, a.n_fol, lane);
-                else if (a.dbg != 2)
-                    ag.wall(rank, colat, bcast_i(e0, q), bcast_i(e1, q), bcast_i(od, q), lane);
+                if (!opt && jw == a.ctrl_idx) {
+                    if (BL) agl.own(ag, lane);
+                    else ag.own(rank, folat, a.n_fol, lane);
+                } else if (a.dbg != 2) {
+                    if (BL) agl.wall_pf(ag, colat, ca, cb, qe0, qe1, bcast_i(od, q), lane);
+                    else ag.wall_pf(rank, colat, ca, cb, qe0, qe1, bcast_i(od, q), lane);
+                }
                 if (lane == q) {
                     wsum = ag.sumR;
                     wval = ag.nvalid;
 #pragma unroll
                     for (int kq = 0; kq < NK; ++kq) wcnt[kq] = ag.cnt[kq];
                 }
+              }
             }
             const uint64_t mo = __ballot(has_o), ma = mo | __ballot(has_w);
             n_events += n + __popcll(ownm);
@@ -447,6 +476,8 @@ __global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
                 ag.sumR = agb.sumR;
                 ag.nvalid = agb.nvalid;
                 ag.cnt[0] = agb.cnt[0];
+            } else if (BL) {
+                agl.own(ag, lane);
             } else {
                 ag.own(rank, folat, a.n_fol, lane);
             }
@@ -1175,11 +1206,11 @@ __global__ __launch_bounds__(64) void rq_replay(ReplayArgs a)
 // ============================================================================
 // launch wrappers
 // ============================================================================
-template <int SPL, int NK, class COL, int W, bool LOG, bool BITS = false>
+template <int SPL, int NK, class COL, int W, bool LOG, bool BITS = false, bool BL = false>
 static hipError_t launch_sweep_t(const SweepArgs& a, hipStream_t s)
 {
     const unsigned blocks = (unsigned)((a.n_chunk + a.wpb - 1) / a.wpb);
-    hipLaunchKernelGGL((rq_sweep<SPL, NK, COL, W, LOG, BITS>), dim3(blocks), dim3(64 * a.wpb), a.lds_total, s, a);
+    hipLaunchKernelGGL((rq_sweep<SPL, NK, COL, W, LOG, BITS, BL>), dim3(blocks), dim3(64 * a.wpb), a.lds_total, s, a);
     return hipGetLastError();
 }
 
@@ -1197,6 +1228,12 @@ static hipError_t launch_sweep_k(const SweepArgs& a, int nK, hipStream_t s)
 template <int SPL>
 static hipError_t launch_sweep_c(const SweepArgs& a, int nK, int col16, int bits, hipStream_t s)
 {
+    if constexpr (SPL >= 2)
+        if (bits == 2)   // K = 1 on per-wave LDS sink bits (> 64 sources): W in {8, 4}
+            return a.win == 8 ? (col16 ? launch_sweep_t<SPL, 1, uint16_t, 8, false, false, true>(a, s)
+                                       : launch_sweep_t<SPL, 1, int, 8, false, false, true>(a, s))
+                              : (col16 ? launch_sweep_t<SPL, 1, uint16_t, 4, false, false, true>(a, s)
+                                       : launch_sweep_t<SPL, 1, int, 4, false, false, true>(a, s));
     if (bits)   // K = 1 on sink bitsets
         return a.win == 16 ? launch_sweep_t<SPL, 1, uint16_t, 16, false, true>(a, s)
                            : launch_sweep_t<SPL, 1, uint16_t, 8, false, true>(a, s);
@@ -1236,11 +1273,11 @@ hipError_t rq_launch_sweep(const SweepArgs& a, int spl, int nK, int col16, int l
 
 // blocks of 64*wpb threads per CU the chosen sweep instance reaches with `lds`
 // bytes of dynamic LDS (VGPR, SGPR and LDS limits all applied by the runtime)
-template <int SPL, int NK, class COL, int W, bool LOG, bool BITS = false>
+template <int SPL, int NK, class COL, int W, bool LOG, bool BITS = false, bool BL = false>
 static int occ_t(int wpb, size_t lds)
 {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rq_sweep<SPL, NK, COL, W, LOG, BITS>, 64 * wpb,
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rq_sweep<SPL, NK, COL, W, LOG, BITS, BL>, 64 * wpb,
                                                       lds) != hipSuccess)
         return 0;
     return nb;
@@ -1258,6 +1295,12 @@ static int occ_k(int nK, int wpb, size_t lds)
 template <int SPL>
 static int occ_c(int nK, int col16, int W, int bits, int wpb, size_t lds)
 {
+    if constexpr (SPL >= 2)
+        if (bits == 2)
+            return W == 8 ? (col16 ? occ_t<SPL, 1, uint16_t, 8, false, false, true>(wpb, lds)
+                                   : occ_t<SPL, 1, int, 8, false, false, true>(wpb, lds))
+                          : (col16 ? occ_t<SPL, 1, uint16_t, 4, false, false, true>(wpb, lds)
+                                   : occ_t<SPL, 1, int, 4, false, false, true>(wpb, lds));
     if (bits)
         return W == 16 ? occ_t<SPL, 1, uint16_t, 16, false, true>(wpb, lds)
                        : occ_t<SPL, 1, uint16_t, 8, false, true>(wpb, lds);

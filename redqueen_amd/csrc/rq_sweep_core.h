@@ -36,6 +36,17 @@ struct Agg {
     template <class RT, class CF>
     __device__ __forceinline__ void wall(RT* rank, CF&& colat, int e0, int e1, int odf, int lane)
     {
+        const int pa = e0 + lane < e1 ? colat(e0 + lane) : 0;
+        const int pb = e0 + 64 + lane < e1 ? colat(e0 + 64 + lane) : 0;
+        wall_pf(rank, colat, pa, pb, e0, e1, odf, lane);
+    }
+    // the same with the first 128 sinks' columns already loaded (pa / pb = sink of
+    // edge e0 + lane / e0 + 64 + lane): the caller issues the next event's column
+    // loads before this event's LDS work, so global column reads overlap it
+    template <class RT, class CF>
+    __device__ __forceinline__ void wall_pf(RT* rank, CF&& colat, int pa, int pb, int e0, int e1, int odf,
+                                            int lane)
+    {
         int dvalid = 0;
         int dle[NK];
 #pragma unroll
@@ -43,8 +54,8 @@ struct Agg {
         for (int e = e0; e < e1; e += 128) {
             const int ea = e + lane, eb = e + 64 + lane;
             const bool acta = ea < e1, actb = eb < e1;
-            const int ca = acta ? colat(ea) : 0;
-            const int cb = actb ? colat(eb) : 0;
+            const int ca = e == e0 ? pa : (acta ? colat(ea) : 0);
+            const int cb = e == e0 ? pb : (actb ? colat(eb) : 0);
             const int ra = acta ? (int)rank[ca] : 0;
             const int rb = actb ? (int)rank[cb] : 0;
             constexpr int kSat = sizeof(RT) == 2 ? 32767 : 0x7FFFFFFF;   // saturating (K <= 32767)
@@ -72,18 +83,25 @@ struct Agg {
         int dle[NK];
 #pragma unroll
         for (int q = 0; q < NK; ++q) dle[q] = 0;
-        for (int f0 = 0; f0 < F; f0 += 64) {
-            const int f = f0 + lane;
-            const bool act = f < F;
-            int r = 0, c = 0;
-            if (act) {
-                c = folat(f);
-                r = (int)rank[c];
-            }
-            dvalid += popc(__ballot(act && r < 0));
+        // 4 x 64 followers per round: their (distinct) sink ids are loaded together
+        for (int f0 = 0; f0 < F; f0 += 256) {
+            int c[4], r[4];
+            bool act[4];
 #pragma unroll
-            for (int q = 0; q < NK; ++q) dle[q] -= popc(__ballot(act && r >= 0 && r <= km1[q]));
-            if (act) rank[c] = (RT)0;
+            for (int u = 0; u < 4; ++u) {
+                const int f = f0 + 64 * u + lane;
+                act[u] = f < F;
+                c[u] = act[u] ? folat(f) : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) r[u] = act[u] ? (int)rank[c[u]] : 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                dvalid += popc(__ballot(act[u] && r[u] < 0));
+#pragma unroll
+                for (int q = 0; q < NK; ++q) dle[q] -= popc(__ballot(act[u] && r[u] >= 0 && r[u] <= km1[q]));
+                if (act[u]) rank[c[u]] = (RT)0;
+            }
         }
 #pragma unroll
         for (int q = 0; q < NK; ++q) cnt[q] += dle[q] + (0 <= km1[q] ? F : 0);
@@ -150,6 +168,76 @@ struct AggB {
         const uint32_t tot = wave_sum_u32((uint32_t)__popc(T) | ((uint32_t)__popc(V) << 16));
         cnt[0] = (int)(tot & 0xFFFFu);
         nvalid = (int)(tot >> 16);
+    }
+};
+
+// K = 1 aggregates for any number of sinks (the general sweep's BL instances):
+// per-wave LDS bitsets T (valid sinks at rank 0) and V (sinks with a row), one bit
+// per sink instead of an int16 rank -- 1/8 of the LDS, so more waves per CU.
+//   wall event : its sinks (distinct; lanes may share a word) clear T and set V with
+//                ds_and/or_rtn, the returned old bits give the count changes;
+//   post       : T |= F, V |= F word-parallel with the follower set F (shared LDS).
+// Updates the Agg<NK> it is given (NK = 1: cnt[0] = #sinks at rank 0).
+struct AggL {
+    uint32_t* T;
+    uint32_t* V;
+    const uint32_t* F;
+    int nw;
+    __device__ __forceinline__ void init(uint32_t* T_, uint32_t* V_, const uint32_t* F_, int nw_, int lane)
+    {
+        T = T_;
+        V = V_;
+        F = F_;
+        nw = nw_;
+        for (int k = lane; k < nw; k += 64) {
+            T[k] = 0u;
+            V[k] = 0u;
+        }
+    }
+    template <int NK, class CF>
+    __device__ __forceinline__ void wall_pf(Agg<NK>& g, CF&& colat, int pa, int pb, int e0, int e1, int odf,
+                                            int lane)
+    {
+        int dvalid = 0, dtop = 0;
+        for (int e = e0; e < e1; e += 128) {
+            const int ea = e + lane, eb = e + 64 + lane;
+            const bool acta = ea < e1, actb = eb < e1;
+            const int ca = e == e0 ? pa : (acta ? colat(ea) : 0);
+            const int cb = e == e0 ? pb : (actb ? colat(eb) : 0);
+            uint32_t ta = 0u, va = 1u, tb = 0u, vb = 1u;
+            if (acta) {
+                const uint32_t bit = 1u << (ca & 31);
+                ta = atomicAnd(&T[ca >> 5], ~bit) & bit;
+                va = atomicOr(&V[ca >> 5], bit) & bit;
+            }
+            if (actb) {
+                const uint32_t bit = 1u << (cb & 31);
+                tb = atomicAnd(&T[cb >> 5], ~bit) & bit;
+                vb = atomicOr(&V[cb >> 5], bit) & bit;
+            }
+            dvalid += popc(__ballot(va == 0u)) + popc(__ballot(vb == 0u));
+            dtop += popc(__ballot(ta != 0u)) + popc(__ballot(tb != 0u));
+        }
+        g.nvalid += dvalid;
+        g.cnt[0] -= dtop;
+        g.sumR += e1 - e0;
+        g.sumF += odf;
+    }
+    template <int NK>
+    __device__ __forceinline__ void own(Agg<NK>& g, int lane)
+    {
+        uint32_t dc = 0u, dv = 0u;
+        for (int k = lane; k < nw; k += 64) {
+            const uint32_t f = F[k], t = T[k], v = V[k];
+            dc += (uint32_t)__popc(f & ~t);
+            dv += (uint32_t)__popc(f & ~v);
+            T[k] = t | f;
+            V[k] = v | f;
+        }
+        g.cnt[0] += (int)wave_sum_u32(dc);
+        g.nvalid += (int)wave_sum_u32(dv);
+        g.sumR -= g.sumF;
+        g.sumF = 0;
     }
 };
 

@@ -15,19 +15,46 @@ from tests.test_gpu_engine import _cmp_replica, _ctx, _graph, _world_with_seeds
 pytestmark = pytest.mark.gpu
 
 
-def test_c5_short_horizon_bit_exact():
+@pytest.mark.parametrize("Ks", [(1, 5), (1,)])
+def test_c5_short_horizon_bit_exact(Ks):
+    """Ks=(1,) runs the K=1 per-wave LDS sink-bit sweep (plan variant 3), (1, 5) the
+    per-sink int16 ranks."""
     torch, engine, graphs, O = _ctx()
     so = dict(graphs.c5(), end_time=100.0)
     g = _graph(engine, so)
     R = 8
-    res = g.run("opt", q=so["q"], s=so["s"], n_rep=R, ctrl_seed=40, world_seed=40, randomize=True,
-                Ks=(1, 5))
+    kw = dict(q=so["q"], s=so["s"], n_rep=R, ctrl_seed=40, world_seed=40, randomize=True, Ks=Ks)
+    assert g.run("opt", plan_only=True, **kw)["variant"] == (3 if Ks == (1,) else 0)
+    res = g.run("opt", **kw)
     assert int(res.status.max().item()) == 0
     for r in (0, 5):
         u = 40 + r
         sc = O.Scenario(_world_with_seeds(so, u), ("opt", u))
-        met, (t, dt, s) = O.engine_metrics(sc, (1, 5))
-        _cmp_replica(res, r, met, t, s, (1, 5))
+        met, (t, dt, s) = O.engine_metrics(sc, Ks)
+        _cmp_replica(res, r, met, t, s, Ks)
+
+
+def test_sink_bits_sweep_many_posts():
+    """The K=1 sink-bit sweep (> 64 sources, > 2048 sinks) on a post-heavy graph
+    (q = 1e3: the post path ORs the follower set into the bits every few events):
+    equal to the per-sink-rank sweep (sweep_mode 3) on every replica and bit-exact
+    against the engine oracle."""
+    torch, engine, graphs, O = _ctx()
+    so = graphs.followers_graph(num_followers=3000, num_sources=96, degree=3, end_time=20.0)
+    so["q"] = 1e3
+    g = _graph(engine, so)
+    kw = dict(q=so["q"], s=so["s"], n_rep=24, ctrl_seed=3, world_seed=3, randomize=True, Ks=(1,))
+    assert g.run("opt", plan_only=True, **kw)["variant"] == 3
+    res = g.run("opt", **kw)
+    ref = g.run("opt", sweep_mode=3, **kw)
+    assert int(res.status.max().item()) == 0
+    assert torch.equal(res.metrics, ref.metrics) and torch.equal(res.counts, ref.counts)
+    assert float(res.counts[:, 0].double().mean().item()) > 50   # posts: the OR path ran
+    for r in (0, 11):
+        u = 3 + r
+        sc = O.Scenario(_world_with_seeds(so, u), ("opt", u))
+        met, (t, dt, s) = O.engine_metrics(sc, (1,))
+        _cmp_replica(res, r, met, t, s, (1,))
 
 
 def test_c5_full_horizon_properties():
