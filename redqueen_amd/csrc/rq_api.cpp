@@ -286,9 +286,12 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
             const size_t o_cbf = sh;  sh = align_up(sh + 4 * g->n_str, 16);
             const size_t o_fb = sh;   if (p->bl) sh = align_up(sh + 4 * (size_t)nwl, 16);
             const int spl = p->spl;
-            for (int W : {16, 8, 4}) {
+            int only_w = 0;
+            if (const char* e = getenv("RQ_G_W")) only_w = atoi(e);   // tuning only
+            for (int W : {16, 8, 4, 2}) {
                 if (p->log && W != 8) continue;
-                if (p->bl ? W == 16 : W == 4) continue;   // BL instances: W in {8, 4}
+                if (p->bl ? W == 16 : W <= 4) continue;   // BL instances: W in {8, 4, 2}
+                if (only_w && W != only_w) continue;
                 const size_t r_off = align_up(8 * (size_t)g->n_str, 16);
                 const size_t rank_b = p->log ? 4 : (p->bits ? 0 : 2);   // fast: int16 saturating
                 // BL: two bits per sink (T, V words) in place of the int16 ranks

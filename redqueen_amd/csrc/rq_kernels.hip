@@ -1229,11 +1229,15 @@ template <int SPL>
 static hipError_t launch_sweep_c(const SweepArgs& a, int nK, int col16, int bits, hipStream_t s)
 {
     if constexpr (SPL >= 2)
-        if (bits == 2)   // K = 1 on per-wave LDS sink bits (> 64 sources): W in {8, 4}
+        if (bits == 2) {   // K = 1 on per-wave LDS sink bits (> 64 sources): W in {8, 4, 2}
+            if (a.win == 2)
+                return col16 ? launch_sweep_t<SPL, 1, uint16_t, 2, false, false, true>(a, s)
+                             : launch_sweep_t<SPL, 1, int, 2, false, false, true>(a, s);
             return a.win == 8 ? (col16 ? launch_sweep_t<SPL, 1, uint16_t, 8, false, false, true>(a, s)
                                        : launch_sweep_t<SPL, 1, int, 8, false, false, true>(a, s))
                               : (col16 ? launch_sweep_t<SPL, 1, uint16_t, 4, false, false, true>(a, s)
                                        : launch_sweep_t<SPL, 1, int, 4, false, false, true>(a, s));
+        }
     if (bits)   // K = 1 on sink bitsets
         return a.win == 16 ? launch_sweep_t<SPL, 1, uint16_t, 16, false, true>(a, s)
                            : launch_sweep_t<SPL, 1, uint16_t, 8, false, true>(a, s);
@@ -1296,11 +1300,15 @@ template <int SPL>
 static int occ_c(int nK, int col16, int W, int bits, int wpb, size_t lds)
 {
     if constexpr (SPL >= 2)
-        if (bits == 2)
+        if (bits == 2) {
+            if (W == 2)
+                return col16 ? occ_t<SPL, 1, uint16_t, 2, false, false, true>(wpb, lds)
+                             : occ_t<SPL, 1, int, 2, false, false, true>(wpb, lds);
             return W == 8 ? (col16 ? occ_t<SPL, 1, uint16_t, 8, false, false, true>(wpb, lds)
                                    : occ_t<SPL, 1, int, 8, false, false, true>(wpb, lds))
                           : (col16 ? occ_t<SPL, 1, uint16_t, 4, false, false, true>(wpb, lds)
                                    : occ_t<SPL, 1, int, 4, false, false, true>(wpb, lds));
+        }
     if (bits)
         return W == 16 ? occ_t<SPL, 1, uint16_t, 16, false, true>(wpb, lds)
                        : occ_t<SPL, 1, uint16_t, 8, false, true>(wpb, lds);
