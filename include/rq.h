@@ -114,8 +114,8 @@ typedef struct rq_graph* rq_graph_t;
 #define RQ_ST_ROWS_OVERFLOW 1    /* metric-row / event-log capacity exceeded: rerun with larger cap_scale */
 #define RQ_ST_STREAM_OVERFLOW 2  /* a source's arrival stream exceeded its capacity: rerun      */
 #define RQ_ST_TIE 4              /* events at equal times shared a pivot row.  Exact (pivot cells
-                                    averaged like pandas) in the sequential sweep -- event log,
-                                    max_events, sweep_mode 2, or any RealData stream; the fast
+                                    averaged like pandas) in the sequential sweep -- max_events,
+                                    sweep_mode 2, or any RealData stream; the fast
                                     tiled sweep keeps the last row, so for a replica flagged
                                     here avg-rank / r^2 may differ: rerun it with sweep_mode 2 */
 #define RQ_ST_EMPTY 8            /* no event reached any sink: the reference's df is empty      */
@@ -148,8 +148,8 @@ typedef struct rq_batch_desc {
     int64_t n_local;             /* a shard of the grid (0 = all n_grid*n_rep); outputs are      */
                                  /* indexed locally, seeds and grid point use the global id     */
     int32_t sweep_mode;          /* 0 auto: fast tiled sweep unless the run needs the sequential
-                                    one (event log, max_events, RealData); 1 fast whenever the
-                                    event log / max_events allow; 2 force the sequential sweep;
+                                    one (max_events, RealData); the fast sweeps write the event
+                                    log themselves; 1 fast whenever max_events allows; 2 force the sequential sweep;
                                     3 as 0 but never a K=1 sink-bit variant (per-sink ranks);
                                     4 / 5 as 0 / 1 on the legacy kernels (arrival streams
                                     pre-generated into HBM by rq_gen_streams, serial wave-min

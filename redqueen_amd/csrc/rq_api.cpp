@@ -254,9 +254,8 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     // RealData streams (recorded times repeat); the fast sweep flags RQ_ST_TIE
     bool has_rd = b->ctrl_kind == RQ_SRC_REALDATA;
     for (int k : g->kind) has_rd = has_rd || k == RQ_SRC_REALDATA;
-    // the fused sweep writes the event log itself; the other fast sweeps do not
-    const bool fw_log_ok = g->n_str <= 64 && b->sweep_mode != 4 && b->sweep_mode != 5;
-    p->log = ((b->flags & RQ_RUN_EVENT_LOG) && !fw_log_ok) || b->max_events >= 0 ||
+    // the fast sweeps (fused and general) write the event log themselves
+    p->log = b->max_events >= 0 ||
              b->sweep_mode == 2 || (has_rd && b->sweep_mode != 1 && b->sweep_mode != 5);
     for (int q = 0; q < b->nK; ++q) p->log = p->log || b->Ks[q] > 32767;   // int16 ranks
     if (p->log) p->spl = g->n_str <= 64 ? 1 : 8;

@@ -354,6 +354,23 @@ __global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
             n_events += n;
         } else {
             const bool own_b = act && ((ownm >> lane) & 1ull);     // controller post before #lane
+            if (a.ev_t) {
+                // event log (t, stream): lane q's post (if any) then its arrival, in tile order
+                const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+                const int64_t pp = n_events + lane + __popcll(ownm & below);
+                const int64_t pw = pp + (own_b ? 1 : 0);
+                double* Et = a.ev_t + o * a.ev_cap;
+                int32_t* Es = a.ev_src + o * a.ev_cap;
+                if (own_b && pp < a.ev_cap) {
+                    Et[pp] = ot;
+                    Es[pp] = a.ctrl_idx;
+                }
+                if (act && pw < a.ev_cap) {
+                    Et[pw] = tt;
+                    Es[pw] = tj;
+                }
+                if (n_events + n + __popcll(ownm) > a.ev_cap) status |= RQ_ST_ROWS_OVERFLOW;
+            }
             const bool strm_own = act && !opt && tj == a.ctrl_idx;  // controlled stream's arrival
             const bool has_o = own_b && a.n_fol > 0;
             const bool has_w = act && e1 > e0;
@@ -469,6 +486,14 @@ __global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
         if (LOG) {
             event(opt_next, true, 0, 0, 0);
         } else {
+            if (a.ev_t && lane == 0) {
+                if (n_events < a.ev_cap) {
+                    a.ev_t[o * a.ev_cap + n_events] = opt_next;
+                    a.ev_src[o * a.ev_cap + n_events] = a.ctrl_idx;
+                } else {
+                    status |= RQ_ST_ROWS_OVERFLOW;
+                }
+            }
             ++n_events;
             if (BITS) {
                 agb.own();

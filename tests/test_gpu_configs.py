@@ -25,7 +25,9 @@ def test_c5_short_horizon_bit_exact(Ks):
     R = 8
     kw = dict(q=so["q"], s=so["s"], n_rep=R, ctrl_seed=40, world_seed=40, randomize=True, Ks=Ks)
     assert g.run("opt", plan_only=True, **kw)["variant"] == (3 if Ks == (1,) else 0)
-    res = g.run("opt", **kw)
+    # the fast sweep writes the event log itself: events compared too
+    res = g.run("opt", event_log=True, **kw)
+    assert g.run("opt", event_log=True, plan_only=True, **kw)["variant"] != 1
     assert int(res.status.max().item()) == 0
     for r in (0, 5):
         u = 40 + r
@@ -45,7 +47,7 @@ def test_sink_bits_sweep_many_posts():
     g = _graph(engine, so)
     kw = dict(q=so["q"], s=so["s"], n_rep=24, ctrl_seed=3, world_seed=3, randomize=True, Ks=(1,))
     assert g.run("opt", plan_only=True, **kw)["variant"] == 3
-    res = g.run("opt", **kw)
+    res = g.run("opt", event_log=True, **kw)
     ref = g.run("opt", sweep_mode=3, **kw)
     assert int(res.status.max().item()) == 0
     assert torch.equal(res.metrics, ref.metrics) and torch.equal(res.counts, ref.counts)

@@ -42,7 +42,7 @@ def _oracle(O, so, ctrl, Ks, max_events=None):
     return met, t, s
 
 
-MODES = ["fast", "scatter", "log", "legacy", "fastlog"]
+MODES = ["fast", "scatter", "log", "legacy", "fastlog", "legacylog"]
 
 
 def _mode_kw(mode):
@@ -50,11 +50,14 @@ def _mode_kw(mode):
     with per-sink LDS ranks (sweep_mode=3); log: the sequential event-log variant
     (sweep_mode=2), events compared too; legacy: pre-generated streams + serial
     wave-min merge (sweep_mode=4); fastlog: the fused sweep writing the event log
-    itself (event_log=True, auto mode), events compared too."""
+    itself (event_log=True, auto mode), events compared too; legacylog: the general
+    (pre-generated streams) fast sweep writing the event log (sweep_mode=4)."""
     if mode == "log":
         return dict(event_log=True, sweep_mode=2)
     if mode == "fastlog":
         return dict(event_log=True, sweep_mode=0)
+    if mode == "legacylog":
+        return dict(event_log=True, sweep_mode=4)
     return dict(event_log=False, sweep_mode={"scatter": 3, "legacy": 4}.get(mode, 0))
 
 
