@@ -144,7 +144,7 @@ struct Plan {
     size_t tables_bytes = 0;
     size_t off_pwc = 0, off_pwmax = 0;
     size_t off_invc = 0, off_streams = 0, off_slen = 0, off_rt = 0, off_rs = 0, off_rv = 0,
-           off_rc = 0, off_sall = 0, off_stoff = 0, off_cap = 0,
+           off_rc = 0, off_sall = 0, off_wq = 0, off_stoff = 0, off_cap = 0,
            total = 0;
 };
 
@@ -390,6 +390,7 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     p->off_rv = o;      o = align_up(o + sizeof(uint32_t) * (size_t)C * p->cap_rows, A);
     p->off_rc = o;      o = align_up(o + sizeof(uint32_t) * (size_t)C * p->cap_rows * p->nK, A);
     p->off_sall = o;    o = align_up(o + sizeof(int) * (size_t)C, A);
+    p->off_wq = o;      o = align_up(o + sizeof(int), A);
     p->total = o;
     return RQ_OK;
 }
@@ -874,6 +875,13 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             sa.lds_total = p.g_total;
             sa.lds_stage_off = p.g_stage_off;
             sa.gen = ga;
+            // fused sweep: waves past their first replica take the next one from a queue,
+            // so the launch tail is spread over every CU instead of whole 16-wave blocks
+            static const int wq_off = getenv("RQ_FW_STATIC") ? atoi(getenv("RQ_FW_STATIC")) : 0;   // A/B only
+            if (p.fw && !wq_off) {
+                sa.wq = (int*)(ws + p.off_wq);
+                if (hipMemsetAsync(sa.wq, 0, sizeof(int), s) != hipSuccess) return RQ_EHIP;
+            }
             TimedLaunch tl(K_SWEEP, s);
             const hipError_t e = p.fw ? rq_launch_sweep_fw(sa, p.nK, p.gcol16, p.gwin, p.bits, s)
                                       : rq_launch_sweep(sa, p.spl, p.nK, p.gcol16, p.log, p.bl ? 2 : p.bits, s);

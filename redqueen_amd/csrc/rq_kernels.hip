@@ -590,22 +590,25 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
         odf[j] = a.outdeg_f[j];
         cbf[j] = a.ctrl_src_id < a.src_id[j];
     }
-    const int64_t rl = (int64_t)blockIdx.x * a.wpb + w;
-    const bool live = rl < a.n_chunk;
-    const int64_t o = a.chunk0 + (live ? rl : 0);
-    const int64_t i = a.rep0 + o;
-    const int g = (int)(i / a.n_rep);
+    __syncthreads();   // block-shared tables ready; no block barrier below this line
     char* wb = base + a.lds_wave + (size_t)w * a.lds_wave_stride;
     double* invc = reinterpret_cast<double*>(wb);
     int16_t* rank = reinterpret_cast<int16_t*>(wb + a.lds_rank_off);   // saturating, exact vs K-1
     double* ring = reinterpret_cast<double*>(wb + a.lds_win_off) + lane * (W + 1);   // odd stride
     double* st_t = reinterpret_cast<double*>(wb + a.lds_stage_off);
     int* st_j = reinterpret_cast<int*>(st_t + 64);
+    // first replica: the wave's static slot; with a work queue (a.wq) the wave then takes
+    // replicas nslot, nslot + 1, ... in queue order until the chunk is exhausted (every
+    // wave leaves once the counter passes n_chunk)
+    const int64_t nslot = (int64_t)gridDim.x * a.wpb;
+    for (int64_t rl = (int64_t)blockIdx.x * a.wpb + w; rl < a.n_chunk;) {
+    const int64_t o = a.chunk0 + rl;
+    const int64_t i = a.rep0 + o;
+    const int g = (int)(i / a.n_rep);
     for (int j = lane; j < a.n_str; j += 64) invc[j] = a.inv_c[(int64_t)g * a.n_str + j];
     if (!BITS)
         for (int c = lane; c < a.n_sinks; c += 64) rank[c] = -1;   // NaN: no row yet
-    __syncthreads();
-    if (!live) return;
+    wave_lds_sync();
 
 #ifdef RQ_PHASE_CLOCK
     unsigned long long ck[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -949,6 +952,11 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
         if (rs.nrow == 0) status |= RQ_ST_EMPTY;
         if (status) atomicOr(&a.status[o], status);
     }
+    if (!a.wq) break;
+    int nx = 0;
+    if (lane == 0) nx = atomicAdd(a.wq, 1);
+    rl = nslot + __builtin_amdgcn_readfirstlane(nx);
+    }   // replica loop
 }
 
 // ============================================================================
@@ -1356,9 +1364,35 @@ int rq_sweep_blocks_per_cu(int spl, int nK, int col16, int W, int log, int bits,
 // fused windowed sweep: (W, H) in {(16, 8), (8, 4)}; OptPWSignificance (PW) instances
 // exist for uint16 columns and W = 16 only (make_plan keeps other PW runs off this path)
 template <int NK, class COL, int W, bool BITS, bool PW = false>
+static int occ_fw_t(int wpb, size_t lds);
+static int rq_cu_count()
+{
+    static int n = 0;
+    if (n <= 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+    }
+    return n;
+}
+template <int NK, class COL, int W, bool BITS, bool PW = false>
 static hipError_t launch_fw_t(const SweepArgs& a, hipStream_t s)
 {
-    const unsigned blocks = (unsigned)((a.n_chunk + a.wpb - 1) / a.wpb);
+    unsigned blocks = (unsigned)((a.n_chunk + a.wpb - 1) / a.wpb);
+    if (a.wq) {
+        // persistent grid: every resident wave slot once, the rest from the queue
+        static int nb_c = 0, wpb_c = 0;
+        static size_t lds_c = 0;
+        if (wpb_c != a.wpb || lds_c != a.lds_total) {
+            nb_c = occ_fw_t<NK, COL, W, BITS, PW>(a.wpb, a.lds_total);
+            wpb_c = a.wpb;
+            lds_c = a.lds_total;
+        }
+        const int nb = nb_c;
+        const unsigned cap = (unsigned)(nb > 0 ? nb : 1) * (unsigned)rq_cu_count();
+        if (cap < blocks) blocks = cap;
+    }
     hipLaunchKernelGGL((rq_sweep_fw<NK, COL, W, W / 2, BITS, PW>), dim3(blocks), dim3(64 * a.wpb), a.lds_total, s, a);
     return hipGetLastError();
 }
@@ -1383,7 +1417,7 @@ hipError_t rq_launch_sweep_fw(const SweepArgs& a, int nK, int col16, int W, int 
     if (W == 16) return col16 ? launch_fw_k<uint16_t, 16>(a, nK, s) : launch_fw_k<int, 16>(a, nK, s);
     return col16 ? launch_fw_k<uint16_t, 8>(a, nK, s) : launch_fw_k<int, 8>(a, nK, s);
 }
-template <int NK, class COL, int W, bool BITS, bool PW = false>
+template <int NK, class COL, int W, bool BITS, bool PW>
 static int occ_fw_t(int wpb, size_t lds)
 {
     int nb = 0;
