@@ -274,7 +274,8 @@ __device__ __forceinline__ uint64_t order_key(double t)
 template <int NV>
 __host__ __device__ constexpr int npsum_lds_doubles()
 {
-    // leaf values [NV][128] + leaf (off,len) [128][2 ints = 1 double] + stack [24][NV+1]
+    // leaf values [NV][128] + leaf (off,len) [128][2 ints = 1 double] + value stack [24][NV+1]
+    // (rows 16-23 of the value stack hold the two int recursion stacks [2][16])
     return NV * 128 + 128 + 24 * (NV + 1);
 }
 
@@ -294,9 +295,13 @@ __device__ void wave_npsum(int64_t n, VAL&& val, double* lds, double out[NV])
     for (int64_t c0 = 0; c0 < n; c0 += 8192) {
         const int m = (int)((n - c0) < 8192 ? (n - c0) : 8192);
         // ---- enumerate the leaves of pairwise(m), left to right (uniform) ----
+        // the uniform recursion stacks live in LDS (slack of stk past depth 16), not in
+        // dynamically indexed VGPR arrays: the scan kernel's occupancy is VGPR-bound
+        int* so = reinterpret_cast<int*>(stk + 16 * (NV + 1));
+        int* sn = so + 16;
         int nleaf = 0;
         {
-            int so[16], sn[16], sp = 0;
+            int sp = 0;
             so[0] = 0;
             sn[0] = m;
             sp = 1;
@@ -371,7 +376,8 @@ __device__ void wave_npsum(int64_t n, VAL&& val, double* lds, double out[NV])
         // ---- post-order walk of the tree; leaves consumed left to right ----
         double cv[NV];
         {
-            int sn[16], st[16], sp = 0, li = 0;
+            int* st = so;   // the enumeration's stacks are free again
+            int sp = 0, li = 0;
             sn[0] = m;
             st[0] = 0;
             sp = 1;

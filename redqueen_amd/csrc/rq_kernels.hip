@@ -30,6 +30,7 @@
 #include "rq_sweep_core.h"
 #include "rq_gen.h"
 #include <type_traits>
+#include <cstdlib>
 
 #pragma clang fp contract(off)
 
@@ -962,8 +963,8 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
 // ============================================================================
 // 3. scan: numpy-order integrals over the pivot rows, one wavefront per replica
 // ============================================================================
-template <int NK>
-__global__ __launch_bounds__(256) void rq_scan(ScanArgs a)
+template <int NK, int WPE>
+__global__ __launch_bounds__(256, WPE) void rq_scan(ScanArgs a)
 {
     constexpr int NV = NK + 2;
     extern __shared__ double lds_scan[];
@@ -1452,7 +1453,14 @@ static hipError_t launch_scan_t(const ScanArgs& a, hipStream_t s)
 {
     const unsigned blocks = (unsigned)((a.n_chunk + 3) / 4);
     const size_t lds = 4 * npsum_lds_doubles<NK + 2>() * sizeof(double);
-    hipLaunchKernelGGL((rq_scan<NK>), dim3(blocks), dim3(256), lds, s, a);
+    // waves per SIMD the build targets (VGPR budget): A/B knob RQ_SCAN_WPE
+    static const int wpe = getenv("RQ_SCAN_WPE") ? atoi(getenv("RQ_SCAN_WPE")) : 6;
+    if (wpe >= 8)
+        hipLaunchKernelGGL((rq_scan<NK, 8>), dim3(blocks), dim3(256), lds, s, a);
+    else if (wpe >= 6)
+        hipLaunchKernelGGL((rq_scan<NK, 6>), dim3(blocks), dim3(256), lds, s, a);
+    else
+        hipLaunchKernelGGL((rq_scan<NK, 4>), dim3(blocks), dim3(256), lds, s, a);
     return hipGetLastError();
 }
 
