@@ -878,7 +878,7 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             // fused sweep: waves past their first replica take the next one from a queue,
             // so the launch tail is spread over every CU instead of whole 16-wave blocks
             static const int wq_off = getenv("RQ_FW_STATIC") ? atoi(getenv("RQ_FW_STATIC")) : 0;   // A/B only
-            if (p.fw && !wq_off) {
+            if (!wq_off) {   // both sweep kinds take replicas past the first from the queue
                 sa.wq = (int*)(ws + p.off_wq);
                 if (hipMemsetAsync(sa.wq, 0, sizeof(int), s) != hipSuccess) return RQ_EHIP;
             }

@@ -138,28 +138,30 @@ __global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
     uint32_t* fbl = reinterpret_cast<uint32_t*>(base + a.lds_fbits);
     if (BL)
         for (int k = threadIdx.x; k < a.nwl; k += blockDim.x) fbl[k] = a.fbits[k];
-    const int64_t rl = (int64_t)blockIdx.x * a.wpb + w;
-    const bool live = rl < a.n_chunk;
-    const int64_t o = a.chunk0 + (live ? rl : 0);
-    const int64_t i = a.rep0 + o;
-    const int g = (int)(i / a.n_rep);
+    __syncthreads();   // block-shared tables ready; no block barrier below this line
     char* wb = base + a.lds_wave + (size_t)w * a.lds_wave_stride;
     double* invc = reinterpret_cast<double*>(wb);
-    AggL agl;
-    if (BL) {
-        uint32_t* tb = reinterpret_cast<uint32_t*>(wb + a.lds_rank_off);
-        agl.init(tb, tb + a.nwl, fbl, a.nwl, lane);
-    }
     // ranks: exact int for the LOG variant (pivot cells average them); the fast
     // sweep only compares them with K-1, so int16 saturating at 32767 is exact
     using RT = typename std::conditional<LOG, int, int16_t>::type;
     RT* rank = reinterpret_cast<RT*>(wb + a.lds_rank_off);
     double* win = reinterpret_cast<double*>(wb + a.lds_win_off);
+    // first replica: the wave's static slot; with a work queue (a.wq) the wave then
+    // takes replicas nslot, nslot + 1, ... until the chunk is exhausted
+    const int64_t nslot = (int64_t)gridDim.x * a.wpb;
+    for (int64_t rl = (int64_t)blockIdx.x * a.wpb + w; rl < a.n_chunk;) {
+    const int64_t o = a.chunk0 + rl;
+    const int64_t i = a.rep0 + o;
+    const int g = (int)(i / a.n_rep);
+    AggL agl;
+    if (BL) {
+        uint32_t* tb = reinterpret_cast<uint32_t*>(wb + a.lds_rank_off);
+        agl.init(tb, tb + a.nwl, fbl, a.nwl, lane);
+    }
     for (int j = lane; j < a.n_str; j += 64) invc[j] = a.inv_c[(int64_t)g * a.n_str + j];
     if (!BITS && !BL)
         for (int c = lane; c < a.n_sinks; c += 64) rank[c] = -1;   // NaN: no row yet
-    __syncthreads();
-    if (!live) return;
+    wave_lds_sync();
 
     // ---- arrival rings: lane owns sources [lane*SPL, lane*SPL+SPL) ----
     const double* st = a.streams + rl * a.capsum;
@@ -548,6 +550,11 @@ __global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
         if (rs.nrow == 0) status |= RQ_ST_EMPTY;
         if (status) atomicOr(&a.status[o], status);
     }
+    if (!a.wq) break;
+    int nx = 0;
+    if (lane == 0) nx = atomicAdd(a.wq, 1);
+    rl = nslot + __builtin_amdgcn_readfirstlane(nx);
+    }   // replica loop
 }
 
 // ============================================================================
@@ -1240,10 +1247,35 @@ __global__ __launch_bounds__(64) void rq_replay(ReplayArgs a)
 // ============================================================================
 // launch wrappers
 // ============================================================================
+static int rq_cu_count()
+{
+    static int n = 0;
+    if (n <= 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+    }
+    return n;
+}
+template <int SPL, int NK, class COL, int W, bool LOG, bool BITS = false, bool BL = false>
+static int occ_t(int wpb, size_t lds);
 template <int SPL, int NK, class COL, int W, bool LOG, bool BITS = false, bool BL = false>
 static hipError_t launch_sweep_t(const SweepArgs& a, hipStream_t s)
 {
-    const unsigned blocks = (unsigned)((a.n_chunk + a.wpb - 1) / a.wpb);
+    unsigned blocks = (unsigned)((a.n_chunk + a.wpb - 1) / a.wpb);
+    if (a.wq) {
+        // persistent grid: every resident wave slot once, the rest from the queue
+        static int nb_c = 0, wpb_c = 0;
+        static size_t lds_c = 0;
+        if (wpb_c != a.wpb || lds_c != a.lds_total) {
+            nb_c = occ_t<SPL, NK, COL, W, LOG, BITS, BL>(a.wpb, a.lds_total);
+            wpb_c = a.wpb;
+            lds_c = a.lds_total;
+        }
+        const unsigned cap = (unsigned)(nb_c > 0 ? nb_c : 1) * (unsigned)rq_cu_count();
+        if (cap < blocks) blocks = cap;
+    }
     hipLaunchKernelGGL((rq_sweep<SPL, NK, COL, W, LOG, BITS, BL>), dim3(blocks), dim3(64 * a.wpb), a.lds_total, s, a);
     return hipGetLastError();
 }
@@ -1311,7 +1343,7 @@ hipError_t rq_launch_sweep(const SweepArgs& a, int spl, int nK, int col16, int l
 
 // blocks of 64*wpb threads per CU the chosen sweep instance reaches with `lds`
 // bytes of dynamic LDS (VGPR, SGPR and LDS limits all applied by the runtime)
-template <int SPL, int NK, class COL, int W, bool LOG, bool BITS = false, bool BL = false>
+template <int SPL, int NK, class COL, int W, bool LOG, bool BITS, bool BL>
 static int occ_t(int wpb, size_t lds)
 {
     int nb = 0;
@@ -1366,17 +1398,6 @@ int rq_sweep_blocks_per_cu(int spl, int nK, int col16, int W, int log, int bits,
 // exist for uint16 columns and W = 16 only (make_plan keeps other PW runs off this path)
 template <int NK, class COL, int W, bool BITS, bool PW = false>
 static int occ_fw_t(int wpb, size_t lds);
-static int rq_cu_count()
-{
-    static int n = 0;
-    if (n <= 0) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-            n = 256;
-    }
-    return n;
-}
 template <int NK, class COL, int W, bool BITS, bool PW = false>
 static hipError_t launch_fw_t(const SweepArgs& a, hipStream_t s)
 {
