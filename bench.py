@@ -70,15 +70,16 @@ def pmc_traffic(workload, R, plan):
     try:
         d = json.load(open(PMC_SUMMARY))
     except (OSError, ValueError):
-        return None, None
+        return None, None, None
     meta = d.get("_meta", {})
     if meta.get("workload") != workload or meta.get("replicas") != R or \
             meta.get("variant") != plan["variant"]:
-        return None, None
+        return None, None, None
     for k, v in d.items():
         if k.startswith("rq_sweep") and "hbm_write_bytes" in v and "hbm_read_bytes" in v:
-            return v["hbm_read_bytes"] + v["hbm_write_bytes"], os.path.relpath(PMC_SUMMARY, ROOT)
-    return None, None
+            issue = {q: v[q] for q in ("frac_active_inst", "frac_wait_any", "frac_wait_inst") if q in v}
+            return v["hbm_read_bytes"] + v["hbm_write_bytes"], os.path.relpath(PMC_SUMMARY, ROOT), issue
+    return None, None, None
 
 
 def main():
@@ -202,7 +203,7 @@ def main():
     gen_gbs = GEN_B_PER_WALL_EVENT * (ev_rank - posts_step) / (gen_ms * 1e-3) / 1e9 \
         if gen_ms > 0 else None
 
-    traffic, traffic_src = pmc_traffic(a.workload, R, plan)
+    traffic, traffic_src, issue = pmc_traffic(a.workload, R, plan)
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
@@ -238,6 +239,8 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic,
                          "traffic_source": traffic_src,
+                         # what does bound it: SQ issue / wait shares of the wave cycles (same PMC run)
+                         "issue": issue,
                          "note": "sweep is latency/issue-bound (serial event chain per replica); "
                                  "algorithmic bytes = 24 B/pivot row written%s" %
                                  ("" if fused else " + 8 B/wall event read")},
