@@ -279,3 +279,42 @@ def test_fused_window_equal_time_blocks(Ks):
         assert torch.equal(a.metrics, b.metrics)
         assert torch.equal(a.status, b.status)
         assert int(a.status[0].item()) & 4
+
+
+@pytest.mark.parametrize("mode", ["fast", "legacy"])
+def test_work_queue_replicas(mode):
+    """Replicas past the resident wave slots come from the sweep's work queue (persistent
+    grid, SweepArgs.wq): they must equal the oracle bit for bit and equal a chunked run
+    whose launches all fit the resident slots (static replica per wave)."""
+    torch, engine, graphs, O = _ctx()
+    so = graphs.readme()
+    g = _graph(engine, so)
+    R = 20000
+    kw = _mode_kw(mode)
+    a = g.run("opt", q=so["q"], s=so["s"], n_rep=R, ctrl_seed=3000, world_seed=3000,
+              randomize=True, Ks=(1, 2), **kw)
+    b = g.run("opt", q=so["q"], s=so["s"], n_rep=R, ctrl_seed=3000, world_seed=3000,
+              randomize=True, Ks=(1, 2), chunk=1000, **kw)
+    assert int(a.status.abs().sum().item()) == 0
+    assert torch.equal(a.metrics, b.metrics) and torch.equal(a.counts, b.counts)
+    for r in (0, 4095, 4096, 8191, 8192, 12345, R - 1):
+        u = 3000 + r
+        met_o, t_o, s_o = _oracle(O, _world_with_seeds(so, u), ("opt", u), (1, 2))
+        _cmp_replica(a, r, met_o, t_o, s_o, (1, 2))
+
+
+def test_work_queue_c3():
+    """The bench network (C3) at 1.5 launches' worth of wave slots: queue == chunked."""
+    torch, engine, graphs, O = _ctx()
+    so = graphs.c3()
+    g = _graph(engine, so)
+    R = 6000
+    a = g.run("opt", q=so["q"], s=so["s"], n_rep=R, ctrl_seed=77, world_seed=77, randomize=True, Ks=(1,))
+    b = g.run("opt", q=so["q"], s=so["s"], n_rep=R, ctrl_seed=77, world_seed=77, randomize=True, Ks=(1,),
+              chunk=500)
+    assert int(a.status.abs().sum().item()) == 0
+    assert torch.equal(a.metrics, b.metrics) and torch.equal(a.counts, b.counts)
+    for r in (4500, R - 1):
+        u = 77 + r
+        met_o, t_o, s_o = _oracle(O, _world_with_seeds(so, u), ("opt", u), (1,))
+        _cmp_replica(a, r, met_o, t_o, s_o, (1,))
