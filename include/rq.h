@@ -20,10 +20,10 @@
  *                       opt_runs.worker_opt/worker_poisson  opt_runs.py:51-126
  *                       with opt_runs.add_perf's fields     opt_runs.py:41-48
  *   rq_metrics_replay   utils.time_in_top_k(df, K, ...)     utils.py:84-98
- *                       utils.average_rank(df, ...)         utils.py:101-114
+ *   (_batch: many dfs)  utils.average_rank(df, ...)         utils.py:101-114
  *                       utils.int_r_2(df, ...)              utils.py:117-121
  *                       utils.num_tweets_of(df, ...)        utils.py:170-176
- *                       on a dataframe in the reference's row layout.
+ *                       on dataframes in the reference's row layout (raw sink ids).
  *   rq_oracle_dp        utils.oracle_ranking(df, sim_opts)  utils.py:181-245
  *                       (batched over walls / q values: the loops of
  *                       find_opt_oracle :260-340 and opt_runs.worker_oracle
@@ -55,7 +55,7 @@
 extern "C" {
 #endif
 
-#define RQ_ABI_VERSION 2
+#define RQ_ABI_VERSION 3
 #define RQ_MAX_K 4 /* at most 4 K values (perf_opts.Ks, opt_runs.py:31-38) per run */
 
 typedef enum {
@@ -200,20 +200,41 @@ int rq_plan_info(rq_graph_t g, const rq_batch_desc* b, int64_t* info);
 int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out,
                  void* workspace, size_t workspace_bytes, void* hip_stream);
 
-/* Metrics on a dataframe in the reference's row layout (State.get_dataframe):
- * one row per (event, sink), rows in df order, 't' non-decreasing.
- *   t, src, event_id : device [n_rows]  (event_id may be NULL: counts[0..1] = -1)
- *   sink_col         : device [n_rows]  column of the row's sink_id among the
- *                      sorted unique sink ids of the df (pivot_table columns)
- *   out              : device [nK + 2]  top_K..., avg_rank, r_2
- *   counts           : device [4]       num_tweets_of(src), world events, pivot rows, columns
- * Workspace: rq_replay_workspace_size(). */
-int rq_replay_workspace_size(int64_t n_rows, int32_t n_cols, size_t* bytes);
-int rq_metrics_replay(const double* t, const int64_t* src, const int32_t* sink_col,
-                      const int64_t* event_id, int64_t n_rows, int32_t n_cols,
-                      int64_t src_id, double end_time, const int32_t* Ks, int32_t nK,
-                      double* out, int64_t* counts, void* workspace, size_t workspace_bytes,
-                      void* hip_stream);
+/* Metrics of dataframes in the reference's row layout (State.get_dataframe,
+ * opt_model.py:85-97): one row per (event, sink) in df order, 't' non-decreasing
+ * within a dataframe, sink ids RAW (any int64; the pivot columns -- the sorted
+ * unique sink ids of each dataframe -- are built on the device).  Replaces
+ *   utils.time_in_top_k(df, K, src_id, end_time)      utils.py:84-98
+ *   utils.average_rank(df, src_id, end_time)           utils.py:101-114
+ *   utils.int_r_2(df, sim_opts)                        utils.py:117-121
+ *   utils.num_tweets_of(df, src_id) (+ world events)   utils.py:170-176, opt_runs.py:41-48
+ * with the reference's arithmetic bit for bit (rank_of_src_in_df utils.py:38-56:
+ * per-sink rank scan, pivot mean of duplicate (t, sink) rows, ffill; numpy's
+ * pairwise sums).
+ *   t, src, sink, event_id : device [n_rows] (event_id may be NULL)
+ *   out                    : device [n_df][nK + 2]  top_K..., avg_rank, r_2 (NaN on error)
+ *   counts                 : device [n_df][4]       num_tweets_of(src_id), world events
+ *                            (-1 without event ids or if event_id decreases), pivot rows
+ *                            (0: empty df; RQ_EUNSORTED: 't' decreases; RQ_EOVERFLOW: the df
+ *                            needs the RQ_REPLAY_LARGE workspace), unique sinks
+ * Workspace: rq_replay_workspace_size; the small one serves dataframes with <= 3071
+ * unique sinks (the per-sink state lives in LDS), RQ_REPLAY_LARGE any width.
+ * Per dataframe: < 2^31 rows. */
+#define RQ_REPLAY_LARGE 1
+int rq_replay_workspace_size(int64_t n_rows, int64_t n_df, int32_t nK, int32_t flags, size_t* bytes);
+int rq_metrics_replay(const double* t, const int64_t* src, const int64_t* sink,
+                      const int64_t* event_id, int64_t n_rows, int64_t src_id, double end_time,
+                      const int32_t* Ks, int32_t nK, double* out, int64_t* counts,
+                      void* workspace, size_t workspace_bytes, void* hip_stream);
+/* Many dataframes at once (the replicas of a batch, the reference's loop of
+ * utils calls over opt_runs worker outputs): dataframe d owns rows
+ * [df_off[d], df_off[d + 1]) of the concatenated columns; df_off device [n_df + 1],
+ * n_rows = df_off[n_df]. */
+int rq_metrics_replay_batch(const double* t, const int64_t* src, const int64_t* sink,
+                            const int64_t* event_id, const int64_t* df_off, int64_t n_df,
+                            int64_t n_rows, int64_t src_id, double end_time, const int32_t* Ks,
+                            int32_t nK, double* out, int64_t* counts, void* workspace,
+                            size_t workspace_bytes, void* hip_stream);
 
 /* Offline oracle (utils.oracle_ranking) for n_inst single-follower walls at once.
  * Instance i: n_i wall events, w_i[0..n_i+2) = np.diff([0, 0, event_times..., end_time])

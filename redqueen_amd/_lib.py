@@ -17,7 +17,8 @@ RQ_OK, RQ_EINVAL, RQ_EOVERFLOW, RQ_EHIP, RQ_ENOMEM, RQ_EUNSORTED, RQ_EUNSUPPORTE
 SRC_NONE, SRC_POISSON, SRC_POISSON2, SRC_HAWKES, SRC_PWCONST, SRC_REALDATA, SRC_OPT, SRC_OPTPW = range(8)
 ST_ROWS_OVERFLOW, ST_STREAM_OVERFLOW, ST_TIE, ST_EMPTY = 1, 2, 4, 8
 RUN_EVENT_LOG = 1
-ABI_VERSION = 2
+ABI_VERSION = 3
+REPLAY_LARGE = 1
 MAX_K = 4
 
 _P = C.c_void_p
@@ -87,9 +88,12 @@ def lib():
     L.rq_event_capacity.argtypes = [_P, C.POINTER(BatchDesc), _pi64]
     L.rq_plan_info.argtypes = [_P, C.POINTER(BatchDesc), _pi64]
     L.rq_run_batch.argtypes = [_P, C.POINTER(BatchDesc), C.POINTER(Outputs), _P, C.c_size_t, _P]
-    L.rq_replay_workspace_size.argtypes = [C.c_int64, C.c_int32, C.POINTER(C.c_size_t)]
-    L.rq_metrics_replay.argtypes = [_P, _P, _P, _P, C.c_int64, C.c_int32, C.c_int64, C.c_double,
+    L.rq_replay_workspace_size.argtypes = [C.c_int64, C.c_int64, C.c_int32, C.c_int32,
+                                           C.POINTER(C.c_size_t)]
+    L.rq_metrics_replay.argtypes = [_P, _P, _P, _P, C.c_int64, C.c_int64, C.c_double,
                                     _pi32, C.c_int32, _P, _P, _P, C.c_size_t, _P]
+    L.rq_metrics_replay_batch.argtypes = [_P, _P, _P, _P, _P, C.c_int64, C.c_int64, C.c_int64,
+                                          C.c_double, _pi32, C.c_int32, _P, _P, _P, C.c_size_t, _P]
     L.rq_oracle_workspace_size.argtypes = [C.c_int32, C.c_int64, C.POINTER(C.c_size_t)]
     L.rq_oracle_dp.argtypes = [_P, _P, _P, _P, C.c_int32, C.c_int64, _P, _P, _P, _P, _P,
                                C.c_size_t, _P]
@@ -103,7 +107,8 @@ def lib():
     L.rq_timing_read.argtypes = [_pd, _pi64]
     for fn in ("rq_timing", "rq_timing_read", "rq_graph_build", "rq_graph_free", "rq_graph_info", "rq_graph_source_ids",
                "rq_graph_followers", "rq_workspace_size", "rq_event_capacity", "rq_run_batch",
-               "rq_replay_workspace_size", "rq_metrics_replay", "rq_oracle_workspace_size",
+               "rq_replay_workspace_size", "rq_metrics_replay", "rq_metrics_replay_batch",
+               "rq_oracle_workspace_size",
                "rq_oracle_dp", "rq_rank_table", "rq_u_int", "rq_log_rows", "rq_log_expand"):
         getattr(L, fn).restype = C.c_int
     if L.rq_abi_version() != ABI_VERSION:
@@ -127,5 +132,5 @@ def check(fn, code):
 EXPORTED = ["rq_abi_version", "rq_strerror", "rq_graph_build", "rq_graph_free", "rq_graph_info",
             "rq_graph_source_ids", "rq_graph_followers", "rq_workspace_size",
             "rq_event_capacity", "rq_plan_info", "rq_run_batch", "rq_replay_workspace_size",
-            "rq_metrics_replay", "rq_oracle_workspace_size", "rq_oracle_dp", "rq_rank_table",
+            "rq_metrics_replay", "rq_metrics_replay_batch", "rq_oracle_workspace_size", "rq_oracle_dp", "rq_rank_table",
             "rq_u_int", "rq_log_rows", "rq_log_expand", "rq_timing", "rq_timing_read"]

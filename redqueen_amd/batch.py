@@ -9,6 +9,7 @@ DataFrame with the same fields (seed, q, type, top_K..., avg_rank, r_2,
 num_events, world_events, capacity).
 """
 import collections
+import hashlib
 
 import numpy as np
 import pandas as pd
@@ -19,10 +20,20 @@ from .engine import Graph
 _CACHE = collections.OrderedDict()
 
 
+def _val_key(v):
+    # arrays (RealData times, PiecewiseConst tables) by dtype, shape and a content
+    # hash: numpy's repr elides the middle of arrays longer than 1000 elements
+    if isinstance(v, (np.ndarray, list, tuple)):
+        a = np.ascontiguousarray(np.asarray(v))
+        if a.dtype != object:
+            return (str(a.dtype), a.shape, hashlib.sha1(a.tobytes()).hexdigest())
+    return repr(v)
+
+
 def _key(so):
     return (so.src_id, float(so.end_time), tuple(map(tuple, so.edge_list)),
             tuple(so.sink_ids), repr([(n if isinstance(n, str) else n.__name__,
-                                       sorted((k, repr(v)) for k, v in kw.items()))
+                                       sorted((k, _val_key(v)) for k, v in kw.items()))
                                       for n, kw in so.other_sources]))
 
 

@@ -940,97 +940,104 @@ int rq_timing_read(double* ms, int64_t* launches)
 }
 
 namespace {
-struct ReplayPlan {
-    size_t off_rt, off_rs, off_rv, off_rc, off_state, off_nrows, off_sall, off_err, total;
+// replay workspace: per-df status, pivot rows, fallback sink keys; the large
+// layout adds per-df hash tables / sequential-replay state (slots [4 r0, 4 r1))
+struct RpPlan {
+    size_t off_info, off_dt, off_sum, off_valid, off_cnt, off_keys, off_gkeys, off_gstate, small, large;
 };
-ReplayPlan replay_plan(int64_t n_rows, int32_t n_cols)
+RpPlan rp_plan(int64_t n_rows, int64_t n_df, int32_t nK)
 {
-    ReplayPlan p{};
-    const size_t A = 256;
+    RpPlan p{};
+    const size_t A = 256, n = (size_t)std::max<int64_t>(n_rows, 1);
     size_t o = 0;
-    p.off_rt = o;    o = align_up(o + 8 * (size_t)n_rows, A);
-    p.off_rs = o;    o = align_up(o + 8 * (size_t)n_rows, A);
-    p.off_rv = o;    o = align_up(o + 4 * (size_t)n_rows, A);
-    p.off_rc = o;    o = align_up(o + 4 * (size_t)n_rows * RQ_MAX_K, A);
-    p.off_state = o; o = align_up(o + 40 * (size_t)n_cols, A);
-    p.off_nrows = o; o = align_up(o + 8, A);
-    p.off_sall = o;  o = align_up(o + 4, A);
-    p.off_err = o;   o = align_up(o + 4, A);
-    p.total = o;
+    p.off_info = o;  o = align_up(o + sizeof(RpInfo) * (size_t)std::max<int64_t>(n_df, 1), A);
+    p.off_dt = o;    o = align_up(o + 8 * n, A);
+    p.off_sum = o;   o = align_up(o + 8 * n, A);
+    p.off_valid = o; o = align_up(o + 4 * n, A);
+    p.off_cnt = o;   o = align_up(o + 4 * n * (size_t)nK, A);
+    p.off_keys = o;  o = align_up(o + 8 * n, A);
+    p.small = o;
+    p.off_gkeys = o; o = align_up(o + 8 * 4 * n, A);
+    p.off_gstate = o; o = align_up(o + 16 * 4 * n, A);
+    p.large = o;
     return p;
+}
+
+int rp_run(const double* t, const int64_t* src, const int64_t* sink, const int64_t* event_id,
+           const int64_t* df_off, int64_t n_df, int64_t n_rows, int64_t src_id, double end_time,
+           const int32_t* Ks, int32_t nK, double* out, int64_t* counts, void* workspace,
+           size_t workspace_bytes, void* hip_stream)
+{
+    if (!out || !counts || !workspace || !Ks || n_df < 1 || n_rows < 0) return RQ_EINVAL;
+    if (n_rows > 0 && (!t || !src || !sink)) return RQ_EINVAL;
+    if (nK < 1 || nK > RQ_MAX_K) return RQ_EINVAL;
+    for (int q = 0; q < nK; ++q)
+        if (Ks[q] < 1) return RQ_EINVAL;
+    const RpPlan p = rp_plan(n_rows, n_df, nK);
+    if (workspace_bytes < p.small) return RQ_EINVAL;
+    const bool large = workspace_bytes >= p.large;
+    char* ws = (char*)workspace;
+    RpArgs a{};
+    a.t = t;
+    a.src = src;
+    a.sink = sink;
+    a.eid = event_id;
+    a.df_off = df_off;
+    a.n_df = n_df;
+    a.n_rows = n_rows;
+    a.src_id = src_id;
+    a.end = end_time;
+    a.nK = nK;
+    for (int q = 0; q < RQ_MAX_K; ++q) a.Ks[q] = q < nK ? Ks[q] : 1;
+    a.info = (RpInfo*)(ws + p.off_info);
+    a.rows_dt = (double*)(ws + p.off_dt);
+    a.rows_sum = (double*)(ws + p.off_sum);
+    a.rows_valid = (uint32_t*)(ws + p.off_valid);
+    a.rows_cnt = (uint32_t*)(ws + p.off_cnt);
+    a.keys = (int64_t*)(ws + p.off_keys);
+    a.gkeys = large ? (uint64_t*)(ws + p.off_gkeys) : nullptr;
+    a.gstate = large ? (void*)(ws + p.off_gstate) : nullptr;
+    a.metrics = out;
+    a.counts = counts;
+    hipStream_t s = (hipStream_t)hip_stream;
+    {
+        TimedLaunch tl(K_REPLAY, s);
+        if (rq_launch_rp(a, RP_PHASE_FAST, s) != hipSuccess) return RQ_EHIP;
+        if (large && rq_launch_rp(a, RP_PHASE_GLOBAL, s) != hipSuccess) return RQ_EHIP;
+        if (rq_launch_rp(a, RP_PHASE_KEYS, s) != hipSuccess) return RQ_EHIP;
+        if (rq_launch_rp(a, RP_PHASE_SEQ, s) != hipSuccess) return RQ_EHIP;
+    }
+    TimedLaunch tl(K_SCAN, s);
+    return rq_launch_rp(a, RP_PHASE_SCAN, s) == hipSuccess ? RQ_OK : RQ_EHIP;
 }
 }  // namespace
 
-int rq_replay_workspace_size(int64_t n_rows, int32_t n_cols, size_t* bytes)
+int rq_replay_workspace_size(int64_t n_rows, int64_t n_df, int32_t nK, int32_t flags, size_t* bytes)
 {
-    if (!bytes || n_rows < 1 || n_cols < 1) return RQ_EINVAL;
-    *bytes = replay_plan(n_rows, n_cols).total;
+    if (!bytes || n_rows < 0 || n_df < 1 || nK < 1 || nK > RQ_MAX_K) return RQ_EINVAL;
+    const RpPlan p = rp_plan(n_rows, n_df, nK);
+    *bytes = (flags & RQ_REPLAY_LARGE) ? p.large : p.small;
     return RQ_OK;
 }
 
-int rq_metrics_replay(const double* t, const int64_t* src, const int32_t* sink_col,
-                      const int64_t* event_id, int64_t n_rows, int32_t n_cols, int64_t src_id,
-                      double end_time, const int32_t* Ks, int32_t nK, double* out, int64_t* counts,
-                      void* workspace, size_t workspace_bytes, void* hip_stream)
+int rq_metrics_replay(const double* t, const int64_t* src, const int64_t* sink,
+                      const int64_t* event_id, int64_t n_rows, int64_t src_id, double end_time,
+                      const int32_t* Ks, int32_t nK, double* out, int64_t* counts, void* workspace,
+                      size_t workspace_bytes, void* hip_stream)
 {
-    if (!t || !src || !sink_col || !out || !counts || !workspace || !Ks) return RQ_EINVAL;
-    if (n_rows < 1 || n_cols < 1 || nK < 1 || nK > RQ_MAX_K) return RQ_EINVAL;
-    const ReplayPlan p = replay_plan(n_rows, n_cols);
-    if (workspace_bytes < p.total) return RQ_EINVAL;
-    hipStream_t s = (hipStream_t)hip_stream;
-    char* ws = (char*)workspace;
-    ReplayArgs ra{};
-    ra.t = t;
-    ra.src = src;
-    ra.col = sink_col;
-    ra.eid = event_id;
-    ra.n_rows = n_rows;
-    ra.n_cols = n_cols;
-    ra.src_id = src_id;
-    for (int q = 0; q < RQ_MAX_K; ++q) ra.Ks[q] = q < nK ? Ks[q] : 1;
-    ra.lds_state = (size_t)n_cols * 40 <= 120 * 1024;
-    double* cell = (double*)(ws + p.off_state);
-    ra.cell = cell;
-    ra.gsum = cell + n_cols;
-    int* q = (int*)(ra.gsum + n_cols);
-    ra.pos = q;
-    ra.last = q + n_cols;
-    ra.gtag = q + 2 * n_cols;
-    ra.gcnt = q + 3 * n_cols;
-    ra.ctag = q + 4 * n_cols;
-    ra.touched = q + 5 * n_cols;
-    ra.cap_rows = n_rows;
-    ra.rows_t = (double*)(ws + p.off_rt);
-    ra.rows_sum = (double*)(ws + p.off_rs);
-    ra.rows_valid = (uint32_t*)(ws + p.off_rv);
-    ra.rows_cnt = (uint32_t*)(ws + p.off_rc);
-    ra.nrows = (int64_t*)(ws + p.off_nrows);
-    ra.sall = (int*)(ws + p.off_sall);
-    ra.counts = counts;
-    ra.metrics = out;
-    ra.err = (int32_t*)(ws + p.off_err);
-    {
-        TimedLaunch tl(K_REPLAY, s);
-        if (rq_launch_replay(ra, nK, s) != hipSuccess) return RQ_EHIP;
-    }
-    ScanArgs sc{};
-    sc.n_chunk = 1;
-    sc.chunk0 = 0;
-    sc.nrows = ra.nrows;
-    sc.nrows_stride = 1;
-    sc.sall = ra.sall;
-    sc.row_stride = n_rows;
-    sc.rows_t = ra.rows_t;
-    sc.rows_sum = ra.rows_sum;
-    sc.rows_valid = ra.rows_valid;
-    sc.rows_cnt = ra.rows_cnt;
-    sc.end = end_time;
-    sc.metrics = out;
-    {
-        TimedLaunch tl(K_SCAN, s);
-        if (rq_launch_scan(sc, nK, s) != hipSuccess) return RQ_EHIP;
-    }
-    return RQ_OK;
+    return rp_run(t, src, sink, event_id, nullptr, 1, n_rows, src_id, end_time, Ks, nK, out,
+                  counts, workspace, workspace_bytes, hip_stream);
+}
+
+int rq_metrics_replay_batch(const double* t, const int64_t* src, const int64_t* sink,
+                            const int64_t* event_id, const int64_t* df_off, int64_t n_df,
+                            int64_t n_rows, int64_t src_id, double end_time, const int32_t* Ks,
+                            int32_t nK, double* out, int64_t* counts, void* workspace,
+                            size_t workspace_bytes, void* hip_stream)
+{
+    if (!df_off) return RQ_EINVAL;
+    return rp_run(t, src, sink, event_id, df_off, n_df, n_rows, src_id, end_time, Ks, nK, out,
+                  counts, workspace, workspace_bytes, hip_stream);
 }
 
 }  // extern "C"

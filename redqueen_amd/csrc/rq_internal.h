@@ -103,38 +103,47 @@ int rq_sweep_blocks_per_cu(int spl, int nK, int col16, int W, int log, int bits,
 hipError_t rq_launch_sweep_fw(const SweepArgs& a, int nK, int col16, int W, int bits, hipStream_t s);
 int rq_fw_blocks_per_cu(int nK, int col16, int W, int bits, int wpb, size_t lds, int pw);
 
-struct ReplayArgs {
+// ---- dataframe replay (rq_replay.hip) ----
+// per-dataframe status, in the workspace
+struct RpInfo {
+    int64_t n_piv;            // pivot rows (unique t)
+    int64_t n_own, n_world;   // distinct event ids of the source / of the others
+    int32_t S;                // unique sink ids (pivot columns)
+    int32_t flags;            // RP_*
+};
+#define RP_FALLBACK 1    // a duplicate (t, sink) pivot cell: the sequential replay owns the df
+#define RP_UNSORTED 2    // 't' decreases
+#define RP_GLOBAL 4      // more unique sinks than the LDS table: needs the global-table pass
+#define RP_EIDBAD 8      // event_id decreases: the event counts are unknown
+#define RP_BIG 16        // needs the large workspace (or exceeds it)
+#define RP_EMPTYDF 32    // no rows
+enum { RP_PHASE_FAST = 0, RP_PHASE_GLOBAL = 1, RP_PHASE_KEYS = 2, RP_PHASE_SEQ = 3, RP_PHASE_SCAN = 4 };
+
+struct RpArgs {
     const double* t;
     const int64_t* src;
-    const int32_t* col;
-    const int64_t* eid;     // may be null
-    int64_t n_rows;
-    int n_cols;
+    const int64_t* sink;
+    const int64_t* eid;       // may be null
+    const int64_t* df_off;    // device [n_df + 1], or null: one dataframe of n_rows rows
+    int64_t n_df, n_rows;
     int64_t src_id;
+    double end;
     int Ks[RQ_MAX_K];
-    int lds_state;          // 1: per-sink state lives in LDS (n_cols * 40 B fits)
-    // per-sink state (global workspace) [n_cols] each
-    int* pos;
-    int* last;
-    int* gtag;
-    int* gcnt;
-    int* ctag;
-    double* cell;
-    double* gsum;
-    int* touched;           // [n_cols]
-    // pivot-row log
-    int64_t cap_rows;
-    double* rows_t;
+    int nK;
+    RpInfo* info;             // [n_df]
+    // pivot rows of dataframe d at rows [df_off[d], ...): dt, cell sum, #valid, #<=K-1
+    double* rows_dt;
     double* rows_sum;
     uint32_t* rows_valid;
-    uint32_t* rows_cnt;
-    int64_t* nrows;         // out [1]
-    int* sall;              // out [1]
-    int64_t* counts;        // out [4] (caller buffer)
-    double* metrics;        // caller buffer (NaN-filled on error)
-    int32_t* err;           // out [1]: 0 ok, 1 unsorted t
+    uint32_t* rows_cnt;       // [row][nK]
+    int64_t* keys;            // [n_rows]: sorted unique sink ids of fallback dataframes
+    // large workspace only (null otherwise): per-df hash tables, slots [4 r0, 4 r1)
+    uint64_t* gkeys;          // [4 n_rows]
+    void* gstate;             // [4 n_rows] x 16 B
+    double* metrics;          // [n_df][nK + 2]
+    int64_t* counts;          // [n_df][4]
 };
-hipError_t rq_launch_replay(const ReplayArgs& a, int nK, hipStream_t s);
+hipError_t rq_launch_rp(const RpArgs& a, int phase, hipStream_t s);
 
 // ---- analysis kernels (rq_analysis.hip) ----
 struct OracleArgs {

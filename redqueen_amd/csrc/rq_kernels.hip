@@ -1,5 +1,5 @@
 // rq_kernels.hip -- the gfx950 engine: stream generation, RedQueen sweep,
-// metric scan, df replay.  Launch wrappers at the bottom are called by the
+// metric scan (the dataframe replay is rq_replay.hip).  Launch wrappers at the bottom are called by the
 // C ABI in rq_api.cpp.
 //
 // Data layout in HBM (one chunk of C replicas in flight):
@@ -1014,237 +1014,6 @@ __global__ __launch_bounds__(256, WPE) void rq_scan(ScanArgs a)
 }
 
 // ============================================================================
-// 4. replay: metrics of a dataframe in the reference's row layout (one wave)
-//    rank_of_src_in_df utils.py:38-56 -> pivot rows (unique t, mean of
-//    duplicate (t, sink) ranks, ffill) -> the same row log the sweep writes.
-// ============================================================================
-template <int NK>
-__global__ __launch_bounds__(64) void rq_replay(ReplayArgs a)
-{
-    extern __shared__ double lds_rp[];
-    const int lane = lane_id();
-    const int S = a.n_cols;
-    if (a.lds_state) {
-        // per-sink state fits the LDS: carve it after the npsum scratch (generic pointers)
-        char* p = reinterpret_cast<char*>(lds_rp + npsum_lds_doubles<1>());
-        a.cell = reinterpret_cast<double*>(p);
-        a.gsum = a.cell + S;
-        int* q = reinterpret_cast<int*>(a.gsum + S);
-        a.pos = q;
-        a.last = q + S;
-        a.gtag = q + 2 * S;
-        a.gcnt = q + 3 * S;
-        a.ctag = q + 4 * S;
-        a.touched = q + 5 * S;
-    }
-    for (int c = lane; c < S; c += 64) {
-        a.pos[c] = 0;
-        a.last[c] = 0;
-        a.gtag[c] = -1;
-        a.gcnt[c] = 0;
-        a.ctag[c] = 0x7fffffff;
-        a.cell[c] = __builtin_nan("");
-        a.gsum[c] = 0.0;
-    }
-    __threadfence_block();
-    __builtin_amdgcn_wave_barrier();
-
-    int km1[NK];
-#pragma unroll
-    for (int q = 0; q < NK; ++q) km1[q] = a.Ks[q] - 1;
-    int64_t sum_int = 0;       // sum of the integral live cells
-    int nfrac = 0;             // live cells with a fractional value
-    int nvalid = 0;
-    int cnt[NK];
-#pragma unroll
-    for (int q = 0; q < NK; ++q) cnt[q] = 0;
-    int ntouch = 0;            // touched sinks of the open t-group
-    int group = 0;
-    double gt = 0.0;           // t of the open group
-    bool open = false;
-    int err = 0;
-    int64_t n_own = 0, n_world = 0, eid_prev = 0;
-    bool eid_bad = false;
-
-    // pivot-row staging
-    double r_t = 0.0, r_sum = 0.0;
-    int r_valid = 0, r_cnt[NK];
-#pragma unroll
-    for (int q = 0; q < NK; ++q) r_cnt[q] = 0;
-    int64_t nrow = 0;
-    double* lds = lds_rp;   // wave_npsum scratch
-
-    auto store_row = [&](int64_t rr) {
-        a.rows_t[rr] = r_t;
-        a.rows_sum[rr] = r_sum;
-        a.rows_valid[rr] = (uint32_t)r_valid;
-#pragma unroll
-        for (int q = 0; q < NK; ++q) a.rows_cnt[rr * NK + q] = (uint32_t)r_cnt[q];
-    };
-
-    // close the open t-group: new cells = mean of the group's ranks per sink
-    auto finalize = [&]() {
-        int64_t dsum = 0;
-        int dfrac = 0, dvalid = 0;
-        int dle[NK];
-#pragma unroll
-        for (int q = 0; q < NK; ++q) dle[q] = 0;
-        for (int b = 0; b < ntouch; b += 64) {
-            const int k = b + lane;
-            const bool act = k < ntouch;
-            double nw = 0.0, od = 0.0;
-            if (act) {
-                const int c = a.touched[k];
-                nw = a.gsum[c] / (double)a.gcnt[c];
-                od = a.cell[c];
-                a.cell[c] = nw;
-                a.gsum[c] = 0.0;
-                a.gcnt[c] = 0;
-            }
-            const bool onan = act && od != od;
-            const bool ofr = act && !onan && od != __builtin_floor(od);
-            const bool nfr = act && nw != __builtin_floor(nw);
-            dvalid += popc(__ballot(onan));
-            dfrac += popc(__ballot(nfr)) - popc(__ballot(ofr));
-            int64_t dv = 0;
-            if (act && !nfr) dv += (int64_t)nw;
-            if (act && !onan && !ofr) dv -= (int64_t)od;
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) dv += __shfl_xor(dv, o, 64);
-            dsum += dv;
-#pragma unroll
-            for (int q = 0; q < NK; ++q) {
-                const double th = (double)km1[q];
-                dle[q] += popc(__ballot(act && nw <= th)) - popc(__ballot(act && !onan && od <= th));
-            }
-        }
-        sum_int += dsum;
-        nfrac += dfrac;
-        nvalid += dvalid;
-#pragma unroll
-        for (int q = 0; q < NK; ++q) cnt[q] += dle[q];
-        ntouch = 0;
-        double rowsum;
-        if (nfrac == 0) {
-            rowsum = (double)sum_int;
-        } else {
-            // fractional cells are live: numpy's pairwise sum over the row, NaN -> 0
-            auto val = [&](int64_t c, double* v) {
-                const double x = a.cell[c];
-                v[0] = x != x ? 0.0 : x;
-            };
-            double r1[1];
-            wave_npsum<1>((int64_t)S, val, lds, r1);
-            rowsum = r1[0];
-        }
-        if (nrow < a.cap_rows) {
-            const int slot = (int)(nrow & 63);
-            if (lane == slot) {
-                r_t = gt;
-                r_sum = rowsum;
-                r_valid = nvalid;
-#pragma unroll
-                for (int q = 0; q < NK; ++q) r_cnt[q] = cnt[q];
-            }
-            if (slot == 63) store_row(nrow - 63 + lane);
-        }
-        ++nrow;
-        ++group;
-    };
-
-    double tprev = -RQ_INF;
-    for (int64_t i0 = 0; i0 < a.n_rows; i0 += 64) {
-        const int64_t i = i0 + lane;
-        const bool valid = i < a.n_rows;
-        const double ti = valid ? a.t[i] : RQ_INF;
-        const int64_t si = valid ? a.src[i] : 0;
-        const int ci = valid ? a.col[i] : 0;
-        double tp = __shfl_up(ti, 1, 64);
-        if (lane == 0) tp = tprev;
-        if (__ballot(valid && ti < tp)) err = 1;
-        uint64_t starts = __ballot(valid && (ti != tp || (i0 == 0 && lane == 0)));
-        if (a.eid) {
-            const int64_t e = valid ? a.eid[i] : 0;
-            int64_t ep = __shfl_up(e, 1, 64);
-            if (lane == 0) ep = eid_prev;
-            const bool first = valid && (i == 0 || e != ep);
-            if (__ballot(valid && i > 0 && e < ep)) eid_bad = true;
-            n_own += popc(__ballot(first && si == a.src_id));
-            n_world += popc(__ballot(first && si != a.src_id));
-            eid_prev = __shfl(e, 63, 64);
-        }
-        tprev = __shfl(ti, 63, 64);
-        const int nv = (int)((a.n_rows - i0) < 64 ? (a.n_rows - i0) : 64);
-        int lo = 0;
-        while (lo < nv) {
-            // sub-range [lo, hi): same t
-            uint64_t later = starts & ~((2ull << lo) - 1ull);   // starts strictly after lo
-            const int hi = later ? (__ffsll((unsigned long long)later) - 1) : nv;
-            const bool isstart = (starts >> lo) & 1ull;
-            if (isstart && open) finalize();
-            if (isstart) {
-                gt = bcast_d(ti, lo);
-                open = true;
-            }
-            // ranks of rows [lo, hi) in df order, same-sink rows in successive rounds
-            bool pend = lane >= lo && lane < hi;
-            while (__ballot(pend)) {
-                if (pend) atomicMin(&a.ctag[ci], lane);
-                __threadfence_block();
-                __builtin_amdgcn_wave_barrier();
-                const bool lead = pend && a.ctag[ci] == lane;
-                if (lead) {
-                    const int p = a.pos[ci] + 1;
-                    a.pos[ci] = p;
-                    if (si == a.src_id) a.last[ci] = p;
-                    const int r = p - a.last[ci];
-                    if (a.gtag[ci] != group) {
-                        a.gtag[ci] = group;
-                        a.gsum[ci] = 0.0;
-                        a.gcnt[ci] = 0;
-                    }
-                    a.gsum[ci] += (double)r;
-                    a.gcnt[ci] += 1;
-                }
-                // new touched sinks of this group: the lead rows whose sink had gcnt == 1
-                const bool fresh = lead && a.gcnt[ci] == 1;
-                const uint64_t fm = __ballot(fresh);
-                if (fresh) {
-                    const int k = ntouch + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32),
-                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
-                    a.touched[k] = ci;
-                }
-                ntouch += popc(fm);
-                __threadfence_block();
-                __builtin_amdgcn_wave_barrier();
-                if (lead) a.ctag[ci] = 0x7fffffff;
-                pend = pend && !lead;
-                __threadfence_block();
-                __builtin_amdgcn_wave_barrier();
-            }
-            lo = hi;
-        }
-    }
-    if (open) finalize();
-    // flush staged rows
-    {
-        const int64_t ns = nrow < a.cap_rows ? nrow : a.cap_rows;
-        const int rem = (int)(ns & 63);
-        if (lane < rem && (nrow & ~63LL) == (ns & ~63LL)) store_row(ns - rem + lane);
-    }
-    if (lane == 0) {
-        a.nrows[0] = nrow <= a.cap_rows ? nrow : 0;
-        a.sall[0] = S;
-        a.counts[0] = a.eid && !eid_bad ? n_own : -1;
-        a.counts[1] = a.eid && !eid_bad ? n_world : -1;
-        a.counts[2] = err ? -1 : nrow;
-        a.counts[3] = S;
-        a.err[0] = err ? 1 : (nrow > a.cap_rows ? 2 : 0);
-        if (err) a.nrows[0] = 0;
-    }
-}
-
-// ============================================================================
 // launch wrappers
 // ============================================================================
 static int rq_cu_count()
@@ -1483,25 +1252,6 @@ static hipError_t launch_scan_t(const ScanArgs& a, hipStream_t s)
     else
         hipLaunchKernelGGL((rq_scan<NK, 4>), dim3(blocks), dim3(256), lds, s, a);
     return hipGetLastError();
-}
-
-template <int NK>
-static hipError_t launch_replay_t(const ReplayArgs& a, hipStream_t s)
-{
-    const size_t lds = npsum_lds_doubles<1>() * sizeof(double) +
-                       (a.lds_state ? (size_t)a.n_cols * 40 : 0);
-    hipLaunchKernelGGL((rq_replay<NK>), dim3(1), dim3(64), lds, s, a);
-    return hipGetLastError();
-}
-
-hipError_t rq_launch_replay(const ReplayArgs& a, int nK, hipStream_t s)
-{
-    switch (nK) {
-    case 1: return launch_replay_t<1>(a, s);
-    case 2: return launch_replay_t<2>(a, s);
-    case 3: return launch_replay_t<3>(a, s);
-    default: return launch_replay_t<4>(a, s);
-    }
 }
 
 hipError_t rq_launch_scan(const ScanArgs& a, int nK, hipStream_t s)

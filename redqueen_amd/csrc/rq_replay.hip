@@ -1,0 +1,896 @@
+// rq_replay.hip -- metrics of dataframes in the reference's row layout, on the
+// raw (t, src_id, sink_id[, event_id]) columns, many dataframes per call.
+//
+// Reference: utils.rank_of_src_in_df (utils.py:38-56) -> time_in_top_k /
+// average_rank / int_r_2 (utils.py:84-121) and num_tweets_of (:170-176), on the
+// df State.get_dataframe builds (opt_model.py:85-97).  SURVEY.md Appendix B is
+// the exact arithmetic (rank scan per sink, pivot on unique t x sorted sink ids
+// with the mean of duplicate (t, sink) cells, ffill, numpy pairwise sums).
+//
+// Kernels (one launch each, every dataframe of the batch in the same launch):
+//
+//   rq_rp_fast<NK, GLOBAL>   one 1024-thread workgroup per dataframe, rows in
+//       batches of 1024 (prefetched one batch ahead).  Sink ids get a dense slot
+//       from a hash table (LDS, <= 3071 unique sinks; the GLOBAL instance keeps it
+//       in HBM for wider dataframes), so no host-side factorisation is needed.
+//       Per batch: a bitonic sort of (slot, row) keys gives every row its
+//       predecessor in its sink's feed; two block max-scans give the segment start
+//       and the latest own post, so rank = pos - lastown (utils.py:43-46) for every
+//       row at once.  Each row then contributes the change of its pivot cell
+//       (rank - previous rank of that sink; NaN -> value for the first row) to a
+//       block scan in row order; at the last row of every t-group the running
+//       totals ARE the pivot row (sum of the forward-filled cells, #non-NaN cells,
+//       #cells <= K-1).  All of it is integer arithmetic, so it is exact; a pivot
+//       row of integral cells sums exactly in any order, which is what numpy's
+//       pairwise row sum returns.  A dataframe with two rows of one sink at one t
+//       (a pandas pivot MEAN, possibly fractional) is handed to rq_rp_seq.
+//   rq_rp_keys       sorted unique sink ids of those dataframes (bitonic sort).
+//   rq_rp_seq<NK>    the exact sequential replay (one wavefront per dataframe,
+//       pivot-cell means and numpy-pairwise row sums while fractional cells are
+//       live) for the dataframes rq_rp_fast handed over.
+//   rq_rp_scan<NK>   numpy-order integrals over each dataframe's pivot rows
+//       (wave_npsum, rq_device.h) + the per-dataframe counts.
+//
+// HBM: 24 B per df row read (t f64, src i64, sink i64) + 8 B with event ids;
+// pivot rows written once (dt f64, sum f64, #valid u32, #<=K-1 u32 per K) and
+// read once by the scan.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rq_device.h"
+#include "rq_internal.h"
+
+#pragma clang fp contract(off)
+
+using namespace rq;
+
+namespace {
+
+constexpr int RP_B = 1024;              // rows per batch = threads per workgroup
+constexpr int RP_LOG_B = 10;
+constexpr int RP_H = 4096;              // LDS hash slots
+constexpr int RP_LOG_H = 12;
+constexpr int RP_HMAX = RP_H - RP_B - 1;   // unique sinks the LDS table takes: a batch can
+                                           // insert RP_B more and still leave an empty slot
+constexpr uint64_t RP_EMPTY_KEY = 0x8000000000000000ull;   // INT64_MIN: gets its own slot
+
+struct alignas(16) RpSlot {
+    int cnt;        // rows of this sink so far (pos of its last row)
+    int lastown;    // pos of its latest own row (0: none)
+    int prevrank;   // rank of its last row (-1: no row yet, the pivot cell is NaN)
+    int lastgroup;  // t-group of its last row (-1: none)
+};
+
+__device__ __forceinline__ uint32_t rp_hash(uint64_t k, int bits)
+{
+    return (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> (64 - bits));
+}
+
+// open addressing, linear probing; returns the slot of key k (inserting it)
+__device__ __forceinline__ uint32_t rp_insert(unsigned long long* keys, uint32_t mask, int bits,
+                                              uint64_t k, int* count)
+{
+    uint32_t h = rp_hash(k, bits);
+    while (true) {
+        const unsigned long long cur = keys[h];
+        if (cur == k) return h;
+        if (cur == RP_EMPTY_KEY) {
+            const unsigned long long old = atomicCAS(&keys[h], (unsigned long long)RP_EMPTY_KEY,
+                                                     (unsigned long long)k);
+            if (old == RP_EMPTY_KEY) {
+                atomicAdd(count, 1);
+                return h;
+            }
+            if (old == k) return h;
+        }
+        h = (h + 1) & mask;
+    }
+}
+
+__device__ __forceinline__ int64_t df_begin(const RpArgs& a, int64_t d) { return a.df_off ? a.df_off[d] : 0; }
+__device__ __forceinline__ int64_t df_end(const RpArgs& a, int64_t d) { return a.df_off ? a.df_off[d + 1] : a.n_rows; }
+
+// global-table capacity of a dataframe of n rows: a power of two >= 2n, <= 2^24
+// (its region in the large workspace is slots [4 r0, 4 r1), so it never overlaps)
+__device__ __forceinline__ int rp_gbits(int64_t n)
+{
+    int b = 1;
+    while (b < 24 && ((int64_t)1 << b) < 2 * n) ++b;
+    return b;
+}
+
+// ---- block (1024-thread) scans: 16 wave totals through LDS, one barrier ----
+template <class T>
+__device__ __forceinline__ T wave_incl_add(T v)
+{
+    const int lane = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const T u = __shfl_up(v, o, 64);
+        if (lane >= o) v += u;
+    }
+    return v;
+}
+template <class T>
+__device__ __forceinline__ T wave_incl_max(T v)
+{
+    const int lane = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const T u = __shfl_up(v, o, 64);
+        if (lane >= o) v = v > u ? v : u;
+    }
+    return v;
+}
+
+__device__ __forceinline__ int lane_bcast(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ int64_t lane_bcast(int64_t v, int l) { return bcast_i64(v, l); }
+
+// the 16 wave totals t[0..16) (LDS) of a block scan -> this wave's exclusive
+// prefix and the block total; lanes 0-15 scan them (w: this wave, uniform)
+template <class T>
+__device__ __forceinline__ void totals_add(const T* t, int w, T& pre, T& tot)
+{
+    T x = lane_id() < 16 ? t[lane_id()] : (T)0;
+    x = wave_incl_add(x);
+    tot = lane_bcast(x, 15);
+    pre = w > 0 ? lane_bcast(x, w - 1) : (T)0;
+}
+template <class T>
+__device__ __forceinline__ T totals_max(const T* t, int w, T ident)
+{
+    T x = lane_id() < 16 ? t[lane_id()] : ident;
+    x = wave_incl_max(x);
+    return w > 0 ? lane_bcast(x, w - 1) : ident;
+}
+
+// bitonic sort of one key per thread (ascending over threadIdx.x).  Partners
+// below 64 lanes apart exchange by shuffles; farther ones through LDS
+// (double-buffered, so one barrier per stage).
+template <class K>
+__device__ __forceinline__ K bitonic_block(K key, K* buf /* [2][RP_B] */)
+{
+    const int tid = threadIdx.x;
+    int par = 0;
+#pragma unroll 1
+    for (int k = 2; k <= RP_B; k <<= 1) {
+#pragma unroll 1
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            K other;
+            if (j >= 64) {
+                K* b = buf + par * RP_B;
+                b[tid] = key;
+                __syncthreads();
+                other = b[tid ^ j];
+                par ^= 1;
+            } else {
+                other = __shfl_xor(key, j, 64);
+            }
+            const bool up = (tid & k) == 0;
+            const bool lower = (tid & j) == 0;
+            const bool take_min = lower == up;
+            key = take_min ? (key < other ? key : other) : (key < other ? other : key);
+        }
+    }
+    return key;
+}
+
+template <int NK>
+struct RpAcc {
+    int64_t s;      // sum of the (integral) forward-filled pivot cells
+    int v;          // non-NaN cells
+    int c[NK];      // cells <= K-1
+};
+
+}  // namespace
+
+// ============================================================================
+// rq_rp_fast: one workgroup per dataframe
+// ============================================================================
+template <int NK, bool GLOBAL>
+__global__ __launch_bounds__(RP_B) void rq_rp_fast(RpArgs a)
+{
+    using Key = typename std::conditional<GLOBAL, uint64_t, uint32_t>::type;
+    constexpr Key KNONE = ~(Key)0;
+    const int64_t d = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    RpInfo* inf = a.info + d;
+    if (GLOBAL && !(inf->flags & RP_GLOBAL)) return;   // only the dataframes the LDS pass gave up
+    const int64_t r0 = df_begin(a, d), r1 = df_end(a, d);
+    const int64_t nd = r1 - r0;
+
+    extern __shared__ __align__(16) unsigned char rp_smem[];
+    unsigned char* sp = rp_smem;
+    auto carve = [&](size_t bytes) {
+        unsigned char* p = sp;
+        sp += (bytes + 15) & ~(size_t)15;
+        return p;
+    };
+    double* tb = reinterpret_cast<double*>(carve(8 * (RP_B + 2)));       // [0] prev, [1+i], [RP_B+1] next
+    int64_t* eb = reinterpret_cast<int64_t*>(carve(8 * (RP_B + 1)));     // [0] prev eid, [1+i]
+    int* gb = reinterpret_cast<int*>(carve(4 * RP_B));                    // t-group of row i
+    unsigned char* ob = carve(RP_B);                                      // own flag of row i
+    Key* sk = reinterpret_cast<Key*>(carve(sizeof(Key) * 2 * RP_B));     // bitonic buffers / sorted keys
+    int* rk = reinterpret_cast<int*>(carve(4 * RP_B));                    // rank by sorted position
+    int* cs = reinterpret_cast<int*>(carve(4 * RP_B));                    // cell change (row order)
+    int* cv = reinterpret_cast<int*>(carve(4 * RP_B));                    // NaN -> value
+    int* cc = reinterpret_cast<int*>(carve(4 * RP_B * NK));               // <= K-1 change, [q][row]
+    int64_t* wsum = reinterpret_cast<int64_t*>(carve(8 * 16));            // wave totals (int64)
+    int* ws32 = reinterpret_cast<int*>(carve(4 * 16 * (NK + 6)));         // wave totals (int)
+    int* misc = reinterpret_cast<int*>(carve(4 * 16));                    // flags, counters
+    unsigned long long* tkeys;
+    RpSlot* tst;
+    uint32_t tmask;
+    int tbits;
+    int64_t tcap;
+    if constexpr (GLOBAL) {
+        tbits = rp_gbits(nd);
+        tcap = (int64_t)1 << tbits;
+        tkeys = reinterpret_cast<unsigned long long*>(a.gkeys) + 4 * r0;
+        tst = reinterpret_cast<RpSlot*>(a.gstate) + 4 * r0;
+    } else {
+        tbits = RP_LOG_H;
+        tcap = RP_H;
+        tkeys = reinterpret_cast<unsigned long long*>(carve(8 * (RP_H + 1)));
+        tst = reinterpret_cast<RpSlot*>(carve(sizeof(RpSlot) * (RP_H + 1)));
+    }
+    tmask = (uint32_t)(tcap - 1);
+    // misc: [0] unique sinks, [1] sentinel-key seen, [2] dup, [3] unsorted, [4] eid bad,
+    //       [5] own events, [6] world events, [7] key dump cursor
+    if (tid < 16) misc[tid] = 0;
+    if (!GLOBAL && tid == 0) inf->flags = 0;   // this call's status (the LDS pass runs first)
+    for (int64_t h = tid; h <= tcap; h += RP_B) {
+        tkeys[h] = RP_EMPTY_KEY;
+        tst[h] = RpSlot{0, 0, -1, -1};
+    }
+    if (GLOBAL && 2 * nd > tcap) {   // > 2^23 unique sinks possible: not supported
+        if (tid == 0) atomicOr(&inf->flags, RP_BIG);
+        return;
+    }
+    if (GLOBAL) __threadfence();   // the table's reset reaches L2 before the atomics below
+    __syncthreads();
+
+    int km1[NK];
+#pragma unroll
+    for (int q = 0; q < NK; ++q) km1[q] = a.Ks[q] - 1;
+    const bool has_eid = a.eid != nullptr;
+
+    // carries across batches
+    int64_t Gc = 0;        // t-groups started so far
+    RpAcc<NK> carry;
+    carry.s = 0;
+    carry.v = 0;
+#pragma unroll
+    for (int q = 0; q < NK; ++q) carry.c[q] = 0;
+    double tprev = 0.0;
+    int64_t eprev = 0;
+    bool aborted = false;
+
+    // prefetched row of this thread
+    int64_t i = r0 + tid;
+    double ti = 0.0;
+    int64_t si = 0, ki = 0, ei = 0;
+    if (i < r1) {
+        ti = a.t[i];
+        si = a.src[i];
+        ki = a.sink[i];
+        if (has_eid) ei = a.eid[i];
+    }
+
+    for (int64_t b0 = r0; b0 < r1; b0 += RP_B) {
+        i = b0 + tid;
+        const bool valid = i < r1;
+        // next batch (in flight across this batch's barriers)
+        const int64_t in = i + RP_B;
+        double tn = 0.0;
+        int64_t sn = 0, kn = 0, en = 0;
+        if (in < r1) {
+            tn = a.t[in];
+            sn = a.src[in];
+            kn = a.sink[in];
+            if (has_eid) en = a.eid[in];
+        }
+
+        // ---- A: neighbours of every row; dense sink slots ----
+        tb[1 + tid] = valid ? ti : 0.0;
+        if (has_eid) eb[1 + tid] = ei;
+        if (tid == 0) {
+            tb[0] = tprev;
+            eb[0] = eprev;
+            tb[RP_B + 1] = tn;   // row b0 + RP_B (meaningful only if it exists)
+        }
+        uint32_t slot = 0;
+        if (valid) {
+            if ((uint64_t)ki == RP_EMPTY_KEY) {
+                slot = (uint32_t)tcap;   // the sentinel id's own slot
+                if (misc[1] == 0 && atomicExch(&misc[1], 1) == 0) atomicAdd(&misc[0], 1);
+            } else {
+                slot = rp_insert(tkeys, tmask, tbits, (uint64_t)ki, &misc[0]);
+            }
+        }
+        __syncthreads();
+        const double t_prev = tb[tid], t_next = tb[tid + 2];
+        const bool first_row = i == r0;
+        const bool start = valid && (first_row || ti != t_prev);
+        const bool endg = valid && (i == r1 - 1 || t_next != ti);
+        const bool own = valid && si == a.src_id;
+        if (valid && !first_row && ti < t_prev) misc[3] = 1;
+        int ev_own = 0, ev_world = 0;
+        if (has_eid && valid) {
+            const int64_t e_prev = eb[tid];
+            const bool fe = first_row || ei != e_prev;
+            if (!first_row && ei < e_prev) misc[4] = 1;
+            ev_own = fe && own;
+            ev_world = fe && !own;
+        }
+        if (!GLOBAL && misc[0] > RP_HMAX) aborted = true;   // uniform: read after the barrier
+
+        // ---- B: t-group of every row (block scan of group starts) + event counts ----
+        const int st_incl = wave_incl_add((int)start);
+        const uint64_t bo = __ballot(ev_own), bw = __ballot(ev_world);
+        if (lane == 63) {
+            ws32[w] = st_incl;
+            ws32[16 + w] = popc(bo);
+            ws32[32 + w] = popc(bw);
+        }
+        __syncthreads();
+        int st_pre, st_tot, n_ev_own, n_ev_world, dummy;
+        totals_add(ws32, w, st_pre, st_tot);
+        totals_add(ws32 + 16, w, dummy, n_ev_own);
+        totals_add(ws32 + 32, w, dummy, n_ev_world);
+        const int64_t G = Gc + (int64_t)(st_pre + st_incl) - 1;   // this row's t-group (pivot row index)
+        gb[tid] = (int)G;
+        ob[tid] = own ? 1 : 0;
+        if (aborted) break;
+
+        // ---- C: sort (slot, row): a row's predecessor in its sink's feed ----
+        const Key key0 = valid ? (((Key)slot << RP_LOG_B) | (Key)tid) : KNONE;
+        const Key key = bitonic_block<Key>(key0, sk);   // sorted position p = tid
+        __syncthreads();
+        sk[tid] = key;
+        __syncthreads();
+        const Key keyp = tid > 0 ? sk[tid - 1] : KNONE;
+        const Key keyn = tid < RP_B - 1 ? sk[tid + 1] : KNONE;
+        const bool vp = key != KNONE;
+        const Key slp = key >> RP_LOG_B;
+        const int idx = (int)(key & (RP_B - 1));
+        const bool head = vp && (tid == 0 || (keyp >> RP_LOG_B) != slp);
+        const bool tail = vp && (tid == RP_B - 1 || (keyn >> RP_LOG_B) != slp);
+        const bool ownp = vp && ob[idx];
+        const int Gp = vp ? gb[idx] : 0;
+        // segment start and the latest own row at or before p: block max-scans
+        int ss = wave_incl_max(head ? tid : 0);
+        int lo = wave_incl_max(ownp ? tid : -1);
+        if (lane == 63) {
+            ws32[48 + w] = ss;
+            ws32[64 + w] = lo;
+        }
+        __syncthreads();
+        {
+            const int p1 = totals_max(ws32 + 48, w, 0), p2 = totals_max(ws32 + 64, w, -1);
+            ss = ss > p1 ? ss : p1;
+            lo = lo > p2 ? lo : p2;
+        }
+        RpSlot st = RpSlot{0, 0, -1, -1};
+        if (vp) st = tst[slp];
+        const int j = tid - ss;
+        const int pos = st.cnt + j + 1;
+        const int lastown = lo >= ss ? st.cnt + (lo - ss) + 1 : st.lastown;
+        const int rank = pos - lastown;
+        rk[tid] = rank;
+        __syncthreads();
+        if (vp) {
+            const int prevrank = j > 0 ? rk[tid - 1] : st.prevrank;
+            const int prevg = j > 0 ? gb[(int)(keyp & (RP_B - 1))] : st.lastgroup;
+            if (prevg == Gp) misc[2] = 1;   // two rows of one sink at one t: a pivot mean
+            const bool pnan = prevrank < 0;
+            cs[idx] = rank - (pnan ? 0 : prevrank);
+            cv[idx] = pnan ? 1 : 0;
+#pragma unroll
+            for (int q = 0; q < NK; ++q)
+                cc[q * RP_B + idx] = (rank <= km1[q] ? 1 : 0) - ((!pnan && prevrank <= km1[q]) ? 1 : 0);
+            if (tail) tst[slp] = RpSlot{pos, lastown, rank, Gp};
+        }
+        if (!valid) {
+            cs[tid] = 0;
+            cv[tid] = 0;
+#pragma unroll
+            for (int q = 0; q < NK; ++q) cc[q * RP_B + tid] = 0;
+        }
+        __syncthreads();
+
+        // ---- D: running totals in row order; the last row of a t-group emits its pivot row ----
+        RpAcc<NK> x;
+        x.s = cs[tid];
+        x.v = cv[tid];
+#pragma unroll
+        for (int q = 0; q < NK; ++q) x.c[q] = cc[q * RP_B + tid];
+        x.s = wave_incl_add(x.s);
+        x.v = wave_incl_add(x.v);
+#pragma unroll
+        for (int q = 0; q < NK; ++q) x.c[q] = wave_incl_add(x.c[q]);
+        if (lane == 63) {
+            wsum[w] = x.s;
+            ws32[80 + w] = x.v;
+#pragma unroll
+            for (int q = 0; q < NK; ++q) ws32[96 + 16 * q + w] = x.c[q];
+        }
+        __syncthreads();
+        RpAcc<NK> pre, tot;
+        totals_add(wsum, w, pre.s, tot.s);
+        totals_add(ws32 + 80, w, pre.v, tot.v);
+#pragma unroll
+        for (int q = 0; q < NK; ++q) totals_add(ws32 + 96 + 16 * q, w, pre.c[q], tot.c[q]);
+        if (endg) {
+            const int64_t row = r0 + G;
+            a.rows_dt[row] = (i == r1 - 1 ? a.end : t_next) - ti;
+            a.rows_sum[row] = (double)(carry.s + pre.s + x.s);
+            a.rows_valid[row] = (uint32_t)(carry.v + pre.v + x.v);
+#pragma unroll
+            for (int q = 0; q < NK; ++q) a.rows_cnt[row * NK + q] = (uint32_t)(carry.c[q] + pre.c[q] + x.c[q]);
+        }
+        carry.s += tot.s;
+        carry.v += tot.v;
+#pragma unroll
+        for (int q = 0; q < NK; ++q) carry.c[q] += tot.c[q];
+        Gc += st_tot;
+        if (tid == 0) {
+            misc[5] += (int)n_ev_own;
+            misc[6] += (int)n_ev_world;
+        }
+        const int last = (int)((r1 - b0) < RP_B ? (r1 - b0) : RP_B);
+        tprev = tb[last];
+        if (has_eid) eprev = eb[last];
+        ti = tn;
+        si = sn;
+        ki = kn;
+        ei = en;
+        __syncthreads();   // tb / eb / wsum are rewritten by the next batch
+        if (misc[3]) break;   // unsorted: the dataframe is rejected
+    }
+
+    __syncthreads();
+    if (aborted) {
+        if (tid == 0) atomicOr(&inf->flags, RP_GLOBAL);
+        return;
+    }
+    const int S = misc[0];
+    const bool dup = misc[2] != 0;
+    if (tid == 0) {
+        inf->n_piv = Gc;
+        inf->S = S;
+        inf->n_own = misc[5];
+        inf->n_world = misc[6];
+        int fl = 0;
+        if (dup) fl |= RP_FALLBACK;
+        if (misc[3]) fl |= RP_UNSORTED;
+        if (misc[4]) fl |= RP_EIDBAD;
+        if (nd == 0) fl |= RP_EMPTYDF;
+        inf->flags = fl;   // clears RP_GLOBAL after the global pass
+    }
+    // the sequential replay needs this dataframe's sorted unique sink ids: dump them
+    if (dup && !misc[3]) {
+        if (tid == 0) misc[7] = 0;
+        __syncthreads();
+        for (int64_t h = tid; h <= tcap; h += RP_B) {
+            const unsigned long long k = tkeys[h];
+            const bool occ = h < tcap ? k != RP_EMPTY_KEY : misc[1] != 0;
+            if (occ) {
+                const int at = atomicAdd(&misc[7], 1);
+                a.keys[r0 + at] = h < tcap ? (int64_t)k : (int64_t)RP_EMPTY_KEY;
+            }
+        }
+    }
+}
+
+// ============================================================================
+// rq_rp_keys: sort the unique sink ids of every fallback dataframe (ascending,
+// the pivot_table column order).  Bitonic over the next power of two, in LDS up
+// to 8192 keys, else in the large workspace's table region.
+// ============================================================================
+constexpr int RP_KEYS_LDS = 8192;
+
+__global__ __launch_bounds__(RP_B) void rq_rp_keys(RpArgs a)
+{
+    const int64_t d = blockIdx.x;
+    RpInfo* inf = a.info + d;
+    const int fl = inf->flags;
+    if (!(fl & RP_FALLBACK) || (fl & (RP_UNSORTED | RP_GLOBAL | RP_BIG))) return;
+    const int64_t r0 = df_begin(a, d);
+    const int S = inf->S;
+    int64_t* keys = a.keys + r0;
+    int n2 = 1;
+    while (n2 < S) n2 <<= 1;
+    __shared__ int64_t lds[RP_KEYS_LDS];
+    int64_t* buf = lds;
+    if (n2 > RP_KEYS_LDS) {
+        if (!a.gkeys) {
+            if (threadIdx.x == 0) atomicOr(&inf->flags, RP_BIG);
+            return;
+        }
+        buf = reinterpret_cast<int64_t*>(a.gkeys) + 4 * r0;   // this df's table region (>= 2 S)
+    }
+    for (int k = threadIdx.x; k < n2; k += RP_B) buf[k] = k < S ? keys[k] : INT64_MAX;
+    __syncthreads();
+    for (int k = 2; k <= n2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int x = threadIdx.x; x < n2; x += RP_B) {
+                const int y = x ^ j;
+                if (y > x) {
+                    const int64_t u = buf[x], v = buf[y];
+                    const bool up = (x & k) == 0;
+                    if ((u > v) == up) {
+                        buf[x] = v;
+                        buf[y] = u;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int k = threadIdx.x; k < S; k += RP_B) keys[k] = buf[k];
+}
+
+// ============================================================================
+// rq_rp_seq: the exact sequential replay of one dataframe per wavefront, for
+// the dataframes with pivot means (duplicate (t, sink) rows).  Per-sink state in
+// LDS when it fits (40 B per sink), else in the large workspace.
+// ============================================================================
+constexpr size_t RP_SEQ_LDS = 120 * 1024;
+
+template <int NK>
+__global__ __launch_bounds__(64) void rq_rp_seq(RpArgs a)
+{
+    const int64_t d = blockIdx.x;
+    RpInfo* inf = a.info + d;
+    const int fl = inf->flags;
+    if (!(fl & RP_FALLBACK) || (fl & (RP_UNSORTED | RP_GLOBAL | RP_BIG))) return;
+    extern __shared__ double lds_rp[];
+    const int lane = lane_id();
+    const int64_t r0 = df_begin(a, d), r1 = df_end(a, d);
+    const int64_t n_rows = r1 - r0;
+    const int S = inf->S;
+    const int64_t* keys = a.keys + r0;
+    const double* T = a.t + r0;
+    const int64_t* SRC = a.src + r0;
+    const int64_t* SNK = a.sink + r0;
+
+    // per-sink state
+    char* base;
+    if ((size_t)S * 40 <= RP_SEQ_LDS) {
+        base = reinterpret_cast<char*>(lds_rp + npsum_lds_doubles<1>());
+    } else {
+        if (!a.gstate) {
+            if (lane == 0) atomicOr(&inf->flags, RP_BIG);
+            return;
+        }
+        base = reinterpret_cast<char*>(a.gstate) + (size_t)64 * r0;   // the df's state region (64 B/row)
+    }
+    double* cell = reinterpret_cast<double*>(base);
+    double* gsum = cell + S;
+    int* pos = reinterpret_cast<int*>(gsum + S);
+    int* last = pos + S;
+    int* gtag = pos + 2 * S;
+    int* gcnt = pos + 3 * S;
+    int* ctag = pos + 4 * S;
+    int* touched = pos + 5 * S;
+    for (int c = lane; c < S; c += 64) {
+        pos[c] = 0;
+        last[c] = 0;
+        gtag[c] = -1;
+        gcnt[c] = 0;
+        ctag[c] = 0x7fffffff;
+        cell[c] = __builtin_nan("");
+        gsum[c] = 0.0;
+    }
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+
+    int km1[NK];
+#pragma unroll
+    for (int q = 0; q < NK; ++q) km1[q] = a.Ks[q] - 1;
+    int64_t sum_int = 0;       // sum of the integral live cells
+    int nfrac = 0;             // live cells with a fractional value
+    int nvalid = 0;
+    int cnt[NK];
+#pragma unroll
+    for (int q = 0; q < NK; ++q) cnt[q] = 0;
+    int ntouch = 0;            // touched sinks of the open t-group
+    int group = 0;
+    double gt = 0.0;           // t of the open group
+    bool open = false;
+
+    // pivot rows: t staged per lane, stored 64 at a time; converted to dt at the end
+    double r_t = 0.0, r_sum = 0.0;
+    int r_valid = 0, r_cnt[NK];
+#pragma unroll
+    for (int q = 0; q < NK; ++q) r_cnt[q] = 0;
+    int64_t nrow = 0;
+    double* lds = lds_rp;   // wave_npsum scratch
+    double* R_t = a.rows_dt + r0;
+    double* R_s = a.rows_sum + r0;
+    uint32_t* R_v = a.rows_valid + r0;
+    uint32_t* R_c = a.rows_cnt + r0 * NK;
+
+    auto store_row = [&](int64_t rr) {
+        R_t[rr] = r_t;
+        R_s[rr] = r_sum;
+        R_v[rr] = (uint32_t)r_valid;
+#pragma unroll
+        for (int q = 0; q < NK; ++q) R_c[rr * NK + q] = (uint32_t)r_cnt[q];
+    };
+
+    // close the open t-group: new cells = mean of the group's ranks per sink
+    auto finalize = [&]() {
+        int64_t dsum = 0;
+        int dfrac = 0, dvalid = 0;
+        int dle[NK];
+#pragma unroll
+        for (int q = 0; q < NK; ++q) dle[q] = 0;
+        for (int b = 0; b < ntouch; b += 64) {
+            const int k = b + lane;
+            const bool act = k < ntouch;
+            double nw = 0.0, od = 0.0;
+            if (act) {
+                const int c = touched[k];
+                nw = gsum[c] / (double)gcnt[c];
+                od = cell[c];
+                cell[c] = nw;
+                gsum[c] = 0.0;
+                gcnt[c] = 0;
+            }
+            const bool onan = act && od != od;
+            const bool ofr = act && !onan && od != __builtin_floor(od);
+            const bool nfr = act && nw != __builtin_floor(nw);
+            dvalid += popc(__ballot(onan));
+            dfrac += popc(__ballot(nfr)) - popc(__ballot(ofr));
+            int64_t dv = 0;
+            if (act && !nfr) dv += (int64_t)nw;
+            if (act && !onan && !ofr) dv -= (int64_t)od;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) dv += __shfl_xor(dv, o, 64);
+            dsum += dv;
+#pragma unroll
+            for (int q = 0; q < NK; ++q) {
+                const double th = (double)km1[q];
+                dle[q] += popc(__ballot(act && nw <= th)) - popc(__ballot(act && !onan && od <= th));
+            }
+        }
+        sum_int += dsum;
+        nfrac += dfrac;
+        nvalid += dvalid;
+#pragma unroll
+        for (int q = 0; q < NK; ++q) cnt[q] += dle[q];
+        ntouch = 0;
+        double rowsum;
+        if (nfrac == 0) {
+            rowsum = (double)sum_int;
+        } else {
+            // fractional cells are live: numpy's pairwise sum over the row, NaN -> 0
+            auto val = [&](int64_t c, double* v) {
+                const double x = cell[c];
+                v[0] = x != x ? 0.0 : x;
+            };
+            double r1v[1];
+            wave_npsum<1>((int64_t)S, val, lds, r1v);
+            rowsum = r1v[0];
+        }
+        const int slot = (int)(nrow & 63);
+        if (lane == slot) {
+            r_t = gt;
+            r_sum = rowsum;
+            r_valid = nvalid;
+#pragma unroll
+            for (int q = 0; q < NK; ++q) r_cnt[q] = cnt[q];
+        }
+        if (slot == 63) store_row(nrow - 63 + lane);
+        ++nrow;
+        ++group;
+    };
+
+    double tprev = -RQ_INF;
+    for (int64_t i0 = 0; i0 < n_rows; i0 += 64) {
+        const int64_t i = i0 + lane;
+        const bool valid = i < n_rows;
+        const double ti = valid ? T[i] : RQ_INF;
+        const int64_t si = valid ? SRC[i] : 0;
+        int ci = 0;
+        if (valid) {   // column = rank of the sink id among the sorted unique ids
+            const int64_t k = SNK[i];
+            int lo = 0, hi = S;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (keys[mid] < k) lo = mid + 1; else hi = mid;
+            }
+            ci = lo;
+        }
+        double tp = __shfl_up(ti, 1, 64);
+        if (lane == 0) tp = tprev;
+        const uint64_t starts = __ballot(valid && (ti != tp || (i0 == 0 && lane == 0)));
+        tprev = __shfl(ti, 63, 64);
+        const int nv = (int)((n_rows - i0) < 64 ? (n_rows - i0) : 64);
+        int lo = 0;
+        while (lo < nv) {
+            // sub-range [lo, hi): same t
+            const uint64_t later = starts & ~((2ull << lo) - 1ull);   // starts strictly after lo
+            const int hi = later ? (__ffsll((unsigned long long)later) - 1) : nv;
+            const bool isstart = (starts >> lo) & 1ull;
+            if (isstart && open) finalize();
+            if (isstart) {
+                gt = bcast_d(ti, lo);
+                open = true;
+            }
+            // ranks of rows [lo, hi) in df order, same-sink rows in successive rounds
+            bool pend = lane >= lo && lane < hi;
+            while (__ballot(pend)) {
+                if (pend) atomicMin(&ctag[ci], lane);
+                __threadfence_block();
+                __builtin_amdgcn_wave_barrier();
+                const bool lead = pend && ctag[ci] == lane;
+                if (lead) {
+                    const int p = pos[ci] + 1;
+                    pos[ci] = p;
+                    if (si == a.src_id) last[ci] = p;
+                    const int r = p - last[ci];
+                    if (gtag[ci] != group) {
+                        gtag[ci] = group;
+                        gsum[ci] = 0.0;
+                        gcnt[ci] = 0;
+                    }
+                    gsum[ci] += (double)r;
+                    gcnt[ci] += 1;
+                }
+                // new touched sinks of this group: the lead rows whose sink had gcnt == 1
+                const bool fresh = lead && gcnt[ci] == 1;
+                const uint64_t fm = __ballot(fresh);
+                if (fresh) {
+                    const int k = ntouch + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
+                    touched[k] = ci;
+                }
+                ntouch += popc(fm);
+                __threadfence_block();
+                __builtin_amdgcn_wave_barrier();
+                if (lead) ctag[ci] = 0x7fffffff;
+                pend = pend && !lead;
+                __threadfence_block();
+                __builtin_amdgcn_wave_barrier();
+            }
+            lo = hi;
+        }
+    }
+    if (open) finalize();
+    {   // flush the staged rows
+        const int rem = (int)(nrow & 63);
+        if (lane < rem) store_row(nrow - rem + lane);
+    }
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+    // pivot-row t -> dt in place, left to right (a chunk reads t[k + 64] before the
+    // next chunk overwrites it)
+    for (int64_t k0 = 0; k0 < nrow; k0 += 64) {
+        const int64_t k = k0 + lane;
+        double dt = 0.0;
+        if (k < nrow) dt = (k + 1 < nrow ? R_t[k + 1] : a.end) - R_t[k];
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+        if (k < nrow) R_t[k] = dt;
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (lane == 0) inf->n_piv = nrow;
+}
+
+// ============================================================================
+// rq_rp_scan: numpy-order integrals over each dataframe's pivot rows
+// (one wavefront per dataframe) and the per-dataframe outputs
+// ============================================================================
+template <int NK>
+__global__ __launch_bounds__(256) void rq_rp_scan(RpArgs a)
+{
+    constexpr int NV = NK + 2;
+    extern __shared__ double lds_rs[];
+    const int w = threadIdx.x >> 6;
+    const int lane = lane_id();
+    const int64_t d = (int64_t)blockIdx.x * 4 + w;
+    if (d >= a.n_df) return;
+    double* lds = lds_rs + (size_t)w * npsum_lds_doubles<NV>();
+    const RpInfo inf = a.info[d];
+    const int64_t r0 = df_begin(a, d);
+    double* out = a.metrics + d * NV;
+    int64_t* cnt = a.counts + d * 4;
+    const bool eid_ok = a.eid && !(inf.flags & RP_EIDBAD);
+    const int bad = inf.flags & (RP_UNSORTED | RP_GLOBAL | RP_BIG | RP_EMPTYDF);
+    if (lane == 0) {
+        cnt[0] = eid_ok ? inf.n_own : -1;
+        cnt[1] = eid_ok ? inf.n_world : -1;
+        cnt[2] = (inf.flags & RP_UNSORTED) ? RQ_EUNSORTED
+                 : (inf.flags & (RP_GLOBAL | RP_BIG)) ? RQ_EOVERFLOW
+                 : (inf.flags & RP_EMPTYDF) ? 0 : inf.n_piv;
+        cnt[3] = inf.S;
+    }
+    if (bad || inf.n_piv <= 0) {
+        if (lane < NV) out[lane] = __builtin_nan("");
+        return;
+    }
+    const int64_t n = inf.n_piv;
+    const double S = (double)inf.S;
+    const double* Rd = a.rows_dt + r0;
+    const double* Rs = a.rows_sum + r0;
+    const uint32_t* Rv = a.rows_valid + r0;
+    const uint32_t* Rc = a.rows_cnt + r0 * NK;
+    auto val = [&](int64_t kk, double* v) {
+        const double dt = Rd[kk];
+        const double m = Rs[kk] / (double)Rv[kk];
+#pragma unroll
+        for (int q = 0; q < NK; ++q) v[q] = ((double)Rc[kk * NK + q] / S) * dt;
+        v[NK] = m * dt;
+        v[NK + 1] = (m * m) * dt;
+    };
+    double res[NV];
+    wave_npsum<NV>(n, val, lds, res);
+    if (lane == 0) {
+#pragma unroll
+        for (int s = 0; s < NV; ++s) out[s] = res[s];
+    }
+}
+
+// ============================================================================
+// launch wrappers
+// ============================================================================
+namespace {
+template <bool GLOBAL, class Key>
+size_t rp_fast_lds(int nK)
+{
+    auto al = [](size_t b) { return (b + 15) & ~(size_t)15; };
+    size_t s = al(8 * (RP_B + 2)) + al(8 * (RP_B + 1)) + al(4 * RP_B) + al(RP_B) +
+               al(sizeof(Key) * 2 * RP_B) + 3 * al(4 * RP_B) + al(4 * (size_t)RP_B * nK) +
+               al(8 * 16) + al(4 * 16 * (nK + 6)) + al(4 * 16);
+    if (!GLOBAL) s += al(8 * (RP_H + 1)) + al(sizeof(RpSlot) * (RP_H + 1));
+    return s;
+}
+
+template <int NK>
+hipError_t rp_launch_t(const RpArgs& a, int phase, hipStream_t s)
+{
+    const unsigned nd = (unsigned)a.n_df;
+    switch (phase) {
+    case RP_PHASE_FAST: {
+        const size_t lds = rp_fast_lds<false, uint32_t>(NK);
+        hipLaunchKernelGGL((rq_rp_fast<NK, false>), dim3(nd), dim3(RP_B), lds, s, a);
+        break;
+    }
+    case RP_PHASE_GLOBAL: {
+        const size_t lds = rp_fast_lds<true, uint64_t>(NK);
+        hipLaunchKernelGGL((rq_rp_fast<NK, true>), dim3(nd), dim3(RP_B), lds, s, a);
+        break;
+    }
+    case RP_PHASE_KEYS:
+        hipLaunchKernelGGL(rq_rp_keys, dim3(nd), dim3(RP_B), 0, s, a);
+        break;
+    case RP_PHASE_SEQ: {
+        const size_t lds = npsum_lds_doubles<1>() * sizeof(double) + RP_SEQ_LDS;
+        hipLaunchKernelGGL((rq_rp_seq<NK>), dim3(nd), dim3(64), lds, s, a);
+        break;
+    }
+    default: {
+        const size_t lds = 4 * npsum_lds_doubles<NK + 2>() * sizeof(double);
+        hipLaunchKernelGGL((rq_rp_scan<NK>), dim3((nd + 3) / 4), dim3(256), lds, s, a);
+        break;
+    }
+    }
+    return hipGetLastError();
+}
+}  // namespace
+
+hipError_t rq_launch_rp(const RpArgs& a, int phase, hipStream_t s)
+{
+    if (a.n_df <= 0) return hipSuccess;
+    switch (a.nK) {
+    case 1: return rp_launch_t<1>(a, phase, s);
+    case 2: return rp_launch_t<2>(a, phase, s);
+    case 3: return rp_launch_t<3>(a, phase, s);
+    default: return rp_launch_t<4>(a, phase, s);
+    }
+}

@@ -133,7 +133,15 @@ class Graph:
             row = np.ones(F, dtype=np.float64) * np.asarray(s, dtype=np.float64)
         return np.ascontiguousarray(np.tile(row, (n_grid, 1)))
 
-    def run(self, ctrl="opt", q=1.0, s=None, n_rep=1, ctrl_seed=0, world_seed=0,
+    def run(self, *args, stream=None, **kw):
+        """Enqueue one batch on ``stream`` (default: the current torch stream).  Every
+        tensor the batch reads or writes is allocated with that stream current, so
+        the caching allocator, the library and the status check all agree on it."""
+        use = stream or torch.cuda.current_stream()
+        with torch.cuda.stream(use):
+            return self._run(*args, stream=use, **kw)
+
+    def _run(self, ctrl="opt", q=1.0, s=None, n_rep=1, ctrl_seed=0, world_seed=0,
             randomize=False, seed_mod=0, ctrl_rate=None, Ks=(1,), max_events=None,
             event_log=False, cap_scale=1.0, chunk=0, stream=None, check=True, sweep_mode=0, replica0=0, n_local=0,
             plan_only=False, s_pw=None, period=None):
@@ -222,6 +230,11 @@ class Graph:
             keys = ("variant", "sources_per_lane", "ring_depth", "waves_per_block",
                     "blocks_per_cu", "columns_in_lds", "lds_bytes_per_block", "chunk")
             return dict(zip(keys, (int(v) for v in info)))
+        return self._run_loop(lib, b, keep, dev, R, Ks, n_grid, n_rep, ck, event_log,
+                              replica0, check, stream)
+
+    def _run_loop(self, lib, b, keep, dev, R, Ks, n_grid, n_rep, ck, event_log, replica0,
+                  check, use):
         while True:
             nbytes = C.c_size_t()
             L.check("rq_workspace_size", lib.rq_workspace_size(self._h, C.byref(b), C.byref(nbytes)))
@@ -240,27 +253,33 @@ class Graph:
                 ev_t = torch.empty((R, cap.value), dtype=torch.float64, device=dev)
                 ev_src = torch.empty((R, cap.value), dtype=torch.int32, device=dev)
                 out.ev_t, out.ev_src, out.ev_cap = ev_t.data_ptr(), ev_src.data_ptr(), cap.value
-            st = (stream or torch.cuda.current_stream()).cuda_stream
+            st = use.cuda_stream
             L.check("rq_run_batch", lib.rq_run_batch(self._h, C.byref(b), C.byref(out),
                                                      self._ws.data_ptr(), self._ws.numel(), st))
             res = BatchResult(self, metrics, counts, status, ev_t, ev_src, Ks, n_grid, int(n_rep))
             res.replica0 = int(replica0)
             if not check:
                 return res
-            torch.cuda.current_stream().synchronize()
+            use.synchronize()
             ovf = int((status & (L.ST_ROWS_OVERFLOW | L.ST_STREAM_OVERFLOW)).any().item())
             if not ovf:
-                # equal event times in the fast tiled sweep: redo with the exact sequential
-                # sweep (never taken by continuous-time worlds; RealData runs are exact already)
-                seq = (b.max_events >= 0 or b.sweep_mode in (1, 2, 5) or self.has_realdata
-                       or ck == L.SRC_REALDATA or (event_log and self.n_streams > 64))
-                if not seq and int((status & L.ST_TIE).any().item()):
+                # equal event times in a fast tiled sweep: redo with the exact sequential
+                # sweep (never taken by continuous-time worlds).  Whether this run was the
+                # sequential variant comes from the library's own plan (rq_plan_info
+                # variant 1), not from a re-derivation of its rules here.
+                if int((status & L.ST_TIE).any().item()) and b.sweep_mode != 2 \
+                        and self._plan_variant(lib, b) % 10 != 1:
                     b.sweep_mode = 2
                     continue
                 return res
             if b.cap_scale > 64:
                 raise L.RQError("rq_run_batch", L.RQ_EOVERFLOW)
             b.cap_scale = b.cap_scale * 2.0
+
+    def _plan_variant(self, lib, b):
+        info = (C.c_int64 * 8)()
+        L.check("rq_plan_info", lib.rq_plan_info(self._h, C.byref(b), info))
+        return int(info[0])
 
 
 class BatchResult:
@@ -303,9 +322,14 @@ class BatchResult:
         device tensors); replica i owns rows [row_off[i], row_off[i+1])."""
         if self.ev_t is None:
             raise ValueError("run with event_log=True to export the event log")
+        use = stream or torch.cuda.current_stream()
+        with torch.cuda.stream(use):
+            return self._log_columns(use)
+
+    def _log_columns(self, use):
         dev = self.ev_t.device
         R, cap = self.ev_t.shape
-        st = (stream or torch.cuda.current_stream()).cuda_stream
+        st = use.cuda_stream
         row_off = torch.empty(R + 1, dtype=torch.int64, device=dev)
         lib = L.lib()
         L.check("rq_log_rows", lib.rq_log_rows(self.graph._h, self.ev_src.data_ptr(),

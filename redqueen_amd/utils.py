@@ -5,8 +5,9 @@
 and return numpy float64 scalars, computed by ``rq_metrics_replay`` on the GPU
 with the reference's exact arithmetic (rank scan, pivot mean, ffill, numpy
 pairwise sums).  The only host work is handing the
-columns over: the df's sink ids are factorised into pivot-column indices
-(np.unique) and the columns are copied to device memory.
+columns over to device memory: sink ids go over raw and the pivot columns are
+built on the device.  ``replay_frames`` / ``replay_columns`` replay many
+dataframes in one batched call (rq_metrics_replay_batch).
 ``calc_q_capacity_iter`` (utils.py:447-470) runs its seeds as one GPU batch.
 
 Analysis helpers on the same footing: ``rank_of_src_in_df`` (utils.py:38-56)
@@ -45,6 +46,56 @@ def is_sorted(x, ascending=True):
 _WS = {}
 
 
+def _replay_ws(dev, nbytes):
+    ws = _WS.get(dev.index)
+    if ws is None or ws.numel() < nbytes:
+        _WS[dev.index] = None
+        ws = torch_empty_u8(nbytes, dev)
+        _WS[dev.index] = ws
+    return ws
+
+
+def torch_empty_u8(n, dev):
+    import torch
+    return torch.empty(max(256, int(n)), dtype=torch.uint8, device=dev)
+
+
+def replay_columns(t, src, sink, eid=None, df_off=None, src_id=0, end_time=0.0, Ks=(1,)):
+    """rq_metrics_replay(_batch) on device columns (torch tensors: t f64, src / sink /
+    event_id i64, df_off i64 [n_df + 1] or None for one dataframe).  Sink ids are raw:
+    the pivot columns are built on the device.  Returns (metrics [n_df, nK + 2],
+    counts [n_df, 4]) device tensors; counts[:, 2] < 0 flags a rejected dataframe
+    (RQ_EUNSORTED).  Dataframes wider than the LDS tables are rerun with the large
+    workspace, as the engine reruns overflowing replicas."""
+    import torch
+    from . import _lib as L
+    dev = t.device
+    n = int(t.numel())
+    n_df = 1 if df_off is None else int(df_off.numel()) - 1
+    Ks = np.ascontiguousarray(Ks, dtype=np.int32)
+    out = torch.empty((n_df, Ks.size + 2), dtype=torch.float64, device=dev)
+    cnt = torch.empty((n_df, 4), dtype=torch.int64, device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+    lib = L.lib()
+    for flags in (0, L.REPLAY_LARGE):
+        nbytes = C.c_size_t()
+        L.check("rq_replay_workspace_size",
+                lib.rq_replay_workspace_size(n, n_df, Ks.size, flags, C.byref(nbytes)))
+        ws = _replay_ws(dev, nbytes.value)
+        ptr = lambda x: x.data_ptr() if x is not None and x.numel() else None  # noqa: E731
+        args = (ptr(t), ptr(src), ptr(sink), ptr(eid))
+        tail = (int(src_id), float(end_time), Ks.ctypes.data_as(L._pi32), Ks.size,
+                out.data_ptr(), cnt.data_ptr(), ws.data_ptr(), ws.numel(), st)
+        if df_off is None:
+            L.check("rq_metrics_replay", lib.rq_metrics_replay(*args, n, *tail))
+        else:
+            L.check("rq_metrics_replay_batch",
+                    lib.rq_metrics_replay_batch(*args, df_off.data_ptr(), n_df, n, *tail))
+        if flags or not bool((cnt[:, 2] == L.RQ_EOVERFLOW).any().item()):
+            break
+    return out, cnt
+
+
 def replay_metrics(df, src_id, end_time, Ks=(1,)):
     """All metrics of one df in one GPU pass.  Returns dict with top_k (list),
     avg_rank, r_2, num_own, num_world, rows, cols."""
@@ -53,39 +104,46 @@ def replay_metrics(df, src_id, end_time, Ks=(1,)):
     if len(df) == 0:
         raise KeyError("empty dataframe")   # the reference fails on an empty df too
     dev = torch.device("cuda", torch.cuda.current_device())
-    t = np.ascontiguousarray(df["t"].values, dtype=np.float64)
-    src = np.ascontiguousarray(df["src_id"].values, dtype=np.int64)
-    sinks, col = np.unique(df["sink_id"].values, return_inverse=True)
-    col = np.ascontiguousarray(col, dtype=np.int32)
-    eid = np.ascontiguousarray(df["event_id"].values, dtype=np.int64) \
-        if "event_id" in df.columns else None
-    n, S = t.size, int(sinks.size)
-    Ks = np.ascontiguousarray(Ks, dtype=np.int32)
-    nbytes = C.c_size_t()
-    L.check("rq_replay_workspace_size", L.lib().rq_replay_workspace_size(n, S, C.byref(nbytes)))
-    ws = _WS.get(dev.index)
-    if ws is None or ws.numel() < nbytes.value:
-        ws = torch.empty(nbytes.value, dtype=torch.uint8, device=dev)
-        _WS[dev.index] = ws
-    tt = torch.from_numpy(t).to(dev)
-    ts = torch.from_numpy(src).to(dev)
-    tc = torch.from_numpy(col).to(dev)
-    te = torch.from_numpy(eid).to(dev) if eid is not None else None
-    out = torch.empty(Ks.size + 2, dtype=torch.float64, device=dev)
-    cnt = torch.empty(4, dtype=torch.int64, device=dev)
-    st = torch.cuda.current_stream().cuda_stream
-    L.check("rq_metrics_replay", L.lib().rq_metrics_replay(
-        tt.data_ptr(), ts.data_ptr(), tc.data_ptr(), te.data_ptr() if te is not None else None,
-        n, S, int(src_id), float(end_time), Ks.ctypes.data_as(L._pi32), Ks.size,
-        out.data_ptr(), cnt.data_ptr(), ws.data_ptr(), ws.numel(), st))
-    o = out.cpu().numpy()
-    c = cnt.cpu().numpy()
-    if c[2] < 0:
+
+    def col(name):
+        return torch.from_numpy(np.ascontiguousarray(df[name].values, dtype=np.int64)).to(dev)
+    tt = torch.from_numpy(np.ascontiguousarray(df["t"].values, dtype=np.float64)).to(dev)
+    te = col("event_id") if "event_id" in df.columns else None
+    o, c = replay_columns(tt, col("src_id"), col("sink_id"), te, None, src_id, end_time, Ks)
+    o = o[0].cpu().numpy()
+    c = c[0].cpu().numpy()
+    nK = len(Ks)
+    if c[2] == L.RQ_EUNSORTED:
         raise L.RQError("rq_metrics_replay (df 't' column must be non-decreasing)",
                         L.RQ_EUNSORTED)
-    return {"top_k": [np.float64(v) for v in o[:Ks.size]], "avg_rank": np.float64(o[Ks.size]),
-            "r_2": np.float64(o[Ks.size + 1]), "num_own": int(c[0]), "num_world": int(c[1]),
+    if c[2] < 0:
+        raise L.RQError("rq_metrics_replay", int(c[2]))
+    return {"top_k": [np.float64(v) for v in o[:nK]], "avg_rank": np.float64(o[nK]),
+            "r_2": np.float64(o[nK + 1]), "num_own": int(c[0]), "num_world": int(c[1]),
             "rows": int(c[2]), "cols": int(c[3])}
+
+
+def replay_frames(dfs, src_id, end_time, Ks=(1,)):
+    """Metrics of many dataframes (the reference's per-replica utils calls) in one
+    batched replay: a pandas DataFrame with top_K..., avg_rank, r_2, num_events,
+    world_events per input df."""
+    import pandas as pd
+    import torch
+    dev = torch.device("cuda", torch.cuda.current_device())
+    lens = np.asarray([len(d) for d in dfs], dtype=np.int64)
+    off = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)])).to(dev)
+
+    def cat(name, dt):
+        return torch.from_numpy(np.ascontiguousarray(
+            np.concatenate([d[name].values for d in dfs]) if len(dfs) else np.zeros(0), dtype=dt)).to(dev)
+    eid = cat("event_id", np.int64) if all("event_id" in d.columns for d in dfs) else None
+    o, c = replay_columns(cat("t", np.float64), cat("src_id", np.int64), cat("sink_id", np.int64),
+                          eid, off, src_id, end_time, Ks)
+    o, c = o.cpu().numpy(), c.cpu().numpy()
+    res = {("top_" + str(k)): o[:, i] for i, k in enumerate(Ks)}
+    res.update(avg_rank=o[:, len(Ks)], r_2=o[:, len(Ks) + 1], num_events=c[:, 0],
+               world_events=c[:, 1], pivot_rows=c[:, 2], sinks=c[:, 3])
+    return pd.DataFrame(res)
 
 
 def time_in_top_k(df, K, src_id=None, end_time=None, sim_opts=None):

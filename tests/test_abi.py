@@ -28,7 +28,7 @@ def test_exports_every_declared_symbol():
 
 def test_version_and_errors():
     lib = L.lib()
-    assert lib.rq_abi_version() == L.ABI_VERSION == 2
+    assert lib.rq_abi_version() == L.ABI_VERSION == 3
     assert lib.rq_strerror(L.RQ_EINVAL) == b"invalid argument"
     assert lib.rq_strerror(-99) == b"unknown error"
 
@@ -86,8 +86,21 @@ def test_workspace_queries_validate():
     lib = L.lib()
     n = C.c_size_t()
     assert lib.rq_workspace_size(None, None, C.byref(n)) == L.RQ_EINVAL
-    assert lib.rq_replay_workspace_size(100, 3, C.byref(n)) == 0 and n.value > 100 * 24
-    assert lib.rq_replay_workspace_size(0, 3, C.byref(n)) == L.RQ_EINVAL
+    assert lib.rq_replay_workspace_size(100, 1, 1, 0, C.byref(n)) == 0 and n.value >= 100 * 32
+    small = n.value
+    assert lib.rq_replay_workspace_size(100, 1, 1, L.REPLAY_LARGE, C.byref(n)) == 0
+    assert n.value >= small + 100 * 96
+    assert lib.rq_replay_workspace_size(-1, 1, 1, 0, C.byref(n)) == L.RQ_EINVAL
+    assert lib.rq_replay_workspace_size(10, 0, 1, 0, C.byref(n)) == L.RQ_EINVAL
+    assert lib.rq_replay_workspace_size(10, 1, 5, 0, C.byref(n)) == L.RQ_EINVAL
     k = np.asarray([1], dtype=np.int32)
-    assert lib.rq_metrics_replay(None, None, None, None, 10, 1, 1, 1.0, k.ctypes.data_as(L._pi32),
+    # argument validation happens before any HIP call
+    assert lib.rq_metrics_replay(None, None, None, None, 10, 1, 1.0, k.ctypes.data_as(L._pi32),
                                  1, None, None, None, 0, None) == L.RQ_EINVAL
+    assert lib.rq_metrics_replay_batch(None, None, None, None, None, 2, 10, 1, 1.0,
+                                       k.ctypes.data_as(L._pi32), 1, None, None, None, 0,
+                                       None) == L.RQ_EINVAL
+    k0 = np.asarray([0], dtype=np.int32)   # K >= 1 (time_in_top_k compares r <= K - 1)
+    buf = (C.c_char * 4096)()
+    assert lib.rq_metrics_replay(None, None, None, None, 0, 1, 1.0, k0.ctypes.data_as(L._pi32),
+                                 1, buf, buf, buf, 4096, None) == L.RQ_EINVAL
