@@ -152,7 +152,8 @@ def test_wide_dataframes_global_tables(dup_p, tie_p):
     workspace (global hash tables; the fallback's per-sink state in HBM)."""
     torch, O, L, U = _ctx()
     rs = np.random.RandomState(5 + int(dup_p * 100))
-    sinks = rs.choice(10 ** 12, 6000, replace=False).astype(np.int64) - 5 * 10 ** 11
+    sinks = np.unique(rs.randint(-5 * 10 ** 11, 5 * 10 ** 11, 6100, dtype=np.int64))[:6000]
+    rs.shuffle(sinks)
     df = _random_df(rs, 1500, sinks, dup_p, tie_p)
     end = float(df.t.max()) + 0.25
     exp, cnt = _oracle_met(O, df, 1, end)
