@@ -5,7 +5,8 @@
   * rq_log_rows + rq_log_expand: State.get_dataframe rows for a whole batch,
     12 B read per event + 40 B written per (event, sink) row
   * rq_scan: 24 B read per pivot row (timed inside the plain C3 run)
-  * rq_metrics_replay on a reference-layout df: 28 B read per df row
+  * rq_metrics_replay_batch on the 256 exported C3 dataframes (24 B read per df row,
+    32 B with event ids) and rq_metrics_replay on one df through the pandas facade
   * rq_oracle_dp: n = 8000 walls, 64 instances
 Per-kernel times come from the library's HIP events (rq_timing) on the launch stream.
 usage: python scripts/bench_paths.py [--reps N]
@@ -84,11 +85,24 @@ def main():
     res["scan"] = {"replicas": R3, "rows": rows3, "ms": ms[2], "bytes": 24 * rows3,
                    "GBps": 24 * rows3 / ms[2] / 1e6, "frac": 24 * rows3 / ms[2] / 1e6 / PEAK}
 
-    # 4. replay of one reference-layout df (~7e5 rows)
+    # 4. replay (rq_metrics_replay_batch, raw sink ids): the 256 exported C3 dataframes
+    #    as one batch (24 B read per df row: t, src_id, sink_id; +8 B with event ids),
+    #    and one dataframe through the pandas facade (host -> device copies included)
+    off = torch.from_numpy(ro).cuda()
+    for tag, eid in (("replay_batch", None), ("replay_batch_eid", cols["event_id"])):
+        (m4, c4), ms, wall = timed(lambda: utils.replay_columns(
+            cols["t"], cols["src_id"], cols["sink_id"], eid, off, so["src_id"], so["end_time"],
+            (1,)), a.reps)
+        per_row = 24 + (8 if eid is not None else 0)
+        res[tag] = {"dataframes": R2, "rows": nrow, "ms_fast": ms[3], "ms_scan": ms[2],
+                    "wall_ms": wall * 1e3, "bytes": per_row * nrow,
+                    "GBps": per_row * nrow / (ms[3] + ms[2]) / 1e6,
+                    "frac": per_row * nrow / (ms[3] + ms[2]) / 1e6 / PEAK,
+                    "equal_to_sweep": bool(torch.equal(m4, r2.metrics))}
     df = r2.dataframe(0)
     _, ms, wall = timed(lambda: utils.replay_metrics(df, so["src_id"], so["end_time"], (1,)), a.reps)
-    res["replay"] = {"rows": len(df), "ms": ms[3] + ms[2], "wall_ms": wall * 1e3,
-                     "GBps": 28 * len(df) / (ms[3] + ms[2]) / 1e6}
+    res["replay_one_df"] = {"rows": len(df), "ms": ms[3] + ms[2], "wall_ms": wall * 1e3,
+                            "GBps": 32 * len(df) / (ms[3] + ms[2]) / 1e6}
 
     # 5. oracle DP
     rs = np.random.RandomState(0)
