@@ -263,27 +263,58 @@ __global__ __launch_bounds__(RP_B) void rq_rp_fast(RpArgs a)
     carry.v = 0;
 #pragma unroll
     for (int q = 0; q < NK; ++q) carry.c[q] = 0;
-    double tprev = 0.0;
-    int64_t eprev = 0;
     bool aborted = false;
 
-    // prefetched row of this thread
-    int64_t i = r0 + tid;
-    double ti = 0.0;
-    int64_t si = 0, ki = 0, ei = 0;
-    if (i < r1) {
-        ti = a.t[i];
-        si = a.src[i];
-        ki = a.sink[i];
-        if (has_eid) ei = a.eid[i];
+    // A batch's rows reach the workgroup through LDS: the loads for batch b + 1 are
+    // issued at the top of batch b and consumed only after batch b's sort (prep),
+    // so they are in flight across its barriers and nothing loaded is carried over
+    // the loop's back edge (the waitcnt pass would otherwise wait for them early).
+    //   tb[0] = t of the previous batch's last row, tb[1 + i] = row i, tb[RP_B + 1] =
+    //   t of the first row of the following batch; eb likewise for event ids.
+    bool own_c = false;       // this thread's row of the current batch: own post?
+    uint32_t slot_c = 0;      // ... its sink's slot
+    auto prep = [&](int64_t nb0, double t_, int64_t s_, int64_t k_, int64_t e_, double t_after,
+                    double t_before, int64_t e_before) {
+        const bool v = nb0 + tid < r1;
+        tb[1 + tid] = v ? t_ : 0.0;
+        if (has_eid) eb[1 + tid] = e_;
+        if (tid == 0) {
+            tb[0] = t_before;
+            eb[0] = e_before;
+            tb[RP_B + 1] = t_after;
+        }
+        own_c = v && s_ == a.src_id;
+        slot_c = 0;
+        if (v) {
+            if ((uint64_t)k_ == RP_EMPTY_KEY) {
+                slot_c = (uint32_t)tcap;   // the sentinel id's own slot
+                if (misc[1] == 0 && atomicExch(&misc[1], 1) == 0) atomicAdd(&misc[0], 1);
+            } else {
+                slot_c = rp_insert(tkeys, tmask, tbits, (uint64_t)k_, &misc[0]);
+            }
+        }
+    };
+    {
+        const int64_t i0 = r0 + tid;
+        double t0 = 0.0, ta = 0.0;
+        int64_t s0 = 0, k0 = 0, e0 = 0;
+        if (i0 < r1) {
+            t0 = a.t[i0];
+            s0 = a.src[i0];
+            k0 = a.sink[i0];
+            if (has_eid) e0 = a.eid[i0];
+        }
+        if (tid == 0 && r0 + RP_B < r1) ta = a.t[r0 + RP_B];
+        prep(r0, t0, s0, k0, e0, ta, 0.0, 0);
     }
 
     for (int64_t b0 = r0; b0 < r1; b0 += RP_B) {
-        i = b0 + tid;
+        const int64_t i = b0 + tid;
         const bool valid = i < r1;
+        const bool has_next = b0 + RP_B < r1;
         // next batch (in flight across this batch's barriers)
         const int64_t in = i + RP_B;
-        double tn = 0.0;
+        double tn = 0.0, tnn = 0.0;
         int64_t sn = 0, kn = 0, en = 0;
         if (in < r1) {
             tn = a.t[in];
@@ -291,34 +322,24 @@ __global__ __launch_bounds__(RP_B) void rq_rp_fast(RpArgs a)
             kn = a.sink[in];
             if (has_eid) en = a.eid[in];
         }
+        if (tid == 0 && b0 + 2 * RP_B < r1) tnn = a.t[b0 + 2 * RP_B];
 
-        // ---- A: neighbours of every row; dense sink slots ----
-        tb[1 + tid] = valid ? ti : 0.0;
-        if (has_eid) eb[1 + tid] = ei;
-        if (tid == 0) {
-            tb[0] = tprev;
-            eb[0] = eprev;
-            tb[RP_B + 1] = tn;   // row b0 + RP_B (meaningful only if it exists)
-        }
-        uint32_t slot = 0;
-        if (valid) {
-            if ((uint64_t)ki == RP_EMPTY_KEY) {
-                slot = (uint32_t)tcap;   // the sentinel id's own slot
-                if (misc[1] == 0 && atomicExch(&misc[1], 1) == 0) atomicAdd(&misc[0], 1);
-            } else {
-                slot = rp_insert(tkeys, tmask, tbits, (uint64_t)ki, &misc[0]);
-            }
-        }
+        // ---- A: neighbours of every row ----
         __syncthreads();
+        const int last = (int)((r1 - b0) < RP_B ? (r1 - b0) : RP_B);
+        const double ti = tb[1 + tid];
         const double t_prev = tb[tid], t_next = tb[tid + 2];
+        const double t_last = tb[last];
+        const int64_t e_last = has_eid ? eb[last] : 0;
         const bool first_row = i == r0;
         const bool start = valid && (first_row || ti != t_prev);
         const bool endg = valid && (i == r1 - 1 || t_next != ti);
-        const bool own = valid && si == a.src_id;
+        const bool own = own_c;
+        const uint32_t slot = slot_c;
         if (valid && !first_row && ti < t_prev) misc[3] = 1;
         int ev_own = 0, ev_world = 0;
         if (has_eid && valid) {
-            const int64_t e_prev = eb[tid];
+            const int64_t ei = eb[1 + tid], e_prev = eb[tid];
             const bool fe = first_row || ei != e_prev;
             if (!first_row && ei < e_prev) misc[4] = 1;
             ev_own = fe && own;
@@ -400,6 +421,9 @@ __global__ __launch_bounds__(RP_B) void rq_rp_fast(RpArgs a)
         }
         __syncthreads();
 
+        // the next batch's rows (their loads have landed by now) into LDS, sinks hashed
+        if (has_next) prep(b0 + RP_B, tn, sn, kn, en, tnn, t_last, e_last);
+
         // ---- D: running totals in row order; the last row of a t-group emits its pivot row ----
         RpAcc<NK> x;
         x.s = cs[tid];
@@ -436,18 +460,10 @@ __global__ __launch_bounds__(RP_B) void rq_rp_fast(RpArgs a)
         for (int q = 0; q < NK; ++q) carry.c[q] += tot.c[q];
         Gc += st_tot;
         if (tid == 0) {
-            misc[5] += (int)n_ev_own;
-            misc[6] += (int)n_ev_world;
+            misc[5] += n_ev_own;
+            misc[6] += n_ev_world;
         }
-        const int last = (int)((r1 - b0) < RP_B ? (r1 - b0) : RP_B);
-        tprev = tb[last];
-        if (has_eid) eprev = eb[last];
-        ti = tn;
-        si = sn;
-        ki = kn;
-        ei = en;
-        __syncthreads();   // tb / eb / wsum are rewritten by the next batch
-        if (misc[3]) break;   // unsorted: the dataframe is rejected
+        if (misc[3]) break;   // unsorted (set in A, read after barriers): the df is rejected
     }
 
     __syncthreads();
