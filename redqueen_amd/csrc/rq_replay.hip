@@ -99,54 +99,120 @@ __device__ __forceinline__ int rp_gbits(int64_t n)
     return b;
 }
 
-// ---- block (1024-thread) scans: 16 wave totals through LDS, one barrier ----
-template <class T>
-__device__ __forceinline__ T wave_incl_add(T v)
+// ---- wave scans on DPP (VALU latency; ds_bpermute shuffles cost ~100 cycles a step
+// and these chains are the batch's critical path) ----
+__device__ __forceinline__ uint32_t umax32(uint32_t a, uint32_t b) { return a > b ? a : b; }
+// inclusive 64-lane sum of 32-bit values (two's complement wrap, so int works too)
+__device__ __forceinline__ int scan_add_i32(int v) { return (int)wave_scan_add((uint32_t)v); }
+// inclusive 64-lane max of NON-NEGATIVE values (lanes outside a DPP row read 0)
+__device__ __forceinline__ int scan_max_nn(int v)
 {
-    const int lane = lane_id();
+    uint32_t x = (uint32_t)v;
+    x = umax32(x, dpp0<0x111, 0xF>(x));
+    x = umax32(x, dpp0<0x112, 0xF>(x));
+    x = umax32(x, dpp0<0x114, 0xF>(x));
+    x = umax32(x, dpp0<0x118, 0xF>(x));
+    x = umax32(x, dpp0<0x142, 0xA>(x));
+    x = umax32(x, dpp0<0x143, 0xC>(x));
+    return (int)x;
+}
+// inclusive 64-lane sum of int32 values as int64 (16-bit halves scanned apart: exact)
+__device__ __forceinline__ int64_t scan_add_i64_of_i32(int v)
+{
+    const int hi = scan_add_i32(v >> 16);
+    const int lo = scan_add_i32(v & 0xFFFF);
+    return (int64_t)hi * 65536 + (int64_t)lo;
+}
+// 16-lane (row 0) inclusive scans of the wave totals
+__device__ __forceinline__ int row_scan_add(int v)
+{
+    uint32_t x = (uint32_t)v;
+    x += dpp0<0x111, 0xF>(x);
+    x += dpp0<0x112, 0xF>(x);
+    x += dpp0<0x114, 0xF>(x);
+    x += dpp0<0x118, 0xF>(x);
+    return (int)x;
+}
+__device__ __forceinline__ int64_t row_scan_add(int64_t v)
+{
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const T u = __shfl_up(v, o, 64);
-        if (lane >= o) v += u;
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t lo = (uint32_t)v, hi = (uint32_t)((uint64_t)v >> 32);
+        uint32_t plo, phi;
+        switch (k) {
+        case 0: plo = dpp0<0x111, 0xF>(lo); phi = dpp0<0x111, 0xF>(hi); break;
+        case 1: plo = dpp0<0x112, 0xF>(lo); phi = dpp0<0x112, 0xF>(hi); break;
+        case 2: plo = dpp0<0x114, 0xF>(lo); phi = dpp0<0x114, 0xF>(hi); break;
+        default: plo = dpp0<0x118, 0xF>(lo); phi = dpp0<0x118, 0xF>(hi); break;
+        }
+        v += (int64_t)(((uint64_t)phi << 32) | plo);
     }
     return v;
 }
-template <class T>
-__device__ __forceinline__ T wave_incl_max(T v)
+__device__ __forceinline__ int row_scan_max_nn(int v)
 {
-    const int lane = lane_id();
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const T u = __shfl_up(v, o, 64);
-        if (lane >= o) v = v > u ? v : u;
-    }
-    return v;
+    uint32_t x = (uint32_t)v;
+    x = umax32(x, dpp0<0x111, 0xF>(x));
+    x = umax32(x, dpp0<0x112, 0xF>(x));
+    x = umax32(x, dpp0<0x114, 0xF>(x));
+    x = umax32(x, dpp0<0x118, 0xF>(x));
+    return (int)x;
 }
 
 __device__ __forceinline__ int lane_bcast(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 __device__ __forceinline__ int64_t lane_bcast(int64_t v, int l) { return bcast_i64(v, l); }
 
 // the 16 wave totals t[0..16) (LDS) of a block scan -> this wave's exclusive
-// prefix and the block total; lanes 0-15 scan them (w: this wave, uniform)
+// prefix and the block total (w: this wave, uniform)
 template <class T>
 __device__ __forceinline__ void totals_add(const T* t, int w, T& pre, T& tot)
 {
     T x = lane_id() < 16 ? t[lane_id()] : (T)0;
-    x = wave_incl_add(x);
+    x = row_scan_add(x);
     tot = lane_bcast(x, 15);
     pre = w > 0 ? lane_bcast(x, w - 1) : (T)0;
 }
-template <class T>
-__device__ __forceinline__ T totals_max(const T* t, int w, T ident)
+// exclusive max-prefix of non-negative wave totals
+__device__ __forceinline__ int totals_max_nn(const int* t, int w)
 {
-    T x = lane_id() < 16 ? t[lane_id()] : ident;
-    x = wave_incl_max(x);
-    return w > 0 ? lane_bcast(x, w - 1) : ident;
+    int x = lane_id() < 16 ? t[lane_id()] : 0;
+    x = row_scan_max_nn(x);
+    return w > 0 ? lane_bcast(x, w - 1) : 0;
+}
+
+// partner value at lane ^ J for J < 16, on DPP
+template <int J>
+__device__ __forceinline__ uint32_t xlane_u32(uint32_t v)
+{
+    if constexpr (J == 1) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+    if constexpr (J == 2) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+    if constexpr (J == 8) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);
+    if constexpr (J == 4) {
+        const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x12C, 0xF, 0xF, false);  // lane + 4
+        const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false);  // lane - 4
+        return (lane_id() & 4) ? dn : up;
+    }
+    return v;
+}
+template <int J>
+__device__ __forceinline__ uint32_t xlane(uint32_t v) { return xlane_u32<J>(v); }
+template <int J>
+__device__ __forceinline__ uint64_t xlane(uint64_t v)
+{
+    return ((uint64_t)xlane_u32<J>((uint32_t)(v >> 32)) << 32) | xlane_u32<J>((uint32_t)v);
+}
+
+template <class K>
+__device__ __forceinline__ K cmpx(K key, K other, int tid, int k, int j)
+{
+    const bool up = (tid & k) == 0;
+    const bool lower = (tid & j) == 0;
+    return (lower == up) ? (key < other ? key : other) : (key < other ? other : key);
 }
 
 // bitonic sort of one key per thread (ascending over threadIdx.x).  Partners
-// below 64 lanes apart exchange by shuffles; farther ones through LDS
-// (double-buffered, so one barrier per stage).
+// 1-8 lanes apart exchange on DPP, 16-32 apart by shuffles, farther ones
+// through LDS (double-buffered, so one barrier per stage).
 template <class K>
 __device__ __forceinline__ K bitonic_block(K key, K* buf /* [2][RP_B] */)
 {
@@ -155,7 +221,7 @@ __device__ __forceinline__ K bitonic_block(K key, K* buf /* [2][RP_B] */)
 #pragma unroll 1
     for (int k = 2; k <= RP_B; k <<= 1) {
 #pragma unroll 1
-        for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int j = k >> 1; j >= 16; j >>= 1) {
             K other;
             if (j >= 64) {
                 K* b = buf + par * RP_B;
@@ -166,11 +232,12 @@ __device__ __forceinline__ K bitonic_block(K key, K* buf /* [2][RP_B] */)
             } else {
                 other = __shfl_xor(key, j, 64);
             }
-            const bool up = (tid & k) == 0;
-            const bool lower = (tid & j) == 0;
-            const bool take_min = lower == up;
-            key = take_min ? (key < other ? key : other) : (key < other ? other : key);
+            key = cmpx(key, other, tid, k, j);
         }
+        if (k >= 16) key = cmpx(key, xlane<8>(key), tid, k, 8);
+        if (k >= 8) key = cmpx(key, xlane<4>(key), tid, k, 4);
+        if (k >= 4) key = cmpx(key, xlane<2>(key), tid, k, 2);
+        key = cmpx(key, xlane<1>(key), tid, k, 1);
     }
     return key;
 }
@@ -348,7 +415,7 @@ __global__ __launch_bounds__(RP_B) void rq_rp_fast(RpArgs a)
         if (!GLOBAL && misc[0] > RP_HMAX) aborted = true;   // uniform: read after the barrier
 
         // ---- B: t-group of every row (block scan of group starts) + event counts ----
-        const int st_incl = wave_incl_add((int)start);
+        const int st_incl = scan_add_i32((int)start);
         const uint64_t bo = __ballot(ev_own), bw = __ballot(ev_world);
         if (lane == 63) {
             ws32[w] = st_incl;
@@ -381,17 +448,17 @@ __global__ __launch_bounds__(RP_B) void rq_rp_fast(RpArgs a)
         const bool ownp = vp && ob[idx];
         const int Gp = vp ? gb[idx] : 0;
         // segment start and the latest own row at or before p: block max-scans
-        int ss = wave_incl_max(head ? tid : 0);
-        int lo = wave_incl_max(ownp ? tid : -1);
+        int ss = scan_max_nn(head ? tid : 0);
+        int lo = scan_max_nn(ownp ? tid + 1 : 0);   // +1: non-negative, 0 = none
         if (lane == 63) {
             ws32[48 + w] = ss;
             ws32[64 + w] = lo;
         }
         __syncthreads();
         {
-            const int p1 = totals_max(ws32 + 48, w, 0), p2 = totals_max(ws32 + 64, w, -1);
+            const int p1 = totals_max_nn(ws32 + 48, w), p2 = totals_max_nn(ws32 + 64, w);
             ss = ss > p1 ? ss : p1;
-            lo = lo > p2 ? lo : p2;
+            lo = (lo > p2 ? lo : p2) - 1;
         }
         RpSlot st = RpSlot{0, 0, -1, -1};
         if (vp) st = tst[slp];
@@ -426,14 +493,10 @@ __global__ __launch_bounds__(RP_B) void rq_rp_fast(RpArgs a)
 
         // ---- D: running totals in row order; the last row of a t-group emits its pivot row ----
         RpAcc<NK> x;
-        x.s = cs[tid];
-        x.v = cv[tid];
+        x.s = scan_add_i64_of_i32(cs[tid]);
+        x.v = scan_add_i32(cv[tid]);
 #pragma unroll
-        for (int q = 0; q < NK; ++q) x.c[q] = cc[q * RP_B + tid];
-        x.s = wave_incl_add(x.s);
-        x.v = wave_incl_add(x.v);
-#pragma unroll
-        for (int q = 0; q < NK; ++q) x.c[q] = wave_incl_add(x.c[q]);
+        for (int q = 0; q < NK; ++q) x.c[q] = scan_add_i32(cc[q * RP_B + tid]);
         if (lane == 63) {
             wsum[w] = x.s;
             ws32[80 + w] = x.v;
