@@ -55,10 +55,10 @@ constexpr int RP_HMAX = RP_H - RP_B - 1;   // unique sinks the LDS table takes: 
 constexpr uint64_t RP_EMPTY_KEY = 0x8000000000000000ull;   // INT64_MIN: gets its own slot
 
 struct alignas(16) RpSlot {
-    int cnt;        // rows of this sink so far (pos of its last row)
-    int lastown;    // pos of its latest own row (0: none)
-    int prevrank;   // rank of its last row (-1: no row yet, the pivot cell is NaN)
+    int cnt;        // rows of this sink so far (pos of its last row; 0: none yet, cell NaN)
+    int lastown;    // pos of its latest own row (0: none); its last row's rank = cnt - lastown
     int lastgroup;  // t-group of its last row (-1: none)
+    int bucket;     // this batch: rows of the sink (bits 0-11), list offset (bits 12-22)
 };
 
 __device__ __forceinline__ uint32_t rp_hash(uint64_t k, int bits)
@@ -180,68 +180,6 @@ __device__ __forceinline__ int totals_max_nn(const int* t, int w)
     return w > 0 ? lane_bcast(x, w - 1) : 0;
 }
 
-// partner value at lane ^ J for J < 16, on DPP
-template <int J>
-__device__ __forceinline__ uint32_t xlane_u32(uint32_t v)
-{
-    if constexpr (J == 1) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
-    if constexpr (J == 2) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
-    if constexpr (J == 8) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);
-    if constexpr (J == 4) {
-        const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x12C, 0xF, 0xF, false);  // lane + 4
-        const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false);  // lane - 4
-        return (lane_id() & 4) ? dn : up;
-    }
-    return v;
-}
-template <int J>
-__device__ __forceinline__ uint32_t xlane(uint32_t v) { return xlane_u32<J>(v); }
-template <int J>
-__device__ __forceinline__ uint64_t xlane(uint64_t v)
-{
-    return ((uint64_t)xlane_u32<J>((uint32_t)(v >> 32)) << 32) | xlane_u32<J>((uint32_t)v);
-}
-
-template <class K>
-__device__ __forceinline__ K cmpx(K key, K other, int tid, int k, int j)
-{
-    const bool up = (tid & k) == 0;
-    const bool lower = (tid & j) == 0;
-    return (lower == up) ? (key < other ? key : other) : (key < other ? other : key);
-}
-
-// bitonic sort of one key per thread (ascending over threadIdx.x).  Partners
-// 1-8 lanes apart exchange on DPP, 16-32 apart by shuffles, farther ones
-// through LDS (double-buffered, so one barrier per stage).
-template <class K>
-__device__ __forceinline__ K bitonic_block(K key, K* buf /* [2][RP_B] */)
-{
-    const int tid = threadIdx.x;
-    int par = 0;
-#pragma unroll 1
-    for (int k = 2; k <= RP_B; k <<= 1) {
-#pragma unroll 1
-        for (int j = k >> 1; j >= 16; j >>= 1) {
-            K other;
-            if (j >= 64) {
-                K* b = buf + par * RP_B;
-                b[tid] = key;
-                __syncthreads();
-                other = b[tid ^ j];
-                par ^= 1;
-            } else {
-                other = __shfl_xor(key, j, 64);
-            }
-            key = cmpx(key, other, tid, k, j);
-        }
-        if (k >= 16) key = cmpx(key, xlane<8>(key), tid, k, 8);
-        if (k >= 8) key = cmpx(key, xlane<4>(key), tid, k, 4);
-        if (k >= 4) key = cmpx(key, xlane<2>(key), tid, k, 2);
-        key = cmpx(key, xlane<1>(key), tid, k, 1);
-    }
-    return key;
-}
-
 template <int NK>
 struct RpAcc {
     int64_t s;      // sum of the (integral) forward-filled pivot cells
@@ -257,8 +195,6 @@ struct RpAcc {
 template <int NK, bool GLOBAL>
 __global__ __launch_bounds__(RP_B) void rq_rp_fast(RpArgs a)
 {
-    using Key = typename std::conditional<GLOBAL, uint64_t, uint32_t>::type;
-    constexpr Key KNONE = ~(Key)0;
     const int64_t d = blockIdx.x;
     const int tid = threadIdx.x;
     const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -278,11 +214,7 @@ __global__ __launch_bounds__(RP_B) void rq_rp_fast(RpArgs a)
     int64_t* eb = reinterpret_cast<int64_t*>(carve(8 * (RP_B + 1)));     // [0] prev eid, [1+i]
     int* gb = reinterpret_cast<int*>(carve(4 * RP_B));                    // t-group of row i
     unsigned char* ob = carve(RP_B);                                      // own flag of row i
-    Key* sk = reinterpret_cast<Key*>(carve(sizeof(Key) * 2 * RP_B));     // bitonic buffers / sorted keys
-    int* rk = reinterpret_cast<int*>(carve(4 * RP_B));                    // rank by sorted position
-    int* cs = reinterpret_cast<int*>(carve(4 * RP_B));                    // cell change (row order)
-    int* cv = reinterpret_cast<int*>(carve(4 * RP_B));                    // NaN -> value
-    int* cc = reinterpret_cast<int*>(carve(4 * RP_B * NK));               // <= K-1 change, [q][row]
+    int* lst = reinterpret_cast<int*>(carve(4 * RP_B));                   // sink buckets: rows
     int64_t* wsum = reinterpret_cast<int64_t*>(carve(8 * 16));            // wave totals (int64)
     int* ws32 = reinterpret_cast<int*>(carve(4 * 16 * (NK + 6)));         // wave totals (int)
     int* misc = reinterpret_cast<int*>(carve(4 * 16));                    // flags, counters
@@ -304,12 +236,12 @@ __global__ __launch_bounds__(RP_B) void rq_rp_fast(RpArgs a)
     }
     tmask = (uint32_t)(tcap - 1);
     // misc: [0] unique sinks, [1] sentinel-key seen, [2] dup, [3] unsorted, [4] eid bad,
-    //       [5] own events, [6] world events, [7] key dump cursor
+    //       [5] own events, [6] world events, [7] key dump cursor, [8] bucket allocator
     if (tid < 16) misc[tid] = 0;
     if (!GLOBAL && tid == 0) inf->flags = 0;   // this call's status (the LDS pass runs first)
     for (int64_t h = tid; h <= tcap; h += RP_B) {
         tkeys[h] = RP_EMPTY_KEY;
-        tst[h] = RpSlot{0, 0, -1, -1};
+        tst[h] = RpSlot{0, 0, -1, 0};
     }
     if (GLOBAL && 2 * nd > tcap) {   // > 2^23 unique sinks possible: not supported
         if (tid == 0) atomicOr(&inf->flags, RP_BIG);
@@ -317,6 +249,14 @@ __global__ __launch_bounds__(RP_B) void rq_rp_fast(RpArgs a)
     }
     if (GLOBAL) __threadfence();   // the table's reset reaches L2 before the atomics below
     __syncthreads();
+
+    // the bucket word of a sink: LDS atomics, or (global table) atomics at L2 for every
+    // access -- the CU's L1 may hold a stale copy of a line an atomic changed
+    auto bk_add = [&](RpSlot* p) { return atomicAdd(&p->bucket, 1); };
+    auto bk_read = [&](RpSlot* p) { return GLOBAL ? atomicOr(&p->bucket, 0) : p->bucket; };
+    auto bk_write = [&](RpSlot* p, int v) {
+        if (GLOBAL) atomicExch(&p->bucket, v); else p->bucket = v;
+    };
 
     int km1[NK];
 #pragma unroll
@@ -333,9 +273,9 @@ __global__ __launch_bounds__(RP_B) void rq_rp_fast(RpArgs a)
     bool aborted = false;
 
     // A batch's rows reach the workgroup through LDS: the loads for batch b + 1 are
-    // issued at the top of batch b and consumed only after batch b's sort (prep),
-    // so they are in flight across its barriers and nothing loaded is carried over
-    // the loop's back edge (the waitcnt pass would otherwise wait for them early).
+    // issued at the top of batch b and consumed only at its end (prep), so they are
+    // in flight across its barriers and nothing loaded is carried over the loop's
+    // back edge (the waitcnt pass would otherwise wait for them early).
     //   tb[0] = t of the previous batch's last row, tb[1 + i] = row i, tb[RP_B + 1] =
     //   t of the first row of the following batch; eb likewise for event ids.
     bool own_c = false;       // this thread's row of the current batch: own post?
@@ -391,7 +331,7 @@ __global__ __launch_bounds__(RP_B) void rq_rp_fast(RpArgs a)
         }
         if (tid == 0 && b0 + 2 * RP_B < r1) tnn = a.t[b0 + 2 * RP_B];
 
-        // ---- A: neighbours of every row ----
+        // ---- A: neighbours of every row; its ticket in its sink's bucket ----
         __syncthreads();
         const int last = (int)((r1 - b0) < RP_B ? (r1 - b0) : RP_B);
         const double ti = tb[1 + tid];
@@ -402,7 +342,9 @@ __global__ __launch_bounds__(RP_B) void rq_rp_fast(RpArgs a)
         const bool start = valid && (first_row || ti != t_prev);
         const bool endg = valid && (i == r1 - 1 || t_next != ti);
         const bool own = own_c;
-        const uint32_t slot = slot_c;
+        RpSlot* sl = tst + slot_c;
+        const int ticket = valid ? bk_add(sl) : 0;   // rows of this sink before me: unordered
+        ob[tid] = own ? 1 : 0;
         if (valid && !first_row && ti < t_prev) misc[3] = 1;
         int ev_own = 0, ev_world = 0;
         if (has_eid && valid) {
@@ -414,7 +356,8 @@ __global__ __launch_bounds__(RP_B) void rq_rp_fast(RpArgs a)
         }
         if (!GLOBAL && misc[0] > RP_HMAX) aborted = true;   // uniform: read after the barrier
 
-        // ---- B: t-group of every row (block scan of group starts) + event counts ----
+        // ---- B: t-group of every row (block scan of group starts) + event counts;
+        //      buckets of more than one row get list space ----
         const int st_incl = scan_add_i32((int)start);
         const uint64_t bo = __ballot(ev_own), bw = __ballot(ev_world);
         if (lane == 63) {
@@ -423,80 +366,94 @@ __global__ __launch_bounds__(RP_B) void rq_rp_fast(RpArgs a)
             ws32[32 + w] = popc(bw);
         }
         __syncthreads();
+        if (aborted) break;
         int st_pre, st_tot, n_ev_own, n_ev_world, dummy;
         totals_add(ws32, w, st_pre, st_tot);
         totals_add(ws32 + 16, w, dummy, n_ev_own);
         totals_add(ws32 + 32, w, dummy, n_ev_world);
         const int64_t G = Gc + (int64_t)(st_pre + st_incl) - 1;   // this row's t-group (pivot row index)
         gb[tid] = (int)G;
-        ob[tid] = own ? 1 : 0;
-        if (aborted) break;
+        const RpSlot st0 = valid ? *sl : RpSlot{0, 0, -1, 0};   // state before this batch
+        // rows of my sink in this batch (low bits: the ticket-0 row may already have
+        // added the list offset)
+        const int m = valid ? ((GLOBAL ? bk_read(sl) : st0.bucket) & 0xFFF) : 0;
+        if (valid && m > 1 && ticket == 0) bk_write(sl, (atomicAdd(&misc[8], m) << 12) | m);
+        __syncthreads();
 
-        // ---- C: sort (slot, row): a row's predecessor in its sink's feed ----
-        const Key key0 = valid ? (((Key)slot << RP_LOG_B) | (Key)tid) : KNONE;
-        const Key key = bitonic_block<Key>(key0, sk);   // sorted position p = tid
-        __syncthreads();
-        sk[tid] = key;
-        __syncthreads();
-        const Key keyp = tid > 0 ? sk[tid - 1] : KNONE;
-        const Key keyn = tid < RP_B - 1 ? sk[tid + 1] : KNONE;
-        const bool vp = key != KNONE;
-        const Key slp = key >> RP_LOG_B;
-        const int idx = (int)(key & (RP_B - 1));
-        const bool head = vp && (tid == 0 || (keyp >> RP_LOG_B) != slp);
-        const bool tail = vp && (tid == RP_B - 1 || (keyn >> RP_LOG_B) != slp);
-        const bool ownp = vp && ob[idx];
-        const int Gp = vp ? gb[idx] : 0;
-        // segment start and the latest own row at or before p: block max-scans
-        int ss = scan_max_nn(head ? tid : 0);
-        int lo = scan_max_nn(ownp ? tid + 1 : 0);   // +1: non-negative, 0 = none
-        if (lane == 63) {
-            ws32[48 + w] = ss;
-            ws32[64 + w] = lo;
+        // ---- C: my place among my sink's rows in this batch ----
+        int boff = 0;
+        if (valid && m > 1) {
+            boff = bk_read(sl) >> 12;
+            lst[boff + ticket] = tid;
         }
         __syncthreads();
-        {
-            const int p1 = totals_max_nn(ws32 + 48, w), p2 = totals_max_nn(ws32 + 64, w);
-            ss = ss > p1 ? ss : p1;
-            lo = (lo > p2 ? lo : p2) - 1;
+        // j: my sink's rows before me; pred: the last of them; own_le / own_lt: its
+        // latest own row at or before / before me (rows in batch order = tid order)
+        int j = 0, pred = -1, own_le = own ? tid : -1, own_lt = -1;
+        if (valid && m > 1) {
+            for (int k = 0; k < m; ++k) {
+                const int y = lst[boff + k];
+                if (y < tid) {
+                    ++j;
+                    pred = pred > y ? pred : y;
+                    if (ob[y]) {
+                        own_lt = own_lt > y ? own_lt : y;
+                        own_le = own_le > y ? own_le : y;
+                    }
+                }
+            }
         }
-        RpSlot st = RpSlot{0, 0, -1, -1};
-        if (vp) st = tst[slp];
-        const int j = tid - ss;
-        const int pos = st.cnt + j + 1;
-        const int lastown = lo >= ss ? st.cnt + (lo - ss) + 1 : st.lastown;
-        const int rank = pos - lastown;
-        rk[tid] = rank;
-        __syncthreads();
-        if (vp) {
-            const int prevrank = j > 0 ? rk[tid - 1] : st.prevrank;
-            const int prevg = j > 0 ? gb[(int)(keyp & (RP_B - 1))] : st.lastgroup;
-            if (prevg == Gp) misc[2] = 1;   // two rows of one sink at one t: a pivot mean
+        int j_le = 0, j_lt = 0;   // positions of own_le / own_lt among the bucket
+        if (valid && m > 1 && (own_le >= 0 || own_lt >= 0)) {
+            for (int k = 0; k < m; ++k) {
+                const int y = lst[boff + k];
+                j_le += y < own_le;
+                j_lt += y < own_lt;
+            }
+        } else if (own_le >= 0) {
+            j_le = j;   // own_le == tid
+        }
+        RpAcc<NK> x;
+        x.s = 0;
+        x.v = 0;
+#pragma unroll
+        for (int q = 0; q < NK; ++q) x.c[q] = 0;
+        if (valid) {
+            const int pos = st0.cnt + j + 1;
+            const int lastown = own_le >= 0 ? st0.cnt + j_le + 1 : st0.lastown;
+            const int rank = pos - lastown;
+            int prevrank, prevg;
+            if (j > 0) {
+                prevrank = (pos - 1) - (own_lt >= 0 ? st0.cnt + j_lt + 1 : st0.lastown);
+                prevg = gb[pred];
+            } else {
+                prevrank = st0.cnt > 0 ? st0.cnt - st0.lastown : -1;
+                prevg = st0.lastgroup;
+            }
+            if (prevg == (int)G) misc[2] = 1;   // two rows of one sink at one t: a pivot mean
             const bool pnan = prevrank < 0;
-            cs[idx] = rank - (pnan ? 0 : prevrank);
-            cv[idx] = pnan ? 1 : 0;
+            x.s = rank - (pnan ? 0 : prevrank);
+            x.v = pnan ? 1 : 0;
 #pragma unroll
             for (int q = 0; q < NK; ++q)
-                cc[q * RP_B + idx] = (rank <= km1[q] ? 1 : 0) - ((!pnan && prevrank <= km1[q]) ? 1 : 0);
-            if (tail) tst[slp] = RpSlot{pos, lastown, rank, Gp};
+                x.c[q] = (rank <= km1[q] ? 1 : 0) - ((!pnan && prevrank <= km1[q]) ? 1 : 0);
+            if (j == m - 1) {   // my sink's last row of this batch carries its state on
+                sl->cnt = pos;
+                sl->lastown = lastown;
+                sl->lastgroup = (int)G;
+                bk_write(sl, 0);
+            }
         }
-        if (!valid) {
-            cs[tid] = 0;
-            cv[tid] = 0;
-#pragma unroll
-            for (int q = 0; q < NK; ++q) cc[q * RP_B + tid] = 0;
-        }
-        __syncthreads();
 
         // the next batch's rows (their loads have landed by now) into LDS, sinks hashed
+        // (tb / eb were last read in A, two barriers ago)
         if (has_next) prep(b0 + RP_B, tn, sn, kn, en, tnn, t_last, e_last);
 
         // ---- D: running totals in row order; the last row of a t-group emits its pivot row ----
-        RpAcc<NK> x;
-        x.s = scan_add_i64_of_i32(cs[tid]);
-        x.v = scan_add_i32(cv[tid]);
+        x.s = scan_add_i64_of_i32((int)x.s);
+        x.v = scan_add_i32(x.v);
 #pragma unroll
-        for (int q = 0; q < NK; ++q) x.c[q] = scan_add_i32(cc[q * RP_B + tid]);
+        for (int q = 0; q < NK; ++q) x.c[q] = scan_add_i32(x.c[q]);
         if (lane == 63) {
             wsum[w] = x.s;
             ws32[80 + w] = x.v;
@@ -525,6 +482,7 @@ __global__ __launch_bounds__(RP_B) void rq_rp_fast(RpArgs a)
         if (tid == 0) {
             misc[5] += n_ev_own;
             misc[6] += n_ev_world;
+            misc[8] = 0;   // bucket allocator (read in B, two barriers ago)
         }
         if (misc[3]) break;   // unsorted (set in A, read after barriers): the df is rejected
     }
@@ -919,12 +877,11 @@ __global__ __launch_bounds__(256) void rq_rp_scan(RpArgs a)
 // launch wrappers
 // ============================================================================
 namespace {
-template <bool GLOBAL, class Key>
+template <bool GLOBAL>
 size_t rp_fast_lds(int nK)
 {
     auto al = [](size_t b) { return (b + 15) & ~(size_t)15; };
-    size_t s = al(8 * (RP_B + 2)) + al(8 * (RP_B + 1)) + al(4 * RP_B) + al(RP_B) +
-               al(sizeof(Key) * 2 * RP_B) + 3 * al(4 * RP_B) + al(4 * (size_t)RP_B * nK) +
+    size_t s = al(8 * (RP_B + 2)) + al(8 * (RP_B + 1)) + al(4 * RP_B) + al(RP_B) + al(4 * RP_B) +
                al(8 * 16) + al(4 * 16 * (nK + 6)) + al(4 * 16);
     if (!GLOBAL) s += al(8 * (RP_H + 1)) + al(sizeof(RpSlot) * (RP_H + 1));
     return s;
@@ -936,12 +893,12 @@ hipError_t rp_launch_t(const RpArgs& a, int phase, hipStream_t s)
     const unsigned nd = (unsigned)a.n_df;
     switch (phase) {
     case RP_PHASE_FAST: {
-        const size_t lds = rp_fast_lds<false, uint32_t>(NK);
+        const size_t lds = rp_fast_lds<false>(NK);
         hipLaunchKernelGGL((rq_rp_fast<NK, false>), dim3(nd), dim3(RP_B), lds, s, a);
         break;
     }
     case RP_PHASE_GLOBAL: {
-        const size_t lds = rp_fast_lds<true, uint64_t>(NK);
+        const size_t lds = rp_fast_lds<true>(NK);
         hipLaunchKernelGGL((rq_rp_fast<NK, true>), dim3(nd), dim3(RP_B), lds, s, a);
         break;
     }
