@@ -427,4 +427,190 @@ __device__ void wave_npsum(int64_t n, VAL&& val, double* lds, double out[NV])
     for (int s = 0; s < NV; ++s) out[s] = res[s];
 }
 
+// ---------------------------------------------------------------------------
+// wave_npsum over a row log (the sweep's / replay's pivot rows): the same numpy
+// order as wave_npsum, but a leaf's 8 accumulator lanes take 32 consecutive rows
+// per trip (4 per lane, in the accumulators' order), so each load instruction of a
+// trip covers whole 128 B lines of every column and no line is needed again by a
+// later trip -- with ~6 waves per SIMD interleaving 8 leaves each, lines fetched
+// for the next trip were evicted from L2 before use (1.5x the algorithmic bytes).
+// TNEXT: the value of row k needs t[k + 1] (end past the last row), taken from the
+// next lane on DPP (row_shl:1; lane 7 of a group from lane 0 by row_shr:7).
+// LD(uint32_t k) -> Row (32-bit row offsets: saddr + voffset loads); VF(const Row&,
+// double t_next, double* v).  n < 2^32.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double dpp_shl1_f64(double x)
+{
+    const uint64_t b = rq_dbl_bits(x);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, 0x101, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), 0x101, 0xF, 0xF, false);
+    return rq_bits_dbl(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ double dpp_shr7_f64(double x)
+{
+    const uint64_t b = rq_dbl_bits(x);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, 0x117, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), 0x117, 0xF, 0xF, false);
+    return rq_bits_dbl(((uint64_t)hi << 32) | lo);
+}
+
+template <int NV, bool TNEXT, class Row, class LD, class TLD, class VF>
+__device__ void wave_npsum_rows(int64_t n, double end, LD&& ld, TLD&& tld, VF&& vf, double* lds,
+                                double out[NV])
+{
+    const int lane = lane_id();
+    const int grp = lane >> 3, jj = lane & 7;
+    double* leafv = lds;
+    int* leaf = reinterpret_cast<int*>(lds + NV * 128);
+    double* stk = lds + NV * 128 + 128;
+    double res[NV];
+#pragma unroll
+    for (int s = 0; s < NV; ++s) res[s] = 0.0;
+
+    for (int64_t c0 = 0; c0 < n; c0 += 8192) {
+        const int m = (int)((n - c0) < 8192 ? (n - c0) : 8192);
+        int* so = reinterpret_cast<int*>(stk + 16 * (NV + 1));
+        int* sn = so + 16;
+        int nleaf = 0;
+        {
+            int sp = 0;
+            so[0] = 0;
+            sn[0] = m;
+            sp = 1;
+            while (sp > 0) {
+                --sp;
+                const int o = so[sp], len = sn[sp];
+                if (len <= 128) {
+                    if (lane == 0) {
+                        leaf[2 * nleaf] = o;
+                        leaf[2 * nleaf + 1] = len;
+                    }
+                    ++nleaf;
+                } else {
+                    int n2 = len / 2;
+                    n2 -= n2 % 8;
+                    so[sp] = o + n2;
+                    sn[sp] = len - n2;
+                    so[sp + 1] = o;
+                    sn[sp + 1] = n2;
+                    sp += 2;
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int L0 = 0; L0 < nleaf; L0 += 8) {
+            const int L = L0 + grp;
+            const bool act = L < nleaf;
+            const int off = act ? leaf[2 * L] : 0;
+            const int len = act ? leaf[2 * L + 1] : 0;
+            double r[NV];
+#pragma unroll
+            for (int s = 0; s < NV; ++s) r[s] = 0.0;
+            const int lim = len - (len % 8);
+            for (int i = 0; i < lim; i += 32) {
+                const int nu = (lim - i) >> 3 < 4 ? (lim - i) >> 3 : 4;   // group-uniform
+                const int64_t e0 = c0 + off + i + jj;
+                Row R[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (u < nu) R[u] = ld((uint32_t)(e0 + 8 * u));
+                double tx = end;
+                if (TNEXT && jj == 7) {
+                    const int64_t ka = c0 + off + i + 8 * nu;   // the row after lane 7's last
+                    if (ka < n) tx = tld((uint32_t)ka);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (u < nu) {
+                        double tn = 0.0;
+                        if (TNEXT) {
+                            const double nb = dpp_shl1_f64(R[u].t);
+                            const double w7 = u + 1 < nu ? dpp_shr7_f64(R[u + 1 < 4 ? u + 1 : 3].t) : tx;
+                            tn = jj == 7 ? w7 : nb;
+                        }
+                        double v[NV];
+                        vf(R[u], tn, v);
+#pragma unroll
+                        for (int s = 0; s < NV; ++s) r[s] = (u == 0 && i == 0) ? v[s] : r[s] + v[s];
+                    }
+                }
+            }
+#pragma unroll
+            for (int s = 0; s < NV; ++s) {
+                double x = r[s];
+                x = x + __shfl_xor(x, 1, 64);
+                x = x + __shfl_xor(x, 2, 64);
+                x = x + __shfl_xor(x, 4, 64);
+                r[s] = x;
+            }
+            if (act && jj == 0) {
+                double v[NV];
+                if (len < 8) {
+#pragma unroll
+                    for (int s = 0; s < NV; ++s) r[s] = -0.0;
+                }
+                for (int k = (len >= 8 ? lim : 0); k < len; ++k) {
+                    const int64_t e = c0 + off + k;
+                    const Row Rk = ld((uint32_t)e);
+                    double tn = 0.0;
+                    if (TNEXT) tn = e + 1 < n ? tld((uint32_t)(e + 1)) : end;
+                    vf(Rk, tn, v);
+#pragma unroll
+                    for (int s = 0; s < NV; ++s) r[s] += v[s];
+                }
+#pragma unroll
+                for (int s = 0; s < NV; ++s) leafv[s * 128 + L] = r[s];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double cv[NV];
+        {
+            int* st = so;
+            int sp = 0, li = 0;
+            sn[0] = m;
+            st[0] = 0;
+            sp = 1;
+            while (sp > 0) {
+                const int top = sp - 1;
+                const int len = sn[top];
+                if (len <= 128) {
+#pragma unroll
+                    for (int s = 0; s < NV; ++s) cv[s] = leafv[s * 128 + li];
+                    ++li;
+                    --sp;
+                } else if (st[top] == 0) {
+                    int n2 = len / 2;
+                    n2 -= n2 % 8;
+                    st[top] = 1;
+                    sn[sp] = n2;
+                    st[sp] = 0;
+                    ++sp;
+                } else if (st[top] == 1) {
+#pragma unroll
+                    for (int s = 0; s < NV; ++s) stk[top * (NV + 1) + s] = cv[s];
+                    int n2 = len / 2;
+                    n2 -= n2 % 8;
+                    st[top] = 2;
+                    sn[sp] = len - n2;
+                    st[sp] = 0;
+                    ++sp;
+                } else {
+#pragma unroll
+                    for (int s = 0; s < NV; ++s) cv[s] = stk[top * (NV + 1) + s] + cv[s];
+                    --sp;
+                }
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < NV; ++s) res[s] = res[s] + cv[s];
+        __builtin_amdgcn_wave_barrier();
+    }
+#pragma unroll
+    for (int s = 0; s < NV; ++s) out[s] = res[s];
+}
+
 }  // namespace rq

@@ -995,18 +995,30 @@ __global__ __launch_bounds__(256, WPE) void rq_scan(ScanArgs a)
         if (lane_id() < NV) out[lane_id()] = __builtin_nan("");
         return;
     }
-    auto val = [&](int64_t kk, double* v) {
-        const double t0 = Rt[kk];
-        const double t1 = kk + 1 < n ? Rt[kk + 1] : end;
-        const double dt = t1 - t0;
-        const double m = Rs[kk] / (double)Rv[kk];
+    struct Row {
+        double t, s;
+        uint32_t v, c[NK];
+    };
+    auto ld = [&](uint32_t kk) {
+        Row r;
+        r.t = Rt[kk];
+        r.s = Rs[kk];
+        r.v = Rv[kk];
 #pragma unroll
-        for (int q = 0; q < NK; ++q) v[q] = ((double)Rc[kk * NK + q] / S) * dt;
+        for (int q = 0; q < NK; ++q) r.c[q] = Rc[kk * NK + q];
+        return r;
+    };
+    auto tld = [&](uint32_t kk) { return Rt[kk]; };
+    auto vf = [&](const Row& r, double t1, double* v) {
+        const double dt = t1 - r.t;
+        const double m = r.s / (double)r.v;
+#pragma unroll
+        for (int q = 0; q < NK; ++q) v[q] = ((double)r.c[q] / S) * dt;
         v[NK] = m * dt;
         v[NK + 1] = (m * m) * dt;
     };
     double res[NV];
-    wave_npsum<NV>(n, val, lds, res);
+    wave_npsum_rows<NV, true, Row>(n, end, ld, tld, vf, lds, res);
     if (lane_id() == 0) {
 #pragma unroll
         for (int s = 0; s < NV; ++s) out[s] = res[s];

@@ -857,16 +857,29 @@ __global__ __launch_bounds__(256) void rq_rp_scan(RpArgs a)
     const double* Rs = a.rows_sum + r0;
     const uint32_t* Rv = a.rows_valid + r0;
     const uint32_t* Rc = a.rows_cnt + r0 * NK;
-    auto val = [&](int64_t kk, double* v) {
-        const double dt = Rd[kk];
-        const double m = Rs[kk] / (double)Rv[kk];
+    struct Row {
+        double dt, s;
+        uint32_t v, c[NK];
+    };
+    auto ld = [&](uint32_t kk) {
+        Row r;
+        r.dt = Rd[kk];
+        r.s = Rs[kk];
+        r.v = Rv[kk];
 #pragma unroll
-        for (int q = 0; q < NK; ++q) v[q] = ((double)Rc[kk * NK + q] / S) * dt;
-        v[NK] = m * dt;
-        v[NK + 1] = (m * m) * dt;
+        for (int q = 0; q < NK; ++q) r.c[q] = Rc[kk * NK + q];
+        return r;
+    };
+    auto tld = [&](uint32_t) { return 0.0; };
+    auto vf = [&](const Row& r, double, double* v) {
+        const double m = r.s / (double)r.v;
+#pragma unroll
+        for (int q = 0; q < NK; ++q) v[q] = ((double)r.c[q] / S) * r.dt;
+        v[NK] = m * r.dt;
+        v[NK + 1] = (m * m) * r.dt;
     };
     double res[NV];
-    wave_npsum<NV>(n, val, lds, res);
+    wave_npsum_rows<NV, false, Row>(n, 0.0, ld, tld, vf, lds, res);
     if (lane == 0) {
 #pragma unroll
         for (int s = 0; s < NV; ++s) out[s] = res[s];
