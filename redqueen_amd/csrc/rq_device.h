@@ -517,7 +517,7 @@ __device__ void wave_npsum_rows(int64_t n, double end, LD&& ld, TLD&& tld, VF&& 
                 for (int u = 0; u < 4; ++u)
                     if (u < nu) R[u] = ld((uint32_t)(e0 + 8 * u));
                 double tx = end;
-                if (TNEXT && jj == 7) {
+                if constexpr (TNEXT) if (jj == 7) {
                     const int64_t ka = c0 + off + i + 8 * nu;   // the row after lane 7's last
                     if (ka < n) tx = tld((uint32_t)ka);
                 }
@@ -525,7 +525,7 @@ __device__ void wave_npsum_rows(int64_t n, double end, LD&& ld, TLD&& tld, VF&& 
                 for (int u = 0; u < 4; ++u) {
                     if (u < nu) {
                         double tn = 0.0;
-                        if (TNEXT) {
+                        if constexpr (TNEXT) {
                             const double nb = dpp_shl1_f64(R[u].t);
                             const double w7 = u + 1 < nu ? dpp_shr7_f64(R[u + 1 < 4 ? u + 1 : 3].t) : tx;
                             tn = jj == 7 ? w7 : nb;
@@ -555,7 +555,7 @@ __device__ void wave_npsum_rows(int64_t n, double end, LD&& ld, TLD&& tld, VF&& 
                     const int64_t e = c0 + off + k;
                     const Row Rk = ld((uint32_t)e);
                     double tn = 0.0;
-                    if (TNEXT) tn = e + 1 < n ? tld((uint32_t)(e + 1)) : end;
+                    if constexpr (TNEXT) tn = e + 1 < n ? tld((uint32_t)(e + 1)) : end;
                     vf(Rk, tn, v);
 #pragma unroll
                     for (int s = 0; s < NV; ++s) r[s] += v[s];
