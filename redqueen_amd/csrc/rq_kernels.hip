@@ -1256,7 +1256,7 @@ static hipError_t launch_scan_t(const ScanArgs& a, hipStream_t s)
     const unsigned blocks = (unsigned)((a.n_chunk + 3) / 4);
     const size_t lds = 4 * npsum_lds_doubles<NK + 2>() * sizeof(double);
     // waves per SIMD the build targets (VGPR budget): A/B knob RQ_SCAN_WPE
-    static const int wpe = getenv("RQ_SCAN_WPE") ? atoi(getenv("RQ_SCAN_WPE")) : 6;
+    static const int wpe = getenv("RQ_SCAN_WPE") ? atoi(getenv("RQ_SCAN_WPE")) : 4;
     if (wpe >= 8)
         hipLaunchKernelGGL((rq_scan<NK, 8>), dim3(blocks), dim3(256), lds, s, a);
     else if (wpe >= 6)
