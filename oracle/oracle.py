@@ -267,6 +267,17 @@ class Scenario:
                     sink_id=np.asarray(sink, dtype=np.int64))
 
 
+def state_time_deltas(t, start=0.0):
+    """Event.time_delta of the reference for event times t: time_delta_k = t_k - time,
+    time += time_delta_k, time starting at start (opt_model.py:68, :304)."""
+    out = np.empty(len(t))
+    s = float(start)
+    for k, tk in enumerate(np.asarray(t, dtype=np.float64)):
+        out[k] = tk - s
+        s = s + out[k]
+    return out
+
+
 def _events(cap):
     t = np.zeros(cap); dt = np.zeros(cap); s = np.zeros(cap, dtype=np.int64)
     ev = _Events(cap, 0, _p(t, C.c_double), _p(dt, C.c_double), _p(s, C.c_int64))

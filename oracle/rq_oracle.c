@@ -909,7 +909,7 @@ int rqo_engine_run(const rqo_scenario* sc, rqo_events* ev)
     {
         pstream po = {ctrl->seed, rqo_kind_salt(RQO_OPT) | 0x100u, 0};
         double opt_next = opt ? sc->start_time : INFINITY;
-        double prev_t = sc->start_time;
+        double state_time = sc->start_time;   /* State.time, accumulated (opt_model.py:68) */
         ev->n = 0;
         for (;;) {
             if (sc->max_events >= 0 && ev->n >= sc->max_events) break;
@@ -921,15 +921,23 @@ int rqo_engine_run(const rqo_scenario* sc, rqo_events* ev)
                 if (j == 0 && opt) tj = opt_next;
                 else tj = head[j] < st[j].n ? st[j].v[head[j]] : INFINITY;
                 int64_t id = sc->sources[j].src_id;
-                if (tj < bt || (tj == bt && bj >= 0 && id < bid)) { bt = tj; bj = j; bid = id; }
+                /* ties: the (dynamic) controller before a static wall source, else src_id
+                   (opt_model.py:279-281, :289-290) */
+                int beats = id < bid;
+                if (bj >= 0 && tj == bt && opt && (j == 0 || bj == 0)) {
+                    const int other = j == 0 ? sc->sources[bj].kind : sc->sources[j].kind;
+                    if (other == RQO_POISSON2 || other == RQO_PWCONST || other == RQO_REALDATA)
+                        beats = j == 0;
+                }
+                if (tj < bt || (tj == bt && bj >= 0 && beats)) { bt = tj; bj = j; bid = id; }
             }
             if (bj < 0 || !(bt <= sc->end_time)) break;
             if (ev->n >= ev->cap) { rc = -2; goto done; }
             ev->t[ev->n] = bt;
-            ev->time_delta[ev->n] = bt - prev_t;
+            ev->time_delta[ev->n] = bt - state_time;
+            state_time = state_time + ev->time_delta[ev->n];
             ev->src_id[ev->n] = bid;
             ev->n++;
-            prev_t = bt;
             if (bj == 0 && opt) {
                 opt_next = INFINITY;
             } else {

@@ -295,25 +295,40 @@ __global__ __launch_bounds__(1024) void rq_log_expand_k(LogArgs a)
     __shared__ double stt[CH];
     __shared__ double std_[CH];
     __shared__ int64_t wsum[NW];
+    __shared__ double state_time;   // State.time after the previous chunk (accumulated)
+    __shared__ int any_dirty;
     const int64_t r = blockIdx.x;
     const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
     const int64_t n = a.counts[r * 4 + 2];
     const double* T = a.ev_t + r * a.ev_cap;
     const int32_t* J = a.ev_src + r * a.ev_cap;
     int64_t row0 = a.row_off[r];
+    if (tid == 0) state_time = a.start;
     for (int64_t c0 = 0; c0 < n; c0 += CH) {
         const int m = (int)((n - c0) < CH ? (n - c0) : CH);
-        // this thread's event: degree + a block exclusive scan
+        if (tid == 0) any_dirty = 0;
+        __syncthreads();
+        // this thread's event: degree + a block exclusive scan.  time_delta follows the
+        // reference's State: time_delta_k = t_k - time_{k-1}, time_k = time_{k-1} +
+        // time_delta_k (opt_model.py:68, :304).  time_k == t_k unless the subtraction
+        // rounded (t_k > 2 time_{k-1}: early events, long gaps), and the next exact
+        // subtraction heals it; so every event assumes time_{k-1} == t_{k-1} and one
+        // thread redoes the chain from each event where that fails ("dirty").
         const int e = tid;
         int64_t d = 0;
+        bool dirty = false;
         if (e < m) {
             const int j = J[c0 + e];
             const double tk = T[c0 + e];
             d = a.csr_ptr[j + 1] - a.csr_ptr[j];
             sj[e] = j;
             stt[e] = tk;
-            std_[e] = tk - (c0 + e > 0 ? T[c0 + e - 1] : a.start);
+            const double sp = e > 0 ? T[c0 + e - 1] : state_time;
+            const double td = tk - sp;
+            std_[e] = td;
+            dirty = sp + td != tk;
         }
+        if (dirty) any_dirty = 1;
         int64_t v = d;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -329,6 +344,19 @@ __global__ __launch_bounds__(1024) void rq_log_expand_k(LogArgs a)
         }
         if (e < m) off[e] = pre + v - d;
         if (tid == 0) off[m] = chunk_rows;
+        __syncthreads();
+        if (tid == 0) {
+            // the accumulated chain, sequentially, in a chunk where some event's
+            // time != t (rare: the chunk's speculative values are kept otherwise)
+            double s = state_time;
+            if (any_dirty)
+                for (int k = 0; k < m; ++k) {
+                    const double td = stt[k] - s;
+                    std_[k] = td;
+                    s = s + td;
+                }
+            state_time = any_dirty ? s : stt[m - 1];
+        }
         __syncthreads();
         // rows of this chunk, one per thread, coalesced column stores
         for (int64_t x = tid; x < chunk_rows; x += NT) {

@@ -242,7 +242,8 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     }
     double rows = wall_caps + ((ck == RQ_SRC_OPT || ck == RQ_SRC_OPTPW) ? wall_caps + 1.0 : (double)ctrl_cap) + 8.0;
     if (b->max_events >= 0) rows = std::min(rows, (double)b->max_events + 1.0);
-    p->cap_rows = std::max<int64_t>(64, (int64_t)rows);
+    // a multiple of 32 rows: replica row bases stay aligned to the scan's 32-row trips
+    p->cap_rows = (std::max<int64_t>(64, (int64_t)rows) + 31) & ~(int64_t)31;
     p->spl = g->n_str <= 64 ? 1 : g->n_str <= 128 ? 2 : g->n_str <= 256 ? 4 : 8;
     if (g->n_str > 512) return RQ_EUNSUPPORTED;
     p->n_sinks_pad = (g->n_sinks + 1) | 1;   // odd stride: spreads replicas over LDS banks
@@ -390,7 +391,7 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     p->off_rv = o;      o = align_up(o + sizeof(uint32_t) * (size_t)C * p->cap_rows, A);
     p->off_rc = o;      o = align_up(o + sizeof(uint32_t) * (size_t)C * p->cap_rows * p->nK, A);
     p->off_sall = o;    o = align_up(o + sizeof(int) * (size_t)C, A);
-    p->off_wq = o;      o = align_up(o + sizeof(int), A);
+    p->off_wq = o;      o = align_up(o + 2 * sizeof(int), A);   // [0] sweep, [1] scan queue
     p->total = o;
     return RQ_OK;
 }
@@ -878,9 +879,10 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             // fused sweep: waves past their first replica take the next one from a queue,
             // so the launch tail is spread over every CU instead of whole 16-wave blocks
             static const int wq_off = getenv("RQ_FW_STATIC") ? atoi(getenv("RQ_FW_STATIC")) : 0;   // A/B only
+            // both queues of this chunk (sweep, scan) zeroed by one memset
+            if (hipMemsetAsync(ws + p.off_wq, 0, 2 * sizeof(int), s) != hipSuccess) return RQ_EHIP;
             if (!wq_off) {   // both sweep kinds take replicas past the first from the queue
                 sa.wq = (int*)(ws + p.off_wq);
-                if (hipMemsetAsync(sa.wq, 0, sizeof(int), s) != hipSuccess) return RQ_EHIP;
             }
             TimedLaunch tl(K_SWEEP, s);
             const hipError_t e = p.fw ? rq_launch_sweep_fw(sa, p.nK, p.gcol16, p.gwin, p.bits, s)
@@ -901,6 +903,7 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
         sc.rows_cnt = sa.rows_cnt;
         sc.end = g->end;
         sc.metrics = out->metrics;
+        sc.wq = (int*)(ws + p.off_wq) + 1;
         {
             TimedLaunch tl(K_SCAN, s);
             if (rq_launch_scan(sc, p.nK, s) != hipSuccess) return RQ_EHIP;

@@ -94,6 +94,7 @@ struct ScanArgs {
     const uint32_t* rows_cnt;
     double end;
     double* metrics;
+    int* wq;                // replica work queue (zeroed before the launch; null = one replica per wave)
 };
 
 hipError_t rq_launch_gen(const GenArgs& a, hipStream_t s);

@@ -132,7 +132,13 @@ __global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
     for (int j = threadIdx.x; j <= a.n_str; j += blockDim.x) cptr[j] = a.csr_ptr[j];
     for (int j = threadIdx.x; j < a.n_str; j += blockDim.x) {
         odf[j] = a.outdeg_f[j];
-        cbf[j] = a.ctrl_src_id < a.src_id[j];
+        // the controller (a dynamic source) posts before a wall event at the same time
+        // when that source is static (run_dynamic plays a static time only if it is
+        // strictly earlier, opt_model.py:289-290) or has a larger src_id (the sorted
+        // (t_delta, src_id) of the dynamic sources, :279-281)
+        const int kj = a.gen.kind[j];
+        cbf[j] = kj == RQ_SRC_POISSON2 || kj == RQ_SRC_PWCONST || kj == RQ_SRC_REALDATA ||
+                 a.ctrl_src_id < a.src_id[j];
     }
     // BL: the follower set as a sink bitset, shared by the block's waves
     uint32_t* fbl = reinterpret_cast<uint32_t*>(base + a.lds_fbits);
@@ -596,7 +602,13 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
     for (int j = threadIdx.x; j <= a.n_str; j += blockDim.x) cptr[j] = a.csr_ptr[j];
     for (int j = threadIdx.x; j < a.n_str; j += blockDim.x) {
         odf[j] = a.outdeg_f[j];
-        cbf[j] = a.ctrl_src_id < a.src_id[j];
+        // the controller (a dynamic source) posts before a wall event at the same time
+        // when that source is static (run_dynamic plays a static time only if it is
+        // strictly earlier, opt_model.py:289-290) or has a larger src_id (the sorted
+        // (t_delta, src_id) of the dynamic sources, :279-281)
+        const int kj = a.gen.kind[j];
+        cbf[j] = kj == RQ_SRC_POISSON2 || kj == RQ_SRC_PWCONST || kj == RQ_SRC_REALDATA ||
+                 a.ctrl_src_id < a.src_id[j];
     }
     __syncthreads();   // block-shared tables ready; no block barrier below this line
     char* wb = base + a.lds_wave + (size_t)w * a.lds_wave_stride;
@@ -976,52 +988,58 @@ __global__ __launch_bounds__(256, WPE) void rq_scan(ScanArgs a)
     constexpr int NV = NK + 2;
     extern __shared__ double lds_scan[];
     const int w = threadIdx.x >> 6;
-    const int64_t rl = (int64_t)blockIdx.x * 4 + w;
-    if (rl >= a.n_chunk) return;
-    const int64_t i = a.chunk0 + rl;
     double* lds = lds_scan + (size_t)w * npsum_lds_doubles<NV>();
-
-    const int64_t n = a.nrows[i * a.nrows_stride];
-    const double S = (double)a.sall[rl];
-    const int64_t rbase = a.row_stride * rl;
-    const double* Rt = a.rows_t + rbase;
-    const double* Rs = a.rows_sum + rbase;
-    const uint32_t* Rv = a.rows_valid + rbase;
-    const uint32_t* Rc = a.rows_cnt + rbase * NK;
-    const double end = a.end;
-    double* out = a.metrics + i * NV;
-
-    if (n <= 0) {
-        if (lane_id() < NV) out[lane_id()] = __builtin_nan("");
-        return;
-    }
-    struct Row {
-        double t, s;
-        uint32_t v, c[NK];
-    };
-    auto ld = [&](uint32_t kk) {
-        Row r;
-        r.t = Rt[kk];
-        r.s = Rs[kk];
-        r.v = Rv[kk];
+    // persistent: a wave's first replica is its slot, the next ones come from the
+    // queue (10k one-wave replicas over ~4k resident waves otherwise leave a tail)
+    const int64_t nslot = (int64_t)gridDim.x * 4;
+    int64_t rl = (int64_t)blockIdx.x * 4 + w;
+    while (rl < a.n_chunk) {
+        const int64_t i = a.chunk0 + rl;
+        const int64_t n = a.nrows[i * a.nrows_stride];
+        const double S = (double)a.sall[rl];
+        const int64_t rbase = a.row_stride * rl;
+        const double* Rt = a.rows_t + rbase;
+        const double* Rs = a.rows_sum + rbase;
+        const uint32_t* Rv = a.rows_valid + rbase;
+        const uint32_t* Rc = a.rows_cnt + rbase * NK;
+        const double end = a.end;
+        double* out = a.metrics + i * NV;
+        if (n <= 0) {
+            if (lane_id() < NV) out[lane_id()] = __builtin_nan("");
+        } else {
+            struct Row {
+                double t, s;
+                uint32_t v, c[NK];
+            };
+            auto ld = [&](uint32_t kk) {
+                Row r;
+                r.t = Rt[kk];
+                r.s = Rs[kk];
+                r.v = Rv[kk];
 #pragma unroll
-        for (int q = 0; q < NK; ++q) r.c[q] = Rc[kk * NK + q];
-        return r;
-    };
-    auto tld = [&](uint32_t kk) { return Rt[kk]; };
-    auto vf = [&](const Row& r, double t1, double* v) {
-        const double dt = t1 - r.t;
-        const double m = r.s / (double)r.v;
+                for (int q = 0; q < NK; ++q) r.c[q] = Rc[kk * NK + q];
+                return r;
+            };
+            auto tld = [&](uint32_t kk) { return Rt[kk]; };
+            auto vf = [&](const Row& r, double t1, double* v) {
+                const double dt = t1 - r.t;
+                const double m = r.s / (double)r.v;
 #pragma unroll
-        for (int q = 0; q < NK; ++q) v[q] = ((double)r.c[q] / S) * dt;
-        v[NK] = m * dt;
-        v[NK + 1] = (m * m) * dt;
-    };
-    double res[NV];
-    wave_npsum_rows<NV, true, Row>(n, end, ld, tld, vf, lds, res);
-    if (lane_id() == 0) {
+                for (int q = 0; q < NK; ++q) v[q] = ((double)r.c[q] / S) * dt;
+                v[NK] = m * dt;
+                v[NK + 1] = (m * m) * dt;
+            };
+            double res[NV];
+            wave_npsum_rows<NV, true, Row>(n, end, ld, tld, vf, lds, res);
+            if (lane_id() == 0) {
 #pragma unroll
-        for (int s = 0; s < NV; ++s) out[s] = res[s];
+                for (int s = 0; s < NV; ++s) out[s] = res[s];
+            }
+        }
+        if (!a.wq) break;
+        int nx = 0;
+        if (lane_id() == 0) nx = atomicAdd(a.wq, 1);
+        rl = nslot + __builtin_amdgcn_readfirstlane(nx);
     }
 }
 
@@ -1250,19 +1268,31 @@ int rq_fw_blocks_per_cu(int nK, int col16, int W, int bits, int wpb, size_t lds,
     return col16 ? occ_fw_k<uint16_t, 8>(nK, wpb, lds) : occ_fw_k<int, 8>(nK, wpb, lds);
 }
 
+template <int NK, int WPE>
+static unsigned scan_blocks(const ScanArgs& a, size_t lds)
+{
+    unsigned blocks = (unsigned)((a.n_chunk + 3) / 4);
+    if (a.wq) {   // persistent grid: every resident block once
+        static int nb = -1;
+        if (nb < 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rq_scan<NK, WPE>, 256, lds) != hipSuccess)
+            nb = 0;
+        const unsigned cap = (unsigned)(nb > 0 ? nb : 1) * (unsigned)rq_cu_count();
+        if (cap < blocks) blocks = cap;
+    }
+    return blocks;
+}
 template <int NK>
 static hipError_t launch_scan_t(const ScanArgs& a, hipStream_t s)
 {
-    const unsigned blocks = (unsigned)((a.n_chunk + 3) / 4);
     const size_t lds = 4 * npsum_lds_doubles<NK + 2>() * sizeof(double);
     // waves per SIMD the build targets (VGPR budget): A/B knob RQ_SCAN_WPE
     static const int wpe = getenv("RQ_SCAN_WPE") ? atoi(getenv("RQ_SCAN_WPE")) : 4;
     if (wpe >= 8)
-        hipLaunchKernelGGL((rq_scan<NK, 8>), dim3(blocks), dim3(256), lds, s, a);
+        hipLaunchKernelGGL((rq_scan<NK, 8>), dim3(scan_blocks<NK, 8>(a, lds)), dim3(256), lds, s, a);
     else if (wpe >= 6)
-        hipLaunchKernelGGL((rq_scan<NK, 6>), dim3(blocks), dim3(256), lds, s, a);
+        hipLaunchKernelGGL((rq_scan<NK, 6>), dim3(scan_blocks<NK, 6>(a, lds)), dim3(256), lds, s, a);
     else
-        hipLaunchKernelGGL((rq_scan<NK, 4>), dim3(blocks), dim3(256), lds, s, a);
+        hipLaunchKernelGGL((rq_scan<NK, 4>), dim3(scan_blocks<NK, 4>(a, lds)), dim3(256), lds, s, a);
     return hipGetLastError();
 }
 

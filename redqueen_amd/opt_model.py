@@ -56,11 +56,36 @@ class State:
         self._edges = list(edge_list)
         self._events = None
         if self._t.size:
-            self.time = float(self._t[-1])
+            self.time = self._accumulate()[1]
 
     def _time_delta(self):
-        prev = np.concatenate([[self._start], self._t[:-1]]) if self._t.size else self._t
-        return self._t - prev
+        return self._accumulate()[0]
+
+    def _accumulate(self):
+        """Event.time_delta as the reference accumulates it: time_delta_k = t_k - time,
+        time += time_delta_k (opt_model.py:68, :304); returns (time_delta, final time).
+        time == t_k except after a rounded subtraction; the chain is redone from those
+        events until it heals."""
+        t = self._t
+        if not t.size:
+            return t, self._start
+        prev = np.concatenate([[self._start], t[:-1]])
+        td = t - prev
+        dirty = np.flatnonzero(prev + td != t)
+        k, n = 0, t.size
+        final = prev[-1] + td[-1]
+        for k0 in dirty:
+            if k0 < k:
+                continue
+            s = prev[k0] + td[k0]
+            k = k0 + 1
+            while k < n and s != t[k - 1]:
+                td[k] = t[k] - s
+                s = s + td[k]
+                k += 1
+            if k == n:
+                final = s
+        return td, float(final)
 
     @property
     def events(self):

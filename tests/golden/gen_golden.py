@@ -27,6 +27,8 @@ installed and there is no network) and records, as plain data:
   dist_c3.npz      (--c3-dist N) N-replica RedQueen ensemble on the C3 bench network
   dist_sig.npz     (--sig-dist N) N-replica OptPWSignificance ensemble (K3 network,
                    24-segment follower significance, randomized worlds)
+  realdata.npz     all-RealData worlds (create_manager_with_times): the reference's whole
+                   df (deterministic), its metrics and final State.time
   sig_runs.npz     OptPWSignificance runs (notebook "Testing out significance",
                    opt_broadcast.ipynb:5469, :5569): events + metrics
   graphs.npz       opt_runs.make_edge_list networks (C3 parameters) and a
@@ -421,6 +423,26 @@ def gen_sweepq():
     np.savez_compressed(os.path.join(HERE, "sweepq.npz"), **rec)
 
 
+from realdata_worlds import realdata_worlds  # noqa: E402  (plain data, shared with the tests)
+
+
+def gen_realdata():
+    rec = {}
+    names = []
+    for name, w, ctrl, maxev in realdata_worlds():
+        so = SimOpts(**w)
+        m = so.create_manager_with_times(np.asarray(ctrl))
+        m.run_dynamic(max_events=maxev if maxev is not None else float("inf"))
+        df = m.state.get_dataframe()
+        _df_cols(rec, name, df)
+        met, own, world = metrics(df, so)
+        rec[name + "_met"] = met
+        rec[name + "_cnt"] = np.asarray([own, world, len(df), m.state.get_num_events()])
+        rec[name + "_state_time"] = np.asarray([m.state.time])
+        names.append(name)
+    np.savez_compressed(os.path.join(HERE, "realdata.npz"), names=np.asarray(names), **rec)
+
+
 def gen_sig():
     """OptPWSignificance (opt_model.py:547-623) via create_manager_with_significance
     (:850-884): the notebook cells opt_broadcast.ipynb:5469 and :5569 plus variants."""
@@ -605,7 +627,7 @@ if __name__ == "__main__":
     a = ap.parse_args()
     steps = {"npsum": gen_npsum, "draws": gen_draws, "readme": gen_readme, "kats": gen_kats,
              "adv": gen_adversarial, "graphs": gen_graphs, "frac": gen_frac,
-             "oracle": gen_oracle, "sweepq": gen_sweepq, "sig": gen_sig}
+             "oracle": gen_oracle, "sweepq": gen_sweepq, "sig": gen_sig, "realdata": gen_realdata}
     if a.c3_dist:
         gen_c3_dist(a.c3_dist)
         print("done c3 dist", flush=True)

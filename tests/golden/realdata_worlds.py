@@ -1,0 +1,38 @@
+"""World definitions of tests/golden/realdata.npz (plain data: no reference import),
+shared by gen_golden.py and tests/test_gpu_realdata.py."""
+import numpy as np
+
+
+# all-RealData worlds: every source static with given times, so the reference's whole
+# df is deterministic and the engine must reproduce it bit for bit (event order with
+# equal-time events across sources, event_id, accumulated time_delta, t beyond end,
+# times before start, unsorted and duplicate times within a source)
+def realdata_worlds():
+    rs = np.random.RandomState(2024)
+    w1 = dict(src_id=1, end_time=100.0, s=1.0, q=1.0, sink_ids=[1, 2, 3],
+              other_sources=[("RealData", {"src_id": 2, "times": [0.0, 0.5, 1.0, 3.0, 3.0, 7.25, 9.0,
+                                                                 100.0]}),
+                             ("RealData", {"src_id": 3, "times": [0.5, 2.0, 2.5, 8.0, 7.0, -1.0,
+                                                                 101.0]})],
+              edge_list=[(1, 1), (1, 3), (2, 1), (2, 2), (2, 3), (3, 3)])
+    c1 = [0.0, 0.5, 2.0, 2.0, 7.25, 50.0, 99.0, 100.0, 120.0]
+    sinks = list(range(1, 16))
+    srcs = [3, 7, 12, 20]
+    edges = []
+    for sid in [10] + srcs:
+        for y in rs.choice(sinks, rs.randint(2, 9), replace=False):
+            edges.append((sid, int(y)))
+    edges.append((99, 4))   # a source with one edge and times only past end_time
+    others = [("RealData", {"src_id": sid, "times": list(np.round(rs.uniform(-2, 44, rs.randint(5, 30)) * 2) / 2)})
+              for sid in srcs] + [("RealData", {"src_id": 99, "times": [41.0, 45.0]})]
+    w2 = dict(src_id=10, end_time=40.0, s=1.0, q=1.0, sink_ids=sinks, other_sources=others,
+              edge_list=edges)
+    c2 = list(np.round(rs.uniform(0, 42, 25) * 2) / 2) + [0.0]
+    # tiny times first: the accumulated State.time rounds (t_k > 2 time_{k-1})
+    w3 = dict(src_id=4, end_time=3.0, s=1.0, q=1.0, sink_ids=[1, 2],
+              other_sources=[("RealData", {"src_id": 2, "times": [1e-9, 3e-9, 0.1, 0.1 + 1e-12, 1.7,
+                                                                 2.9999999]}),
+                             ("RealData", {"src_id": 7, "times": [0.3, 1.0 / 3.0, 2.0 / 3.0, 3.0]})],
+              edge_list=[(2, 1), (7, 1), (7, 2), (4, 2)])
+    c3 = [1e-300, 0.1 + 1e-12, 0.7, 1.7]
+    return [("rd1", w1, c1, None), ("rd2", w2, c2, None), ("rd2m", w2, c2, 17), ("rd3", w3, c3, None)]

@@ -80,7 +80,8 @@ def test_state_log_without_a_run():
     assert st.get_num_events() == len(t)
     ev = st.events[3]
     assert ev.event_id == 103 and ev.src_id == s[3] and ev.cur_time == t[3]
-    assert ev.time_delta == t[3] - t[2]
+    assert ev.time_delta == dt[3]   # accumulated State.time (opt_model.py:68)
+    assert np.array_equal([e.time_delta for e in st.events], O.state_time_deltas(t))
 
 
 def test_graph_generators_reproduce_reference_networks(golden):

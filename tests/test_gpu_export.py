@@ -13,7 +13,7 @@ COLS = ["event_id", "time_delta", "src_id", "t", "sink_id"]
 
 def _check(res, O, so, i):
     t, s = res.events(i)
-    dt = np.diff(np.concatenate([[0.0], t]))
+    dt = O.state_time_deltas(t)
     sc = O.Scenario(so, ("opt", 0))
     ref = sc.expand(t, dt, s)
     df = res.dataframe(i)
@@ -65,7 +65,7 @@ def test_manager_dataframe_and_export(tmp_path):
     m.run_dynamic()
     df = m.state.get_dataframe()
     t, s = m.state._t, m.state._src
-    ref = O.Scenario(graphs.readme(), ("opt", 101)).expand(t, np.diff(np.concatenate([[0.0], t])), s)
+    ref = O.Scenario(graphs.readme(), ("opt", 101)).expand(t, O.state_time_deltas(t), s)
     for c in COLS:
         assert np.array_equal(df[c].values, ref[c]), c
     g = _graph(engine, graphs.readme())

@@ -255,3 +255,25 @@ def test_engine_c3_matches_reference_distribution(golden):
         r = ref[k]
         z = (v.mean() - r.mean()) / math.sqrt(v.var() / len(v) + r.var() / len(r))
         assert abs(z) < 2.576, (k, r.mean(), v.mean(), z)
+
+
+def test_realdata_worlds_both_restatements_exact(golden):
+    """All-RealData worlds (create_manager_with_times): the reference restatement
+    AND the engine-semantics restatement reproduce the reference's whole df -- event
+    order under equal times, accumulated time_delta -- and its metrics (realdata.npz)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from realdata_worlds import realdata_worlds
+    d = golden("realdata.npz")
+    for name, w, ctrl, maxev in realdata_worlds():
+        sc = O.Scenario(w, ("times", np.asarray(ctrl, dtype=np.float64)), max_events=maxev)
+        for run in (O.ref_run, O.engine_run):
+            t, dt, s = run(sc)
+            cols = sc.expand(t, dt, s)
+            for c in ("event_id", "time_delta", "src_id", "t", "sink_id"):
+                assert np.array_equal(cols[c], d[name + "_" + c]), (name, run.__name__, c)
+            top, avg, r2, cnt = O.metrics_df(cols["t"], cols["src_id"], cols["sink_id"],
+                                             cols["event_id"], w["src_id"], w["end_time"], KS)
+            assert np.array_equal(np.asarray(top + [avg, r2]), d[name + "_met"]), name
+            assert np.array_equal(O.state_time_deltas(t), dt)
