@@ -38,10 +38,18 @@
  *     exception crosses the ABI; rq_strerror() names a code.
  *   - rq_graph_t handles are immutable after build and may be shared by threads.
  *   - rq_run_batch / rq_metrics_replay are stream-ordered and asynchronous:
- *     they only enqueue work on `hip_stream` (a hipStream_t, NULL = default
- *     stream) and never allocate, free or synchronise.  The caller owns every
+ *     they enqueue work on `hip_stream` (a hipStream_t, NULL = default stream)
+ *     and never touch caller memory on the host side.  The caller owns every
  *     device buffer (workspace and outputs) and must keep them alive until the
- *     stream has passed the work.  One device per process; the caller selects it.
+ *     stream has passed the work.  rq_run_batch stages its per-run parameter
+ *     tables through a ring of 4 pinned host buffers owned by the graph handle:
+ *     the ring is allocated (hipHostMalloc) on the first call and when a larger
+ *     table is needed, and a call waits (hipEventSynchronize) for the copy
+ *     issued by the call 4 earlier on the same graph before reusing its slot --
+ *     so a warm-up call keeps allocation out of timed regions, and a caller
+ *     issuing many batches back to back runs at most 4 copies ahead.
+ *     rq_metrics_replay never allocates or waits.  One device per process; the
+ *     caller selects it.
  *   - "device pointer" = memory allocated on the current HIP device
  *     (e.g. torch.empty(..., device="cuda").data_ptr()).
  */
@@ -161,7 +169,20 @@ typedef struct rq_batch_desc {
     int32_t n_seg;
     double period;
     const double* s_pw;          /* host [n_grid][n_followers][n_seg]                            */
+    /* Per-replica times of RealData sources -- the static broadcasters a user registers
+       with SimOpts.registerSource (opt_model.py:768-771): the host runs their
+       initialize() / get_all_times() (:336-338, :391-394) once per replica (seeded as
+       randomize_other_sources gives them) and hands the times over here.  Source k is the
+       graph's RealData source rd_src_id[k] (declared with no times); replica i (global id)
+       plays rd_times[rd_off[i * n_rd + k] .. rd_off[i * n_rd + k + 1]), sorted and within
+       [start_time, end_time].  n_rd = 0: every RealData source plays its graph times. */
+    int32_t n_rd;                /* <= RQ_MAX_RD                                                 */
+    const int64_t* rd_src_id;    /* host [n_rd]                                                  */
+    const int64_t* rd_cap;       /* host [n_rd]: the most times any replica gives source k       */
+    const double* rd_times;      /* device                                                       */
+    const int64_t* rd_off;       /* device [n_grid * n_rep * n_rd + 1]                           */
 } rq_batch_desc;
+#define RQ_MAX_RD 64
 
 typedef struct rq_outputs {
     double* metrics;   /* device [R][nK + 2]: top_K..., avg_rank, r_2  (R = n_local or n_grid*n_rep) */

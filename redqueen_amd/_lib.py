@@ -20,6 +20,7 @@ RUN_EVENT_LOG = 1
 ABI_VERSION = 3
 REPLAY_LARGE = 1
 MAX_K = 4
+MAX_RD = 64
 
 _P = C.c_void_p
 _pd = C.POINTER(C.c_double)
@@ -50,7 +51,9 @@ class BatchDesc(C.Structure):
                 ("Ks", _pi32), ("nK", C.c_int32), ("max_events", C.c_int64),
                 ("flags", C.c_int32), ("cap_scale", C.c_double), ("chunk", C.c_int64),
                 ("replica0", C.c_int64), ("n_local", C.c_int64), ("sweep_mode", C.c_int32),
-                ("n_seg", C.c_int32), ("period", C.c_double), ("s_pw", _pd)]
+                ("n_seg", C.c_int32), ("period", C.c_double), ("s_pw", _pd),
+                ("n_rd", C.c_int32), ("rd_src_id", _pi64), ("rd_cap", _pi64), ("rd_times", _P),
+                ("rd_off", _P)]
 
 
 class Outputs(C.Structure):

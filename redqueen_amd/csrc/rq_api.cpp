@@ -129,6 +129,7 @@ struct Plan {
     int64_t R = 0, chunk = 0, capsum = 0, cap_rows = 0;
     std::vector<int> cap;
     std::vector<int64_t> st_off;
+    std::vector<int> rd_k;   // stream -> per-replica RealData source k (rq_batch_desc.rd_*) or -1
     // sequential (event log / max_events) sweep variant; K=1 sink-bitset variant
     bool log = false, bits = false;
     // K=1 on per-wave LDS sink bits for graphs past the bitset variant (> 64 sources)
@@ -144,7 +145,7 @@ struct Plan {
     size_t tables_bytes = 0;
     size_t off_pwc = 0, off_pwmax = 0;
     size_t off_invc = 0, off_streams = 0, off_slen = 0, off_rt = 0, off_rs = 0, off_rv = 0,
-           off_rc = 0, off_sall = 0, off_wq = 0, off_stoff = 0, off_cap = 0,
+           off_rc = 0, off_sall = 0, off_wq = 0, off_stoff = 0, off_cap = 0, off_rdk = 0,
            total = 0;
 };
 
@@ -220,6 +221,21 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     p->chunk = b->chunk > 0 ? std::min<int64_t>(b->chunk, p->R) : std::min<int64_t>(p->R, 16384);
     p->cap.assign(g->n_str, 0);
     p->st_off.assign(g->n_str, 0);
+    p->rd_k.assign(g->n_str, -1);
+    if (b->n_rd < 0 || b->n_rd > RQ_MAX_RD) return RQ_EINVAL;
+    if (b->n_rd > 0) {
+        if (!b->rd_src_id || !b->rd_cap || !b->rd_times || !b->rd_off) return RQ_EINVAL;
+        for (int k = 0; k < b->n_rd; ++k) {
+            int jk = -1;
+            for (int j = 0; j < g->n_str; ++j)
+                if (g->src_id[j] == b->rd_src_id[k]) jk = j;
+            // a RealData wall source of the graph, named once
+            if (jk < 0 || jk == g->ctrl_idx || g->kind[jk] != RQ_SRC_REALDATA || p->rd_k[jk] >= 0 ||
+                b->rd_cap[k] < 0 || b->rd_cap[k] > ((int64_t)1 << 30))
+                return RQ_EINVAL;
+            p->rd_k[jk] = k;
+        }
+    }
     double wall_caps = 0.0;
     int64_t ctrl_cap = 0;
     for (int j = 0; j < g->n_str; ++j) {
@@ -230,7 +246,7 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
         const double m = stream_mean_var(g, j, kind, b, &var);
         int64_t c = 0;
         if (kind != RQ_SRC_NONE)
-            c = kind == RQ_SRC_REALDATA ? (int64_t)m
+            c = kind == RQ_SRC_REALDATA ? (p->rd_k[j] >= 0 ? b->rd_cap[p->rd_k[j]] : (int64_t)m)
                                         : (int64_t)std::ceil((m + 8.0 * std::sqrt(var) + 32.0) * scale);
         if (c > (int64_t)1 << 30) return RQ_EINVAL;
         c = (c + 7) & ~(int64_t)7;   // 64-byte chunks for the generator's stores
@@ -377,6 +393,7 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     p->off_invc = o;    o = o + sizeof(double) * (size_t)b->n_grid * g->n_str;
     p->off_stoff = o;   o = o + sizeof(int64_t) * g->n_str;
     p->off_cap = o;     o = o + sizeof(int) * g->n_str;
+    p->off_rdk = o;     o = o + sizeof(int) * g->n_str;
     const size_t nseg = b->ctrl_kind == RQ_SRC_OPTPW ? (size_t)b->n_seg : 0;
     o = align_up(o, 8);
     p->off_pwc = o;     o = o + sizeof(double) * (size_t)b->n_grid * g->n_str * nseg;
@@ -712,7 +729,7 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
                 pwmax[(size_t)gi * g->n_str + j] = m;
             }
     }
-    // parameter tables [inv_c | st_off | cap | pw_c | pw_max]: staged in one of the graph's pinned host
+    // parameter tables [inv_c | st_off | cap | rd_k | pw_c | pw_max]: staged in one of the graph's pinned host
     // buffers so the copy is truly asynchronous (a pageable copy would stall the host)
     {
         std::lock_guard<std::mutex> lk(g->stage_mu);
@@ -739,6 +756,7 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
         std::memcpy(tab + p.off_invc, invc.data(), invc.size() * sizeof(double));
         std::memcpy(tab + p.off_stoff, p.st_off.data(), p.st_off.size() * sizeof(int64_t));
         std::memcpy(tab + p.off_cap, p.cap.data(), p.cap.size() * sizeof(int));
+        std::memcpy(tab + p.off_rdk, p.rd_k.data(), p.rd_k.size() * sizeof(int));
         if (!pwc.empty()) {
             std::memcpy(tab + p.off_pwc, pwc.data(), pwc.size() * sizeof(double));
             std::memcpy(tab + p.off_pwmax, pwmax.data(), pwmax.size() * sizeof(double));
@@ -786,6 +804,12 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
         ga.streams = (double*)(ws + p.off_streams);
         ga.slen = (int*)(ws + p.off_slen);
         ga.status = out->status;
+        if (b->n_rd > 0) {
+            ga.rd_k = (const int*)(ws + p.off_rdk);
+            ga.n_rd = b->n_rd;
+            ga.rd_times = b->rd_times;
+            ga.rd_off = b->rd_off;
+        }
         if (!p.fw) {
             TimedLaunch tl(K_GEN, s);
             if (rq_launch_gen(ga, s) != hipSuccess) return RQ_EHIP;

@@ -4,14 +4,15 @@
 // refilled in LDS), so both produce the same bits.  One step() = one candidate:
 //   Poisson / Poisson2  opt_model.py:424-433 / :396-405 -- exponential gaps
 //                       t += Exp(1) / rate (one draw per arrival)
-//   Hawkes              opt_model.py:466-490 -- Ogata thinning, bound B = lambda at
-//                       the last accepted arrival (not refreshed on rejection), the
-//                       exponential kernel's O(1) recurrence for lambda; two draws
-//                       (Exp, uniform) per candidate; accept when U * B < lambda
-//                       (the reference's U < lambda / B, division-free); after a
-//                       rejection the bound is refreshed to lambda at the candidate
-//                       (the reference keeps the stale bound: same law, more
-//                       candidates)
+//   Hawkes              opt_model.py:466-490 -- Ogata thinning with the exponential
+//                       kernel's O(1) recurrence for lambda; two draws (Exp, uniform)
+//                       per candidate; accept when U * B < lambda (the reference's
+//                       U < lambda / B, division-free).  The bound B starts at lambda
+//                       at the last accepted arrival and, after a rejection, is
+//                       refreshed to lambda at the rejected candidate (lambda only
+//                       decays until the next arrival, so it still bounds it).  The
+//                       reference keeps the stale bound: the same point process (law),
+//                       a different draw sequence and more candidates per arrival.
 //   PiecewiseConst      opt_model.py:642-663 -- thinning of exponential gaps at the
 //                       max rate; two draws per candidate
 //   RealData            opt_model.py:722-750 -- the given (host-filtered) times
@@ -91,8 +92,15 @@ struct SrcGen {
             else done = true;
             p0 = mx;
         } else if (kind == RQ_SRC_REALDATA) {
-            na = a.arr_n[j];
-            ta = a.arr_a + a.arr_off[j];
+            const int rk = (a.rd_k && !is_ctrl) ? a.rd_k[j] : -1;
+            if (rk >= 0) {   // this replica's own times (a registered static broadcaster)
+                const int64_t o = a.rd_off[i * a.n_rd + rk];
+                na = (int)(a.rd_off[i * a.n_rd + rk + 1] - o);
+                ta = a.rd_times + o;
+            } else {
+                na = a.arr_n[j];
+                ta = a.arr_a + a.arr_off[j];
+            }
             done = na <= 0;
         } else {
             done = true;   // the controlled slot of an Opt / wall-only run: no stream

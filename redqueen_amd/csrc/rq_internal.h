@@ -27,6 +27,11 @@ struct GenArgs {
     double* streams;
     int* slen;
     int32_t* status;
+    // per-replica RealData times (rq_batch_desc.rd_*): stream j -> source k or -1
+    const int* rd_k;
+    int n_rd;
+    const double* rd_times;
+    const int64_t* rd_off;
 };
 
 #define RQ_MAX_STREAMS 512

@@ -24,15 +24,26 @@ def _arr(x, dt):
     return np.ascontiguousarray(np.asarray(x, dtype=dt))
 
 
-def _source_kind(name):
+def _source_class(name):
+    """The class behind an other_sources entry: a built-in name, a name registered
+    with SimOpts.registerSource (opt_model.py:768-771), or a callable."""
     if isinstance(name, str):
-        if name not in KIND_BY_NAME:
+        if name in KIND_BY_NAME:
+            return None
+        from .opt_model import SimOpts
+        cls = SimOpts.broadcasters.get(name)
+        if cls is None:
             raise ValueError("Unknown type of broadcaster: {}".format(name))
+        return cls
+    return name
+
+
+def _source_kind(name):
+    if isinstance(name, str) and name in KIND_BY_NAME:
         return KIND_BY_NAME[name]
-    kind = getattr(name, "_rq_kind", None)
-    if kind is None:
-        raise NotImplementedError("broadcaster %r has no engine kernel" % (name,))
-    return kind
+    cls = _source_class(name)
+    kind = getattr(cls, "_rq_kind", None)
+    return L.SRC_REALDATA if kind is None else kind   # a plugin: its times as RealData
 
 
 class Graph:
@@ -43,8 +54,19 @@ class Graph:
         self._keep = []
         srcs = []
         self.has_realdata = False
-        for name, kw in other_sources:
+        # registered static plugin broadcasters: (position in other_sources, class, kwargs)
+        self.plugins = []
+        for idx, (name, kw) in enumerate(other_sources):
             kind = _source_kind(name)
+            cls = _source_class(name)
+            if cls is not None and getattr(cls, "_rq_kind", None) is None:
+                # graph-level times: the instance its own kwargs make (the seed as given);
+                # randomized batches replace them per replica (run(randomize=True))
+                from .opt_model import plugin_times
+                self.plugins.append((idx, cls, dict(kw), int(kw["src_id"])))
+                kw = {"src_id": kw["src_id"],
+                      "times": plugin_times(cls(**kw), float(start_time), sink_ids, edge_list,
+                                            float(end_time))}
             self.has_realdata = self.has_realdata or kind == L.SRC_REALDATA
             if kind == L.SRC_OPT:
                 raise NotImplementedError("an Opt broadcaster among the other sources")
@@ -78,6 +100,7 @@ class Graph:
         self.start_time = float(start_time)
         self.sink_ids = _arr(sink_ids, np.int64)
         edges = list(edge_list)
+        self._edges = edges
         self.edge_src = _arr([e[0] for e in edges], np.int64)
         self.edge_sink = _arr([e[1] for e in edges], np.int64)
         arr = (L.SourceDesc * max(1, len(srcs)))(*srcs)
@@ -200,6 +223,8 @@ class Graph:
         else:
             b.world_seed0 = int(world_seed) & 0xFFFFFFFF
         b.seed_mod = int(seed_mod)
+        if self.plugins and randomize:
+            self._plugin_streams(b, keep, dev, R_all, int(replica0), R, world_seed, int(seed_mod))
         if ck == L.SRC_POISSON2:
             if ctrl_rate is None:
                 raise ValueError("ctrl_rate required for a Poisson controlled source")
@@ -275,6 +300,39 @@ class Graph:
             if b.cap_scale > 64:
                 raise L.RQError("rq_run_batch", L.RQ_EOVERFLOW)
             b.cap_scale = b.cap_scale * 2.0
+
+    def _plugin_streams(self, b, keep, dev, R_all, replica0, R, world_seed, seed_mod):
+        """Per-replica times of the registered static broadcasters of a randomized
+        batch: replica i's instance gets seed u_i + 99 idx (randomize_other_sources,
+        opt_model.py:795-804) and the host runs its initialize() / get_all_times();
+        the times reach the kernels as per-replica RealData streams (rq_batch_desc.rd_*)."""
+        from .opt_model import plugin_times
+        wseed = world_seed.to(torch.int64).cpu().numpy() if torch.is_tensor(world_seed) else None
+        nrd = len(self.plugins)
+        if nrd > L.MAX_RD:
+            raise NotImplementedError("more than %d plugin broadcasters" % L.MAX_RD)
+        counts = np.zeros((R_all, nrd), dtype=np.int64)
+        chunks = []
+        for i in range(replica0, replica0 + R):
+            k = i % seed_mod if seed_mod > 0 else i
+            u = int(wseed[i]) if wseed is not None else int(world_seed) + k
+            for c, (idx, cls, kw, _sid) in enumerate(self.plugins):
+                t = plugin_times(cls(**dict(kw, seed=(u + 99 * idx) & 0xFFFFFFFF)), self.start_time,
+                                 self.sink_ids, self._edges, self.end_time)
+                counts[i, c] = t.size
+                chunks.append(t)
+        off = np.concatenate([[0], np.cumsum(counts.ravel())]).astype(np.int64)
+        times = np.concatenate(chunks) if chunks else np.zeros(0)
+        td = torch.from_numpy(np.ascontiguousarray(np.concatenate([times, [0.0]]))).to(dev)
+        to = torch.from_numpy(off).to(dev)
+        sid = _arr([p[3] for p in self.plugins], np.int64)
+        cap = _arr(counts.max(0) if R_all else np.zeros(nrd), np.int64)
+        keep += [td, to, sid, cap]
+        b.n_rd = nrd
+        b.rd_src_id = sid.ctypes.data_as(L._pi64)
+        b.rd_cap = cap.ctypes.data_as(L._pi64)
+        b.rd_times = td.data_ptr()
+        b.rd_off = to.data_ptr()
 
     def _plan_variant(self, lib, b):
         info = (C.c_int64 * 8)()

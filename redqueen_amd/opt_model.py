@@ -116,23 +116,63 @@ class State:
 
 # ----------------------------------------------------------------- broadcasters
 class Broadcaster:
-    """Parameter holder; the arrival process runs in the engine kernels."""
+    """Base of every broadcaster (opt_model.py:323-378).
+
+    The built-in kinds are parameter holders: their arrival processes are the
+    engine's kernels.  A class a user registers with ``SimOpts.registerSource``
+    keeps the reference's plugin contract: ``__init__(src_id, seed, ...)`` gets
+    ``self.random_state = RandomState(seed)``; a STATIC one (``is_dynamic =
+    False``) implements ``initialize()`` and ``get_all_times()`` after
+    ``init_state(start_time, all_sink_ids, follower_sink_ids, end_time)``.  The host
+    calls them (once per run, or once per replica of a randomized batch) and the
+    times play as RealData-kind streams on the GPU.  A DYNAMIC plugin
+    (``get_next_interval`` queried on every event) has no kernel: running one
+    raises NotImplementedError (RQ_EUNSUPPORTED)."""
     _rq_kind = None
 
     def __init__(self, src_id, seed):
         self.src_id = src_id
         self.seed = seed
+        self.random_state = np.random.RandomState(seed)
+        self.t_delta = None
+        self.end_time = None
+        self.last_self_event_time = None
         self.used = False
         self.is_dynamic = True
 
     def is_fresh(self):
         return not self.used
 
+    def init_state(self, start_time, all_sink_ids, follower_sink_ids, end_time):
+        self.sink_ids = sorted(follower_sink_ids)
+        self.state = State(start_time, all_sink_ids)
+        self.start_time = start_time
+        self.end_time = end_time
+
+    def get_all_times(self):
+        assert not self.is_dynamic
+        raise NotImplementedError()
+
     def get_next_interval(self, event):  # pragma: no cover - engine-side
         raise NotImplementedError("arrival processes run in librq.so (gfx950)")
 
     def _kwargs(self):
         return {"src_id": self.src_id, "seed": self.seed}
+
+
+def plugin_times(obj, start_time, sink_ids, edge_list, end_time):
+    """Times of a registered static broadcaster instance, as run_dynamic collects
+    them (init_state + initialize + get_all_times, opt_model.py:256-264), sorted and
+    clipped to [start_time, end_time] (events past end_time never play)."""
+    if getattr(obj, "is_dynamic", True):
+        raise NotImplementedError(
+            "broadcaster %s is dynamic (get_next_interval per event): only static plugin "
+            "broadcasters run on the GPU engine (RQ_EUNSUPPORTED)" % type(obj).__name__)
+    followers = [e[1] for e in edge_list if e[0] == obj.src_id]
+    obj.init_state(start_time, list(sink_ids), followers, end_time)
+    obj.initialize()
+    t = np.sort(np.asarray(obj.get_all_times(), dtype=np.float64).ravel())
+    return t[(t >= start_time) & (t <= end_time)]
 
 
 class Poisson(Broadcaster):
@@ -305,7 +345,7 @@ class Manager:
         ctrl = self._controlled()
         others = [s for s in self.sources if s is not ctrl]
         for s in others:
-            if s._rq_kind is None or s._rq_kind in (L.SRC_OPT, L.SRC_OPTPW):
+            if s._rq_kind in (L.SRC_OPT, L.SRC_OPTPW):
                 raise NotImplementedError("broadcaster %s has no engine kernel" %
                                           type(s).__name__)
         if ctrl is None:
@@ -313,7 +353,12 @@ class Manager:
             ctrl_id = min(ids) - 1
         else:
             ctrl_id = ctrl.src_id
-        other_desc = [(type(s).__name__, s._kwargs()) for s in others]
+        # registered plugin broadcasters: their own initialize() / get_all_times()
+        other_desc = [(type(s).__name__, s._kwargs()) if s._rq_kind is not None else
+                      ("RealData", {"src_id": s.src_id,
+                                    "times": plugin_times(s, self.start_time, self.sink_ids,
+                                                          self.edge_list, self.end_time)})
+                      for s in others]
         ctrl_a = ctrl_b = None
         if isinstance(ctrl, PiecewiseConst):
             ctrl_a, ctrl_b = ctrl.change_times, ctrl.rates

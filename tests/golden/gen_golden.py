@@ -29,6 +29,8 @@ installed and there is no network) and records, as plain data:
                    24-segment follower significance, randomized worlds)
   realdata.npz     all-RealData worlds (create_manager_with_times): the reference's whole
                    df (deterministic), its metrics and final State.time
+  plugin.npz       a registered static broadcaster (registerSource): df + metrics of the
+                   seeded world and of randomize_other_sources(u), u = 0..15
   sig_runs.npz     OptPWSignificance runs (notebook "Testing out significance",
                    opt_broadcast.ipynb:5469, :5569): events + metrics
   graphs.npz       opt_runs.make_edge_list networks (C3 parameters) and a
@@ -443,6 +445,37 @@ def gen_realdata():
     np.savez_compressed(os.path.join(HERE, "realdata.npz"), names=np.asarray(names), **rec)
 
 
+def gen_plugin():
+    """A registered static broadcaster (SimOpts.registerSource, opt_model.py:768-771)
+    in a deterministic world (RealData controlled): the df of the given seeds, and the
+    metrics of randomize_other_sources(u) for u in 0..15."""
+    from realdata_worlds import BurstyMixin, plugin_world
+    from redqueen.opt_model import Broadcaster
+
+    class Bursty(BurstyMixin, Broadcaster):
+        pass
+    SimOpts.registerSource("Bursty", Bursty)
+    w, ctrl, us = plugin_world()
+    so = SimOpts(**w)
+    rec = {}
+    m = so.create_manager_with_times(np.asarray(ctrl))
+    m.run_dynamic()
+    df = m.state.get_dataframe()
+    _df_cols(rec, "base", df)
+    met, own, world = metrics(df, so)
+    rec["base_met"], rec["base_cnt"] = met, np.asarray([own, world, len(df)])
+    mets, cnts = [], []
+    for u in us:
+        m = so.randomize_other_sources(u).create_manager_with_times(np.asarray(ctrl))
+        m.run_dynamic()
+        df = m.state.get_dataframe()
+        met, own, world = metrics(df, so)
+        mets.append(met)
+        cnts.append([own, world, m.state.get_num_events()])
+    rec["rand_met"], rec["rand_cnt"], rec["rand_u"] = np.asarray(mets), np.asarray(cnts), np.asarray(us)
+    np.savez_compressed(os.path.join(HERE, "plugin.npz"), **rec)
+
+
 def gen_sig():
     """OptPWSignificance (opt_model.py:547-623) via create_manager_with_significance
     (:850-884): the notebook cells opt_broadcast.ipynb:5469 and :5569 plus variants."""
@@ -627,7 +660,8 @@ if __name__ == "__main__":
     a = ap.parse_args()
     steps = {"npsum": gen_npsum, "draws": gen_draws, "readme": gen_readme, "kats": gen_kats,
              "adv": gen_adversarial, "graphs": gen_graphs, "frac": gen_frac,
-             "oracle": gen_oracle, "sweepq": gen_sweepq, "sig": gen_sig, "realdata": gen_realdata}
+             "oracle": gen_oracle, "sweepq": gen_sweepq, "sig": gen_sig, "realdata": gen_realdata,
+             "plugin": gen_plugin}
     if a.c3_dist:
         gen_c3_dist(a.c3_dist)
         print("done c3 dist", flush=True)

@@ -36,3 +36,38 @@ def realdata_worlds():
               edge_list=[(2, 1), (7, 1), (7, 2), (4, 2)])
     c3 = [1e-300, 0.1 + 1e-12, 0.7, 1.7]
     return [("rd1", w1, c1, None), ("rd2", w2, c2, None), ("rd2m", w2, c2, 17), ("rd3", w3, c3, None)]
+
+
+class BurstyMixin:
+    """A static plugin broadcaster (the SimOpts.registerSource contract,
+    opt_model.py:323-378, :768-771): N ~ Poisson(rate * T) burst centres, each with
+    `size` posts at centre + Exp(0.05), rounded to 1e-3 (so different sources post
+    at equal times).  Only numpy RandomState draws through self.random_state."""
+
+    def __init__(self, src_id, seed, rate=0.2, size=3):
+        super().__init__(src_id, seed)
+        self.rate, self.size = rate, size
+        self.is_dynamic = False
+        self.times = None
+
+    def initialize(self):
+        T = self.end_time - self.start_time
+        n = self.random_state.poisson(self.rate * T)
+        c = self.random_state.uniform(self.start_time, self.end_time, n)
+        off = self.random_state.exponential(0.05, (n, self.size))
+        self.times = np.round((c[:, None] + off).ravel(), 3)
+
+    def get_all_times(self):
+        return self.times
+
+
+def plugin_world():
+    """Two Bursty sources + a RealData controlled source (create_manager_with_times):
+    deterministic for given seeds; randomize_other_sources(u) reseeds the plugins."""
+    w = dict(src_id=4, end_time=30.0, s=1.0, q=1.0, sink_ids=[1, 2, 3, 4, 5, 6],
+             other_sources=[("Bursty", {"src_id": 2, "seed": 11, "rate": 0.3, "size": 3}),
+                            ("Bursty", {"src_id": 6, "seed": 12, "rate": 0.2, "size": 4})],
+             edge_list=[(2, 1), (2, 2), (2, 5), (6, 2), (6, 3), (6, 6), (4, 1), (4, 3), (4, 4),
+                        (4, 6)])
+    ctrl = [0.0, 1.5, 4.0, 9.25, 12.0, 20.0, 27.5]
+    return w, ctrl, list(range(16))
