@@ -77,7 +77,8 @@ def test_dynamic_plugin_is_unsupported():
         def get_next_interval(self, event):
             return 1.0
     SimOpts.registerSource("Chatty", Chatty)
-    w2 = dict(w, other_sources=[("Chatty", {"src_id": 2, "seed": 1})])
+    w2 = dict(w, other_sources=[("Chatty", {"src_id": 2, "seed": 1})],
+              edge_list=[e for e in w["edge_list"] if e[0] != 6])
     so = SimOpts(**w2)
     with pytest.raises(NotImplementedError):
         so.create_manager_with_times(np.asarray(ctrl)).run_dynamic()
