@@ -104,6 +104,7 @@ def main():
 
     from redqueen_amd import engine
     from redqueen_amd import _lib as L
+    from redqueen_amd import dist as D
     so, desc = workload(a.workload)
     g = engine.Graph(so["src_id"], so["other_sources"], so["sink_ids"], so["edge_list"],
                      so["end_time"])
@@ -124,7 +125,9 @@ def main():
             dist.all_reduce(evs)
             ev = evs[0]
             m = allm
-        means = m.mean(0)
+        # ensemble means in a fixed order (redqueen_amd.dist.grid_means): identical on
+        # every rank and for every GPU count
+        means = D.grid_means(m, 1, m.shape[0])[0]
         return res, means, ev
 
     # capacity check once at full size (overflow -> the engine reruns with doubled

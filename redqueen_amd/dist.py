@@ -31,22 +31,27 @@ def gather_rows(local, n_total, world=None, rank=None, group=None):
     rank = dist.get_rank(group) if rank is None else rank
     sizes = [shard(n_total, world, r)[1] - shard(n_total, world, r)[0] for r in range(world)]
     m = max(sizes)
-    pad = torch.zeros((m,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    pad[:local.shape[0]] = local
-    out = torch.empty((world * m,) + tuple(local.shape[1:]), dtype=local.dtype,
-                      device=local.device)
+    # gloo exchanges host tensors (a CPU-only or test group); nccl = RCCL over xGMI
+    dev = torch.device("cpu") if dist.get_backend(group) == "gloo" else local.device
+    pad = torch.zeros((m,) + tuple(local.shape[1:]), dtype=local.dtype, device=dev)
+    pad[:local.shape[0]] = local.to(dev)
+    out = torch.empty((world * m,) + tuple(local.shape[1:]), dtype=local.dtype, device=dev)
     dist.all_gather_into_tensor(out, pad, group=group)
-    return torch.cat([out[r * m:r * m + sizes[r]] for r in range(world)], 0)
+    return torch.cat([out[r * m:r * m + sizes[r]] for r in range(world)], 0).to(local.device)
 
 
 def grid_means(rows, n_grid, n_rep):
-    """Per-grid-point means of gathered rows [n_grid*n_rep, C], summed in replica
-    order (deterministic; independent of how the replicas were sharded)."""
+    """Per-grid-point means of gathered rows [n_grid*n_rep, C]: the replicas of a grid
+    point are summed by a fixed pairwise tree over replica order (halving; an odd
+    count carries its last element up), so the result depends only on the gathered
+    rows -- bit-identical however the replicas were sharded -- in log2(n_rep) launches."""
     x = rows.reshape(n_grid, n_rep, -1).to(torch.float64)
-    acc = torch.zeros((n_grid, x.shape[2]), dtype=torch.float64, device=x.device)
-    for r in range(n_rep):     # fixed order
-        acc += x[:, r]
-    return acc / n_rep
+    while x.shape[1] > 1:
+        n = x.shape[1]
+        h = n // 2
+        y = x[:, 0:2 * h:2] + x[:, 1:2 * h:2]
+        x = torch.cat([y, x[:, 2 * h:]], 1) if n % 2 else y
+    return x[:, 0] / n_rep
 
 
 def run_sharded(graph, n_grid, n_rep, world=None, rank=None, group=None, **run_kw):
