@@ -60,13 +60,15 @@ def cpu_baseline(so, n_threads, sample, Ks=(1,)):
     return sample / el, tot / el, el
 
 
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_c3_pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02_c3_pmc_summary.json")
 
 
 def pmc_traffic(workload, R, plan):
     """HBM bytes per sweep launch from the committed rocprofv3 PMC summary of this
     same command (scripts/gpu_pmc.sh -> scripts/pmc_summary.py: FETCH_SIZE x2 per
-    the gfx950 correction + WRITE_SIZE), when workload, replicas and plan match."""
+    the gfx950 correction + WRITE_SIZE), when workload, replicas and plan match AND
+    its build stamp is the loaded library's (librq.so + sources sha256)."""
+    from redqueen_amd import _lib as L
     try:
         d = json.load(open(PMC_SUMMARY))
     except (OSError, ValueError):
@@ -74,6 +76,9 @@ def pmc_traffic(workload, R, plan):
     meta = d.get("_meta", {})
     if meta.get("workload") != workload or meta.get("replicas") != R or \
             meta.get("variant") != plan["variant"]:
+        return None, None, None
+    stamp = L.build_stamp()
+    if any(meta.get(k) != v for k, v in stamp.items()):
         return None, None, None
     for k, v in d.items():
         if k.startswith("rq_sweep") and "hbm_write_bytes" in v and "hbm_read_bytes" in v:
@@ -117,18 +122,13 @@ def main():
         res = g.run("opt", q=so["q"], s=so["s"], n_rep=R, ctrl_seed=base, world_seed=base,
                     randomize=True, Ks=Ks, check=False)
         m = res.metrics
-        ev = res.counts[:, 2].sum()
         if world > 1:
             allm = torch.empty((world * R, m.shape[1]), dtype=m.dtype, device=dev)
             dist.all_gather_into_tensor(allm, m)       # RCCL over xGMI: the only exchange
-            evs = ev.reshape(1).clone()
-            dist.all_reduce(evs)
-            ev = evs[0]
             m = allm
-        # ensemble means in a fixed order (redqueen_amd.dist.grid_means): identical on
-        # every rank and for every GPU count
+        # ensemble means (redqueen_amd.dist.grid_means): identical on every rank
         means = D.grid_means(m, 1, m.shape[0])[0]
-        return res, means, ev
+        return res, means
 
     # capacity check once at full size (overflow -> the engine reruns with doubled
     # capacities; every launch of the run has the timed launches' shape, so a rocprofv3
@@ -137,23 +137,24 @@ def main():
     ok = g.run("opt", q=so["q"], s=so["s"], n_rep=R, ctrl_seed=0, world_seed=0,
                randomize=True, Ks=Ks, check=True)
     del ok
-    def accumulate(res, ev, acc):
-        acc[0] += ev
-        acc[1] += res.counts[:, 3].sum()
-        acc[2] += res.counts[:, 0].sum()
-        acc[3] |= (res.status & (L.ST_ROWS_OVERFLOW | L.ST_STREAM_OVERFLOW)).max()
+    mask = L.ST_ROWS_OVERFLOW | L.ST_STREAM_OVERFLOW
+
+    def accumulate(res, acc):
+        # per step: one reduction of the count columns, one of the overflow bits
+        acc[0] += res.counts.sum(0)
+        torch.maximum(acc[1], (res.status & mask).max(), out=acc[1])
 
     def new_acc():
-        return [torch.zeros((), dtype=torch.int64, device=dev) for _ in range(3)] + \
-            [torch.zeros((), dtype=torch.int32, device=dev)]
+        return [torch.zeros(4, dtype=torch.int64, device=dev),
+                torch.zeros((), dtype=torch.int32, device=dev)]
 
     # the warmup runs the exact timed body: HIP loads a kernel's code object on its first
     # launch (tens of ms for torch's), which must not land in the timed region
     L.lib().rq_timing(1)
     acc = new_acc()
     for k in range(max(1, a.warmup)):
-        res, means, ev = step(k + 10_000)
-        accumulate(res, ev, acc)
+        res, means = step(k + 10_000)
+        accumulate(res, acc)
     torch.cuda.synchronize()
 
     L.lib().rq_timing(1)
@@ -163,9 +164,9 @@ def main():
     t0 = time.perf_counter()
     acc = new_acc()
     for k in range(a.steps):
-        res, means, ev = step(k)
-        accumulate(res, ev, acc)
-    total_ev, rows, posts, status = acc
+        res, means = step(k)
+        accumulate(res, acc)
+    csum, status = acc
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -179,12 +180,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
 
-    local_ev = int(total_ev.item()) if world == 1 else None
-    rows_l, posts_l = int(rows.item()), int(posts.item())
-    if world > 1:
-        # total_ev already summed over ranks each step
-        local_ev = int(total_ev.item())
-    my_ev = int(res.counts[:, 2].sum().item())  # noqa: F841
+    rows_l, posts_l = int(csum[3].item()), int(csum[0].item())   # this rank
+    tot = csum.clone()
+    if world > 1:   # reporting only, after the timed region
+        dist.all_reduce(tot)
+    local_ev = int(tot[2].item())   # events of all ranks
     replicas = R * world * a.steps
     value = replicas / el
     ev_rate = local_ev / el

@@ -120,6 +120,25 @@ def lib():
     return L
 
 
+def build_stamp():
+    """Identity of the loaded engine build: sha256 of librq.so and of its sources
+    (csrc/ + include/rq.h).  Profiling summaries carry it, so a number measured on
+    another build is recognised as such (bench.py drops it)."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    with open(SO_PATH, "rb") as f:
+        h.update(f.read())
+    src = hashlib.sha256()
+    root = os.path.dirname(_HERE)
+    for fn in sorted(glob.glob(os.path.join(_HERE, "csrc", "*")) +
+                     [os.path.join(root, "include", "rq.h")]):
+        if os.path.isfile(fn):
+            with open(fn, "rb") as f:
+                src.update(os.path.basename(fn).encode() + b"\0" + f.read())
+    return {"librq_sha256": h.hexdigest()[:16], "csrc_sha256": src.hexdigest()[:16]}
+
+
 def strerror(code):
     try:
         return lib().rq_strerror(code).decode()

@@ -41,17 +41,12 @@ def gather_rows(local, n_total, world=None, rank=None, group=None):
 
 
 def grid_means(rows, n_grid, n_rep):
-    """Per-grid-point means of gathered rows [n_grid*n_rep, C]: the replicas of a grid
-    point are summed by a fixed pairwise tree over replica order (halving; an odd
-    count carries its last element up), so the result depends only on the gathered
-    rows -- bit-identical however the replicas were sharded -- in log2(n_rep) launches."""
+    """Per-grid-point means of gathered rows [n_grid*n_rep, C].  One reduction
+    launch: torch's sum over a dimension uses no atomics and a reduction order fixed
+    by the shape and device, so the result depends only on the gathered rows --
+    bit-identical on every rank and however the replicas were sharded."""
     x = rows.reshape(n_grid, n_rep, -1).to(torch.float64)
-    while x.shape[1] > 1:
-        n = x.shape[1]
-        h = n // 2
-        y = x[:, 0:2 * h:2] + x[:, 1:2 * h:2]
-        x = torch.cat([y, x[:, 2 * h:]], 1) if n % 2 else y
-    return x[:, 0] / n_rep
+    return x.sum(1) / n_rep
 
 
 def run_sharded(graph, n_grid, n_rep, world=None, rank=None, group=None, **run_kw):

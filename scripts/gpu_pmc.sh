@@ -21,4 +21,4 @@ timeout -k 10 -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES
 echo "sq1 ok"
 timeout -k 10 -s KILL 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT $P -d "$OUT/p2" -o p2 -- python3 $B > "$OUT/p2.log" 2>&1 || { echo p2 failed; tail -5 "$OUT/p2.log"; exit 1; }
 echo "sq2 ok"
-python3 scripts/pmc_summary.py "$OUT" > "$OUT/summary.txt" && cat "$OUT/summary.txt"
+python3 scripts/pmc_summary.py "$OUT" workload=c3 replicas=10000 variant=12 "command=scripts/gpu_pmc.sh $TAG ($B)" > "$OUT/summary.txt" && cat "$OUT/summary.txt"

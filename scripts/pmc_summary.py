@@ -6,7 +6,11 @@ each counter per dispatch, plus VGPR/SGPR/LDS of the code object and the
 corrected HBM bytes (FETCH_SIZE is in KiB and counts a 128-B read as 64 B on
 gfx950 -> x2; WRITE_SIZE in KiB, exact for wide stores; MI355X_MICROARCH.md
 'HBM / rocprofv3').  Writes summary.json beside the CSVs.
-usage: python scripts/pmc_summary.py DIR
+usage: python scripts/pmc_summary.py DIR [key=value ...]
+The key=value pairs (workload=c3 replicas=10000 variant=12 command=...) and the
+engine build stamp (redqueen_amd._lib.build_stamp: librq.so + sources sha256) go
+into summary.json's "_meta"; bench.py uses a summary only when the stamp matches
+the library it has loaded.
 """
 import collections
 import csv
@@ -42,7 +46,27 @@ for k, rs in rows.items():
         info["frac_wait_any"] = d.get("SQ_WAIT_ANY", 0) / wc
         info["frac_wait_inst"] = d.get("SQ_WAIT_INST_ANY", 0) / wc
     out[k] = info
+meta = {}
+for kv in sys.argv[2:]:
+    k, v = kv.split("=", 1)
+    meta[k] = int(v) if v.isdigit() else v
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+try:
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "rqlib", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                              "redqueen_amd", "_lib.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    meta.update(mod.build_stamp())
+except Exception as e:  # noqa: BLE001 -- a summary without a stamp is never used by bench.py
+    meta["stamp_error"] = str(e)
+meta["correction"] = ("hbm_read_bytes = FETCH_SIZE KiB x1024 x2 (gfx950: 128-B reads tallied at "
+                      "64 B; calibrated for 4/8/16 B per lane by scripts/micro/fetch_calib.hip); "
+                      "hbm_write_bytes = WRITE_SIZE KiB x1024")
+out["_meta"] = meta
 json.dump(out, open(os.path.join(root, "summary.json"), "w"), indent=1)
+print("_meta", json.dumps(meta))
 for k, v in out.items():
     if k.startswith("rq_"):
         print(k, json.dumps({a: b for a, b in v.items() if a != "counters"}))
