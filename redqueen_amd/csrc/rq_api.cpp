@@ -304,22 +304,24 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
             const int spl = p->spl;
             int only_w = 0;
             if (const char* e = getenv("RQ_G_W")) only_w = atoi(e);   // tuning only
-            for (int W : {16, 8, 4, 2}) {
-                if (p->log && W != 8) continue;
-                if (p->bl ? W == 16 : W <= 4) continue;   // BL instances: W in {8, 4, 2}
+            // LOG: LDS rings of W = 8 per source; the fast sweep: a register window of 4
+            for (int W : {8, 4}) {
+                if (p->log != (W == 8)) continue;
                 if (only_w && W != only_w) continue;
                 const size_t r_off = align_up(8 * (size_t)g->n_str, 16);
                 const size_t rank_b = p->log ? 4 : (p->bits ? 0 : 2);   // fast: int16 saturating
                 // BL: two bits per sink (T, V words) in place of the int16 ranks
                 const size_t w_off = p->bl ? align_up(r_off + 8 * (size_t)nwl, 16)
                                            : align_up(r_off + rank_b * (size_t)p->n_sinks_pad, 16);
-                // rings: W arrivals for each real source (lanes past n_str own none)
-                size_t stride = align_up(w_off + 8 * (size_t)g->n_str * W, 16);
+                // LOG: rings of W arrivals for each real source; fast: the tile's staging
+                size_t stride = p->log ? align_up(w_off + 8 * (size_t)g->n_str * W, 16)
+                                       : align_up(w_off + 64 * 12, 16);
                 // LOG: per-sink gtag/gcnt/gsum + a wave_npsum<1> scratch (304 doubles)
                 const size_t x_off = stride;
                 if (p->log) stride = align_up(x_off + 12 * (size_t)p->n_sinks_pad + 8 * 304, 16);
                 for (int wpb : {16, 12, 10, 8, 6, 5, 4, 3, 2, 1}) {
                     if (p->log && wpb > 4) continue;   // LOG instances: 256-thread blocks
+                    if (!p->log && spl >= 4 && wpb > 8) continue;   // 512-thread instances
                     const size_t tot = sh + wpb * stride;
                     if (tot > kLdsMax) continue;
                     // resident waves per CU: the runtime's occupancy for this instance
@@ -327,8 +329,8 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
                     int blocks = rq_sweep_blocks_per_cu(spl, p->nK, c16, W, p->log, p->bl ? 2 : p->bits, wpb, tot);
                     if (blocks <= 0) blocks = (int)std::min<size_t>(kLdsMax / tot, 16 / wpb);
                     const int waves = blocks * wpb;
-                    // W=16 refills half as often; LDS columns skip the global latency
-                    const int score = waves * 8 + col_lds * 2 + (W == 16 ? 1 : 0);
+                    // LDS columns skip the global latency
+                    const int score = waves * 8 + col_lds * 2;
                     if (score > best) {
                         best = score;
                         p->gwin = W; p->gwpb = wpb; p->gcol_lds = col_lds; p->gcol16 = c16;

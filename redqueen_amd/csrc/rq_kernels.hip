@@ -106,7 +106,7 @@ __global__ __launch_bounds__(256) void rq_gen_streams(GenArgs a)
 //    LOG = the event log / max_events variant: phase C goes event by event.
 // ============================================================================
 template <int SPL, int NK, class COL, int W, bool LOG, bool BITS, bool BL>
-__global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
+__global__ __launch_bounds__(LOG ? 256 : (SPL >= 4 ? 512 : 1024)) void rq_sweep(SweepArgs a)
 {
     extern __shared__ double lds_g[];
     char* base = reinterpret_cast<char*>(lds_g);
@@ -169,11 +169,19 @@ __global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
         for (int c = lane; c < a.n_sinks; c += 64) rank[c] = -1;   // NaN: no row yet
     wave_lds_sync();
 
-    // ---- arrival rings: lane owns sources [lane*SPL, lane*SPL+SPL) ----
+    // ---- arrivals: lane owns sources [lane*SPL, lane*SPL+SPL) ----
     const double* st = a.streams + rl * a.capsum;
     const int* slen = a.slen + rl * a.n_str;
     double head[SPL];
     int pos[SPL], fil[SPL], len[SPL], off[SPL];
+    // fast sweep: a register window of each source's next W arrivals (INF past its
+    // end), reloaded from the stream buffer only for the sources a tile advanced
+    constexpr int HW = LOG ? 1 : W;
+    double wv[SPL][HW];
+    auto load_win = [&](int q) __attribute__((always_inline)) {
+#pragma unroll
+        for (int h = 0; h < HW; ++h) wv[q][h] = pos[q] + h < len[q] ? st[off[q] + pos[q] + h] : RQ_INF;
+    };
 #pragma unroll
     for (int q = 0; q < SPL; ++q) {
         const int j = lane * SPL + q;
@@ -203,17 +211,25 @@ __global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
             fil[q] = nf;
         }
     };
-    refill();
     double lmin = RQ_INF;
     int larg = 0;
+    if constexpr (LOG) {
+        refill();
 #pragma unroll
-    for (int q = 0; q < SPL; ++q) {
-        head[q] = len[q] > 0 ? win[(lane * SPL + q) * W] : RQ_INF;
-        if (head[q] < lmin) {
-            lmin = head[q];
-            larg = q;
+        for (int q = 0; q < SPL; ++q) {
+            head[q] = len[q] > 0 ? win[(lane * SPL + q) * W] : RQ_INF;
+            if (head[q] < lmin) {
+                lmin = head[q];
+                larg = q;
+            }
         }
+    } else {
+#pragma unroll
+        for (int q = 0; q < SPL; ++q) load_win(q);
     }
+    double span = -1.0;   // fast sweep: adaptive tile width in time (< 0: not estimated yet)
+    double* st_t = reinterpret_cast<double*>(win);   // fast sweep: tile staging (64 t + 64 j)
+    int* st_j = reinterpret_cast<int*>(st_t + 64);
 
     const bool opt = a.ctrl_kind == RQ_SRC_OPT || a.ctrl_kind == RQ_SRC_OPTPW;
     const double* pwc = a.pw_c ? a.pw_c + (size_t)g * a.n_str * a.n_seg : nullptr;
@@ -284,7 +300,132 @@ __global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
         // ---- A: the next <= 64 arrivals (t <= end) in (t, source) order; lane n holds #n ----
         double tt = RQ_INF;
         int tj = 0, n = 0;
-        while (n < 64) {
+        bool fin_w = false;
+        if constexpr (!LOG) {
+            // windowed: every arrival before a cut tau, tau < the W-th pending arrival of
+            // every source that has more (so the tile is complete) and tuned so the tile
+            // holds <= 64; staged in source order, rank-sorted into (t, source) order --
+            // the reference's (time, src_id) order (opt_model.py:279-281)
+            double lb = RQ_INF;
+            lmin = RQ_INF;
+#pragma unroll
+            for (int q = 0; q < SPL; ++q) {
+                lmin = wv[q][0] < lmin ? wv[q][0] : lmin;
+                if (pos[q] + W < len[q] && wv[q][W - 1] < lb) lb = wv[q][W - 1];
+            }
+            const double tfirst = wave_min_f64(lmin);
+            if (!(tfirst <= a.end)) break;   // every source consumed
+            const double tmax = wave_min_f64(lb);
+            int cq[SPL];
+            int c = 0;
+            bool trunc = !(tmax > tfirst);
+            if (!trunc) {
+                double cut = tmax;
+                if (span > 0.0 && tfirst + span < cut) cut = tfirst + span;
+                if (!(cut > tfirst)) cut = next_up(tfirst);
+                for (;;) {
+                    c = 0;
+#pragma unroll
+                    for (int q = 0; q < SPL; ++q) {
+                        cq[q] = 0;
+#pragma unroll
+                        for (int h = 0; h < W; ++h) cq[q] += wv[q][h] < cut ? 1 : 0;
+                        c += cq[q];
+                    }
+                    n = (int)wave_sum_u32((uint32_t)c);
+                    if (n <= 64) break;
+                    const double nc = tfirst + (cut - tfirst) * 0.5;
+                    const double lo = next_up(tfirst);
+                    if (nc > tfirst && nc < cut) {
+                        cut = nc < lo ? lo : nc;
+                    } else if (cut != lo) {
+                        cut = lo;
+                    } else {
+                        trunc = true;   // > 64 arrivals share tfirst
+                        break;
+                    }
+                }
+                if (!trunc) span = (cut - tfirst) * (a.tile_target / (double)(n > 8 ? n : 8));
+            }
+            int off_l;
+            if (trunc) {
+                // the arrivals equal to tfirst, in source order, up to the first source
+                // whose window may continue at tfirst, at most 64
+                int qb = SPL;   // this lane's first such source
+#pragma unroll
+                for (int q = SPL - 1; q >= 0; --q)
+                    if (pos[q] + W < len[q] && wv[q][W - 1] == tfirst) qb = q;
+                const uint64_t bl = __ballot(qb < SPL);
+                const int lbn = bl ? __ffsll((unsigned long long)bl) - 1 : 64;
+                c = 0;
+#pragma unroll
+                for (int q = 0; q < SPL; ++q) {
+                    cq[q] = 0;
+#pragma unroll
+                    for (int h = 0; h < W; ++h) cq[q] += wv[q][h] == tfirst ? 1 : 0;
+                    if (lane > lbn || (lane == lbn && q > qb)) cq[q] = 0;
+                    c += cq[q];
+                }
+                off_l = (int)wave_scan_add((uint32_t)c) - c;
+                int room = 64 - off_l;
+                c = 0;
+#pragma unroll
+                for (int q = 0; q < SPL; ++q) {
+                    room = room > 0 ? room : 0;
+                    cq[q] = cq[q] < room ? cq[q] : room;
+                    room -= cq[q];
+                    c += cq[q];
+                }
+                n = (int)wave_sum_u32((uint32_t)c);
+            } else {
+                off_l = (int)wave_scan_add((uint32_t)c) - c;
+            }
+            // stage in source order; rank = #staged arrivals before this one in (t, source)
+            // order, the staged times read back two at a time (broadcast ds_read_b128)
+            {
+                int k = off_l;
+#pragma unroll
+                for (int q = 0; q < SPL; ++q)
+#pragma unroll
+                    for (int h = 0; h < W; ++h)
+                        if (h < cq[q]) {
+                            st_t[k] = wv[q][h];
+                            st_j[k] = lane * SPL + q;
+                            ++k;
+                        }
+            }
+            wave_lds_sync();
+            const bool actw = lane < n;
+            const double ti = actw ? st_t[lane] : RQ_INF;
+            const int ji = actw ? st_j[lane] : 0;
+            int rnk = 0;
+            for (int q = 0; q < n; q += 2) {
+                const double2 tq = *reinterpret_cast<const double2*>(st_t + q);
+                rnk += (tq.x < ti || (tq.x == ti && q < lane)) ? 1 : 0;
+                rnk += (q + 1 < n && (tq.y < ti || (tq.y == ti && q + 1 < lane))) ? 1 : 0;
+            }
+            wave_lds_sync();
+            if (actw) {
+                st_t[rnk] = ti;
+                st_j[rnk] = ji;
+            }
+            wave_lds_sync();
+            tt = actw ? st_t[lane] : RQ_INF;
+            tj = actw ? st_j[lane] : 0;
+            wave_lds_sync();   // the staging area is rewritten by the next tile
+            // consume: sources the tile advanced reload their window
+            bool left = false;
+#pragma unroll
+            for (int q = 0; q < SPL; ++q) {
+                if (cq[q] > 0) {
+                    pos[q] += cq[q];
+                    load_win(q);
+                }
+                left = left || pos[q] < len[q];
+            }
+            fin_w = !__ballot(left);
+        }
+        while (LOG && n < 64) {
             const uint64_t key = order_key(lmin);
             const uint32_t khi = (uint32_t)(key >> 32), klo = (uint32_t)key;
             const uint32_t mhi = wave_min_u32(khi);
@@ -326,7 +467,7 @@ __global__ __launch_bounds__(LOG ? 256 : 1024) void rq_sweep(SweepArgs a)
                 }
             }
         }
-        const bool fin = n < 64;
+        const bool fin = LOG ? n < 64 : fin_w;
         const bool act = lane < n;
         int e0 = 0, e1 = 0, od = 0;
         if (act) {
@@ -1090,27 +1231,19 @@ static hipError_t launch_sweep_k(const SweepArgs& a, int nK, hipStream_t s)
     }
 }
 
+// the fast general sweep: a register window of W = 4 arrivals per source
+constexpr int kGW = 4;
 template <int SPL>
 static hipError_t launch_sweep_c(const SweepArgs& a, int nK, int col16, int bits, hipStream_t s)
 {
     if constexpr (SPL >= 2)
-        if (bits == 2) {   // K = 1 on per-wave LDS sink bits (> 64 sources): W in {8, 4, 2}
-            if (a.win == 2)
-                return col16 ? launch_sweep_t<SPL, 1, uint16_t, 2, false, false, true>(a, s)
-                             : launch_sweep_t<SPL, 1, int, 2, false, false, true>(a, s);
-            return a.win == 8 ? (col16 ? launch_sweep_t<SPL, 1, uint16_t, 8, false, false, true>(a, s)
-                                       : launch_sweep_t<SPL, 1, int, 8, false, false, true>(a, s))
-                              : (col16 ? launch_sweep_t<SPL, 1, uint16_t, 4, false, false, true>(a, s)
-                                       : launch_sweep_t<SPL, 1, int, 4, false, false, true>(a, s));
-        }
+        if (bits == 2)   // K = 1 on per-wave LDS sink bits (> 64 sources)
+            return col16 ? launch_sweep_t<SPL, 1, uint16_t, kGW, false, false, true>(a, s)
+                         : launch_sweep_t<SPL, 1, int, kGW, false, false, true>(a, s);
     if (bits)   // K = 1 on sink bitsets
-        return a.win == 16 ? launch_sweep_t<SPL, 1, uint16_t, 16, false, true>(a, s)
-                           : launch_sweep_t<SPL, 1, uint16_t, 8, false, true>(a, s);
-    if (a.win == 16)
-        return col16 ? launch_sweep_k<SPL, uint16_t, 16, false>(a, nK, s)
-                     : launch_sweep_k<SPL, int, 16, false>(a, nK, s);
-    return col16 ? launch_sweep_k<SPL, uint16_t, 8, false>(a, nK, s)
-                 : launch_sweep_k<SPL, int, 8, false>(a, nK, s);
+        return launch_sweep_t<SPL, 1, uint16_t, kGW, false, true>(a, s);
+    return col16 ? launch_sweep_k<SPL, uint16_t, kGW, false>(a, nK, s)
+                 : launch_sweep_k<SPL, int, kGW, false>(a, nK, s);
 }
 
 hipError_t rq_launch_gen(const GenArgs& a, hipStream_t s)
@@ -1164,21 +1297,13 @@ static int occ_k(int nK, int wpb, size_t lds)
 template <int SPL>
 static int occ_c(int nK, int col16, int W, int bits, int wpb, size_t lds)
 {
+    (void)W;
     if constexpr (SPL >= 2)
-        if (bits == 2) {
-            if (W == 2)
-                return col16 ? occ_t<SPL, 1, uint16_t, 2, false, false, true>(wpb, lds)
-                             : occ_t<SPL, 1, int, 2, false, false, true>(wpb, lds);
-            return W == 8 ? (col16 ? occ_t<SPL, 1, uint16_t, 8, false, false, true>(wpb, lds)
-                                   : occ_t<SPL, 1, int, 8, false, false, true>(wpb, lds))
-                          : (col16 ? occ_t<SPL, 1, uint16_t, 4, false, false, true>(wpb, lds)
-                                   : occ_t<SPL, 1, int, 4, false, false, true>(wpb, lds));
-        }
-    if (bits)
-        return W == 16 ? occ_t<SPL, 1, uint16_t, 16, false, true>(wpb, lds)
-                       : occ_t<SPL, 1, uint16_t, 8, false, true>(wpb, lds);
-    if (W == 16) return col16 ? occ_k<SPL, uint16_t, 16, false>(nK, wpb, lds) : occ_k<SPL, int, 16, false>(nK, wpb, lds);
-    return col16 ? occ_k<SPL, uint16_t, 8, false>(nK, wpb, lds) : occ_k<SPL, int, 8, false>(nK, wpb, lds);
+        if (bits == 2)
+            return col16 ? occ_t<SPL, 1, uint16_t, kGW, false, false, true>(wpb, lds)
+                         : occ_t<SPL, 1, int, kGW, false, false, true>(wpb, lds);
+    if (bits) return occ_t<SPL, 1, uint16_t, kGW, false, true>(wpb, lds);
+    return col16 ? occ_k<SPL, uint16_t, kGW, false>(nK, wpb, lds) : occ_k<SPL, int, kGW, false>(nK, wpb, lds);
 }
 int rq_sweep_blocks_per_cu(int spl, int nK, int col16, int W, int log, int bits, int wpb, size_t lds)
 {
