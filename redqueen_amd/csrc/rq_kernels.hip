@@ -162,7 +162,7 @@ __global__ __launch_bounds__(LOG ? 256 : (SPL >= 4 ? 512 : 1024)) void rq_sweep(
     AggL agl;
     if (BL) {
         uint32_t* tb = reinterpret_cast<uint32_t*>(wb + a.lds_rank_off);
-        agl.init(tb, tb + a.nwl, fbl, a.nwl, lane);
+        agl.init(tb, tb + a.nwl, fbl, a.nwl, lane, a.n_sinks);
     }
     for (int j = lane; j < a.n_str; j += 64) invc[j] = a.inv_c[(int64_t)g * a.n_str + j];
     if (!BITS && !BL)
@@ -581,21 +581,29 @@ __global__ __launch_bounds__(LOG ? 256 : (SPL >= 4 ? 512 : 1024)) void rq_sweep(
                 wcnt[0] = wc0;
                 ocnt[0] = oc0;
             } else {
-              // event q + 1's first 128 sink columns are loaded while event q runs
-              int pa = 0, pb = 0;
-              if (n > 0) {
-                  const int f0 = bcast_i(e0, 0), f1 = bcast_i(e1, 0);
-                  pa = f0 + lane < f1 ? colat(f0 + lane) : 0;
-                  pb = f0 + 64 + lane < f1 ? colat(f0 + 64 + lane) : 0;
-              }
+              // the first 128 sink columns of events q + 1 .. q + PF are in flight while
+              // event q runs (global columns: an L2 round trip outlasts one event's work)
+              constexpr int PF = col_lds ? 1 : 4;
+              int pa[PF], pb[PF];
+              auto fetch = [&](int q, int& ra, int& rb) __attribute__((always_inline)) {
+                  ra = rb = 0;
+                  if (q < n) {
+                      const int f0 = bcast_i(e0, q), f1 = bcast_i(e1, q);
+                      ra = f0 + lane < f1 ? colat(f0 + lane) : 0;
+                      rb = f0 + 64 + lane < f1 ? colat(f0 + 64 + lane) : 0;
+                  }
+              };
+#pragma unroll
+              for (int d = 0; d < PF; ++d) fetch(d, pa[d], pb[d]);
               for (int q = 0; q < n; ++q) {
-                const int ca = pa, cb = pb;
+                const int ca = pa[0], cb = pb[0];
                 const int qe0 = bcast_i(e0, q), qe1 = bcast_i(e1, q);
-                if (q + 1 < n) {
-                    const int f0 = bcast_i(e0, q + 1), f1 = bcast_i(e1, q + 1);
-                    pa = f0 + lane < f1 ? colat(f0 + lane) : 0;
-                    pb = f0 + 64 + lane < f1 ? colat(f0 + 64 + lane) : 0;
+#pragma unroll
+                for (int d = 0; d + 1 < PF; ++d) {
+                    pa[d] = pa[d + 1];
+                    pb[d] = pb[d + 1];
                 }
+                fetch(q + PF, pa[PF - 1], pb[PF - 1]);
                 if ((ownm >> q) & 1ull) {
                     if (BL) agl.own(ag, lane);
                     else ag.own(rank, folat, a.n_fol, lane);

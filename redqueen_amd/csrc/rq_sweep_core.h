@@ -182,13 +182,15 @@ struct AggL {
     uint32_t* T;
     uint32_t* V;
     const uint32_t* F;
-    int nw;
-    __device__ __forceinline__ void init(uint32_t* T_, uint32_t* V_, const uint32_t* F_, int nw_, int lane)
+    int nw, nsink;
+    __device__ __forceinline__ void init(uint32_t* T_, uint32_t* V_, const uint32_t* F_, int nw_, int lane,
+                                         int nsink_ = 0x7fffffff)
     {
         T = T_;
         V = V_;
         F = F_;
         nw = nw_;
+        nsink = nsink_;
         for (int k = lane; k < nw; k += 64) {
             T[k] = 0u;
             V[k] = 0u;
@@ -199,6 +201,7 @@ struct AggL {
                                             int lane)
     {
         int dvalid = 0, dtop = 0;
+        const bool vfull = g.nvalid >= nsink;   // every sink seen: V is all ones, leave it
         for (int e = e0; e < e1; e += 128) {
             const int ea = e + lane, eb = e + 64 + lane;
             const bool acta = ea < e1, actb = eb < e1;
@@ -208,12 +211,12 @@ struct AggL {
             if (acta) {
                 const uint32_t bit = 1u << (ca & 31);
                 ta = atomicAnd(&T[ca >> 5], ~bit) & bit;
-                va = atomicOr(&V[ca >> 5], bit) & bit;
+                if (!vfull) va = atomicOr(&V[ca >> 5], bit) & bit;
             }
             if (actb) {
                 const uint32_t bit = 1u << (cb & 31);
                 tb = atomicAnd(&T[cb >> 5], ~bit) & bit;
-                vb = atomicOr(&V[cb >> 5], bit) & bit;
+                if (!vfull) vb = atomicOr(&V[cb >> 5], bit) & bit;
             }
             dvalid += popc(__ballot(va == 0u)) + popc(__ballot(vb == 0u));
             dtop += popc(__ballot(ta != 0u)) + popc(__ballot(tb != 0u));
