@@ -581,7 +581,97 @@ __global__ __launch_bounds__(LOG ? 256 : (SPL >= 4 ? 512 : 1024)) void rq_sweep(
                 wcnt[0] = wc0;
                 ocnt[0] = oc0;
             } else {
-              // the first 128 sink columns of events q + 1 .. q + PF are in flight while
+              if constexpr (BL) {
+                // batches of up to 8 wall events (no post inside, <= 128 sinks each): the
+                // batch's columns are loaded together, then every LDS atomic of the batch
+                // is issued back to back -- a wave's LDS operations complete in order, so
+                // each returns the T / V bits as of its own event's turn -- and counted
+                // after; one latency chain per batch instead of one per event
+                int wsl = 0, wsh = 0, osl = 0, osh = 0;
+                int q = 0;
+                while (q < n) {
+                    if ((ownm >> q) & 1ull) {
+                        agl.own(ag, lane);
+                        osl = writelane(osl, (int)(uint32_t)ag.sumR, q);
+                        osh = writelane(osh, (int)(ag.sumR >> 32), q);
+                        oval = writelane(oval, ag.nvalid, q);
+                        ocnt[0] = writelane(ocnt[0], ag.cnt[0], q);
+                    }
+                    const int jq = bcast_i(tj, q);
+                    const int d0 = bcast_i(e1, q) - bcast_i(e0, q);
+                    if ((!opt && jq == a.ctrl_idx) || d0 > 128 || a.dbg == 2) {
+                        // an own-stream arrival, or more than 128 sinks: one event alone
+                        if (!opt && jq == a.ctrl_idx) {
+                            agl.own(ag, lane);
+                        } else if (a.dbg != 2) {
+                            const int f0 = bcast_i(e0, q), f1 = bcast_i(e1, q);
+                            const int ca = f0 + lane < f1 ? colat(f0 + lane) : 0;
+                            const int cb = f0 + 64 + lane < f1 ? colat(f0 + 64 + lane) : 0;
+                            agl.wall_pf(ag, colat, ca, cb, f0, f1, bcast_i(od, q), lane);
+                        }
+                        wsl = writelane(wsl, (int)(uint32_t)ag.sumR, q);
+                        wsh = writelane(wsh, (int)(ag.sumR >> 32), q);
+                        wval = writelane(wval, ag.nvalid, q);
+                        wcnt[0] = writelane(wcnt[0], ag.cnt[0], q);
+                        ++q;
+                        continue;
+                    }
+                    int m = 1;
+                    while (m < 8 && q + m < n) {
+                        if ((ownm >> (q + m)) & 1ull) break;
+                        const int jm = bcast_i(tj, q + m);
+                        if ((!opt && jm == a.ctrl_idx) || bcast_i(e1, q + m) - bcast_i(e0, q + m) > 128) break;
+                        ++m;
+                    }
+                    int ca[8], cb[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        ca[k] = cb[k] = -1;
+                        if (k < m) {
+                            const int f0 = bcast_i(e0, q + k), f1 = bcast_i(e1, q + k);
+                            if (f0 + lane < f1) ca[k] = colat(f0 + lane);
+                            if (f0 + 64 + lane < f1) cb[k] = colat(f0 + 64 + lane);
+                        }
+                    }
+                    const bool vfull = ag.nvalid >= a.n_sinks;   // V all ones: leave it
+                    uint32_t ta[8], tb[8], va[8], vb[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        ta[k] = tb[k] = 0u;
+                        va[k] = vb[k] = 1u;
+                        if (k < m) {
+                            if (ca[k] >= 0) {
+                                const uint32_t bit = 1u << (ca[k] & 31);
+                                ta[k] = atomicAnd(&agl.T[ca[k] >> 5], ~bit) & bit;
+                                if (!vfull) va[k] = atomicOr(&agl.V[ca[k] >> 5], bit) & bit;
+                            }
+                            if (cb[k] >= 0) {
+                                const uint32_t bit = 1u << (cb[k] & 31);
+                                tb[k] = atomicAnd(&agl.T[cb[k] >> 5], ~bit) & bit;
+                                if (!vfull) vb[k] = atomicOr(&agl.V[cb[k] >> 5], bit) & bit;
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        if (k < m) {
+                            const int qk = q + k;
+                            ag.cnt[0] -= popc(__ballot(ta[k] != 0u)) + popc(__ballot(tb[k] != 0u));
+                            ag.nvalid += popc(__ballot(va[k] == 0u)) + popc(__ballot(vb[k] == 0u));
+                            ag.sumR += bcast_i(e1, qk) - bcast_i(e0, qk);
+                            ag.sumF += bcast_i(od, qk);
+                            wsl = writelane(wsl, (int)(uint32_t)ag.sumR, qk);
+                            wsh = writelane(wsh, (int)(ag.sumR >> 32), qk);
+                            wval = writelane(wval, ag.nvalid, qk);
+                            wcnt[0] = writelane(wcnt[0], ag.cnt[0], qk);
+                        }
+                    }
+                    q += m;
+                }
+                wsum = (int64_t)(((uint64_t)(uint32_t)wsh << 32) | (uint32_t)wsl);
+                osum = (int64_t)(((uint64_t)(uint32_t)osh << 32) | (uint32_t)osl);
+              } else {
+                // the first 128 sink columns of events q + 1 .. q + PF are in flight while
               // event q runs (global columns: an L2 round trip outlasts one event's work)
               constexpr int PF = col_lds ? 1 : 4;
               int pa[PF], pb[PF];
@@ -628,6 +718,7 @@ __global__ __launch_bounds__(LOG ? 256 : (SPL >= 4 ? 512 : 1024)) void rq_sweep(
 #pragma unroll
                     for (int kq = 0; kq < NK; ++kq) wcnt[kq] = ag.cnt[kq];
                 }
+              }
               }
             }
             const uint64_t mo = __ballot(has_o), ma = mo | __ballot(has_w);
