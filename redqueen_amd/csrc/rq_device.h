@@ -161,6 +161,11 @@ __device__ __forceinline__ void wave_sum_u32_n(uint32_t (&v)[N])
 
 // v into lane l (v, l uniform): v_cmp + v_cndmask
 __device__ __forceinline__ int writelane(int old, int v, int l) { return lane_id() == l ? v : old; }
+// the same with v_writelane_b32: v and l must be wave-uniform
+// (the LLVM intrinsic, which this clang has no builtin for; the backend moves the
+// lane select to m0 when both operands are SGPRs)
+__device__ int rq_llvm_writelane(int v, int l, int old) __asm("llvm.amdgcn.writelane");
+__device__ __forceinline__ int wlane(int old, int v, int l) { return rq_llvm_writelane(v, l, old); }
 
 // ---- DPP prefix scans (inclusive): row shifts 1, 2, 4, 8 then row broadcasts 15, 31.
 // A lane whose DPP source is out of its row (or whose row is masked off) reads 0,

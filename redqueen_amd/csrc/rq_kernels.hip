@@ -588,20 +588,28 @@ __global__ __launch_bounds__(LOG ? 256 : (SPL >= 4 ? 512 : 1024)) void rq_sweep(
                 // each returns the T / V bits as of its own event's turn -- and counted
                 // after; one latency chain per batch instead of one per event
                 int wsl = 0, wsh = 0, osl = 0, osh = 0;
+                // per tile: events that cannot join a batch -- an own-stream arrival, no
+                // sinks or more than 128 -- and the batch breaks (those, an own post
+                // before the event, the end of the tile)
+                const int degl = e1 - e0;
+                const uint64_t specm =
+                    __ballot(act && ((!opt && tj == a.ctrl_idx) || degl == 0 || degl > 128 || a.dbg == 2));
+                const uint64_t brk = specm | ownm | (n >= 64 ? 0ull : ~0ull << n);
+                // the word a lane with no sink in a batch slot touches with a no-op atomic
+                // (its own word: no same-address serialisation)
+                const int nopw = lane < agl.nw ? lane : 0;
                 int q = 0;
                 while (q < n) {
                     if ((ownm >> q) & 1ull) {
                         agl.own(ag, lane);
-                        osl = writelane(osl, (int)(uint32_t)ag.sumR, q);
-                        osh = writelane(osh, (int)(ag.sumR >> 32), q);
-                        oval = writelane(oval, ag.nvalid, q);
-                        ocnt[0] = writelane(ocnt[0], ag.cnt[0], q);
+                        osl = wlane(osl, (int)(uint32_t)ag.sumR, q);
+                        osh = wlane(osh, (int)(ag.sumR >> 32), q);
+                        oval = wlane(oval, ag.nvalid, q);
+                        ocnt[0] = wlane(ocnt[0], ag.cnt[0], q);
                     }
-                    const int jq = bcast_i(tj, q);
-                    const int d0 = bcast_i(e1, q) - bcast_i(e0, q);
-                    if ((!opt && jq == a.ctrl_idx) || d0 > 128 || a.dbg == 2) {
-                        // an own-stream arrival, or more than 128 sinks: one event alone
-                        if (!opt && jq == a.ctrl_idx) {
+                    if ((specm >> q) & 1ull) {
+                        // an own-stream arrival, or no / more than 128 sinks: one event alone
+                        if (!opt && bcast_i(tj, q) == a.ctrl_idx) {
                             agl.own(ag, lane);
                         } else if (a.dbg != 2) {
                             const int f0 = bcast_i(e0, q), f1 = bcast_i(e1, q);
@@ -609,63 +617,66 @@ __global__ __launch_bounds__(LOG ? 256 : (SPL >= 4 ? 512 : 1024)) void rq_sweep(
                             const int cb = f0 + 64 + lane < f1 ? colat(f0 + 64 + lane) : 0;
                             agl.wall_pf(ag, colat, ca, cb, f0, f1, bcast_i(od, q), lane);
                         }
-                        wsl = writelane(wsl, (int)(uint32_t)ag.sumR, q);
-                        wsh = writelane(wsh, (int)(ag.sumR >> 32), q);
-                        wval = writelane(wval, ag.nvalid, q);
-                        wcnt[0] = writelane(wcnt[0], ag.cnt[0], q);
+                        wsl = wlane(wsl, (int)(uint32_t)ag.sumR, q);
+                        wsh = wlane(wsh, (int)(ag.sumR >> 32), q);
+                        wval = wlane(wval, ag.nvalid, q);
+                        wcnt[0] = wlane(wcnt[0], ag.cnt[0], q);
                         ++q;
                         continue;
                     }
-                    int m = 1;
-                    while (m < 8 && q + m < n) {
-                        if ((ownm >> (q + m)) & 1ull) break;
-                        const int jm = bcast_i(tj, q + m);
-                        if ((!opt && jm == a.ctrl_idx) || bcast_i(e1, q + m) - bcast_i(e0, q + m) > 128) break;
-                        ++m;
-                    }
-                    int ca[8], cb[8];
+                    // events q .. q+m-1: no break after q, at most 8
+                    const uint64_t rest = (brk >> q) & ~1ull;
+                    int m = rest ? __builtin_ctzll(rest) : 64 - q;
+                    m = m < 8 ? m : 8;
+                    // straight-line batch: every slot loads and issues its atomics (slots
+                    // past m and lanes past the event's sinks: index 0, no-op masks), so the
+                    // compiler keeps the 16 loads and then the atomics in flight together
+                    auto batch = [&](auto vf) __attribute__((always_inline)) {
+                        constexpr bool VF = decltype(vf)::value;   // V all ones: leave it
+                        int ca[8], cb[8];
+                        bool aa[8], ab[8];
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        ca[k] = cb[k] = -1;
-                        if (k < m) {
-                            const int f0 = bcast_i(e0, q + k), f1 = bcast_i(e1, q + k);
-                            if (f0 + lane < f1) ca[k] = colat(f0 + lane);
-                            if (f0 + 64 + lane < f1) cb[k] = colat(f0 + 64 + lane);
+                        for (int k = 0; k < 8; ++k) {
+                            const int f0 = bcast_i(e0, q + k < 64 ? q + k : 63);
+                            const int f1 = k < m ? bcast_i(e1, q + k) : f0;
+                            aa[k] = f0 + lane < f1;
+                            ab[k] = f0 + 64 + lane < f1;
+                            ca[k] = colat(aa[k] ? f0 + lane : 0);
+                            cb[k] = colat(ab[k] ? f0 + 64 + lane : 0);
                         }
-                    }
-                    const bool vfull = ag.nvalid >= a.n_sinks;   // V all ones: leave it
-                    uint32_t ta[8], tb[8], va[8], vb[8];
+                        uint32_t ta[8], tb[8], va[8], vb[8];
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        ta[k] = tb[k] = 0u;
-                        va[k] = vb[k] = 1u;
-                        if (k < m) {
-                            if (ca[k] >= 0) {
-                                const uint32_t bit = 1u << (ca[k] & 31);
-                                ta[k] = atomicAnd(&agl.T[ca[k] >> 5], ~bit) & bit;
-                                if (!vfull) va[k] = atomicOr(&agl.V[ca[k] >> 5], bit) & bit;
+                        for (int k = 0; k < 8; ++k) {
+                            const uint32_t ba = aa[k] ? 1u << (ca[k] & 31) : 0u;
+                            const uint32_t bb = ab[k] ? 1u << (cb[k] & 31) : 0u;
+                            const int wa = aa[k] ? ca[k] >> 5 : nopw;
+                            const int wb = ab[k] ? cb[k] >> 5 : nopw;
+                            ta[k] = atomicAnd(&agl.T[wa], ~ba) & ba;
+                            tb[k] = atomicAnd(&agl.T[wb], ~bb) & bb;
+                            if (!VF) {
+                                va[k] = ba & ~atomicOr(&agl.V[wa], ba);
+                                vb[k] = bb & ~atomicOr(&agl.V[wb], bb);
                             }
-                            if (cb[k] >= 0) {
-                                const uint32_t bit = 1u << (cb[k] & 31);
-                                tb[k] = atomicAnd(&agl.T[cb[k] >> 5], ~bit) & bit;
-                                if (!vfull) vb[k] = atomicOr(&agl.V[cb[k] >> 5], bit) & bit;
+                        }
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) {
+                            if (k < m) {
+                                const int qk = q + k;
+                                ag.cnt[0] -= popc(__ballot(ta[k] != 0u)) + popc(__ballot(tb[k] != 0u));
+                                if (!VF) ag.nvalid += popc(__ballot(va[k] != 0u)) + popc(__ballot(vb[k] != 0u));
+                                ag.sumR += bcast_i(degl, qk);
+                                ag.sumF += bcast_i(od, qk);
+                                wsl = wlane(wsl, (int)(uint32_t)ag.sumR, qk);
+                                wsh = wlane(wsh, (int)(ag.sumR >> 32), qk);
+                                wval = wlane(wval, ag.nvalid, qk);
+                                wcnt[0] = wlane(wcnt[0], ag.cnt[0], qk);
                             }
                         }
-                    }
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        if (k < m) {
-                            const int qk = q + k;
-                            ag.cnt[0] -= popc(__ballot(ta[k] != 0u)) + popc(__ballot(tb[k] != 0u));
-                            ag.nvalid += popc(__ballot(va[k] == 0u)) + popc(__ballot(vb[k] == 0u));
-                            ag.sumR += bcast_i(e1, qk) - bcast_i(e0, qk);
-                            ag.sumF += bcast_i(od, qk);
-                            wsl = writelane(wsl, (int)(uint32_t)ag.sumR, qk);
-                            wsh = writelane(wsh, (int)(ag.sumR >> 32), qk);
-                            wval = writelane(wval, ag.nvalid, qk);
-                            wcnt[0] = writelane(wcnt[0], ag.cnt[0], qk);
-                        }
-                    }
+                    };
+                    if (ag.nvalid >= a.n_sinks)
+                        batch(std::true_type{});
+                    else
+                        batch(std::false_type{});
                     q += m;
                 }
                 wsum = (int64_t)(((uint64_t)(uint32_t)wsh << 32) | (uint32_t)wsl);
