@@ -60,7 +60,8 @@ def cpu_baseline(so, n_threads, sample, Ks=(1,)):
     return sample / el, tot / el, el
 
 
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02_c3_pmc_summary.json")
+def pmc_summary_path(workload):
+    return os.path.join(ROOT, "profiles", "r02_%s_pmc_summary.json" % workload)
 
 
 def pmc_traffic(workload, R, plan):
@@ -69,8 +70,9 @@ def pmc_traffic(workload, R, plan):
     the gfx950 correction + WRITE_SIZE), when workload, replicas and plan match AND
     its build stamp is the loaded library's (librq.so + sources sha256)."""
     from redqueen_amd import _lib as L
+    path = pmc_summary_path(workload)
     try:
-        d = json.load(open(PMC_SUMMARY))
+        d = json.load(open(path))
     except (OSError, ValueError):
         return None, None, None
     meta = d.get("_meta", {})
@@ -83,7 +85,7 @@ def pmc_traffic(workload, R, plan):
     for k, v in d.items():
         if k.startswith("rq_sweep") and "hbm_write_bytes" in v and "hbm_read_bytes" in v:
             issue = {q: v[q] for q in ("frac_active_inst", "frac_wait_any", "frac_wait_inst") if q in v}
-            return v["hbm_read_bytes"] + v["hbm_write_bytes"], os.path.relpath(PMC_SUMMARY, ROOT), issue
+            return v["hbm_read_bytes"] + v["hbm_write_bytes"], os.path.relpath(path, ROOT), issue
     return None, None, None
 
 
@@ -92,7 +94,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--replicas", type=int, default=10000, help="replicas per GPU per step")
+    # C5 default: two rounds of the 2048 waves the general sweep keeps resident
+    ap.add_argument("--replicas", type=int, default=0,
+                    help="replicas per GPU per step (default: C3/C2 10000, C5 4096)")
     ap.add_argument("--workload", default="c3")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=0)
@@ -113,7 +117,7 @@ def main():
     so, desc = workload(a.workload)
     g = engine.Graph(so["src_id"], so["other_sources"], so["sink_ids"], so["edge_list"],
                      so["end_time"])
-    R = a.replicas
+    R = a.replicas or (4096 if a.workload == "c5" else 10000)
     Ks = (1,)
     plan = g.run("opt", q=so["q"], s=so["s"], n_rep=R, randomize=True, Ks=Ks, plan_only=True)
 
@@ -211,11 +215,12 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
         nt = min(16, os.cpu_count() or 1)
-        sample = a.cpu_sample or 128 * nt
+        sample = a.cpu_sample or (2 if a.workload == "c5" else 128) * nt
         crate, cev, cel = cpu_baseline(so, nt, sample, Ks)
         cpu = {"value": crate, "unit": "replicas/s", "cores": nt, "kind": "port",
-               "sample": "%d C3 replicas through the C oracle (engine semantics + Appendix-B "
-                         "metrics), %d pthreads, %.1f s, %.0f events/s" % (sample, nt, cel, cev)}
+               "sample": "%d %s replicas through the C oracle (engine semantics + Appendix-B "
+                         "metrics), %d pthreads, %.1f s, %.0f events/s" %
+                         (sample, a.workload.upper(), nt, cel, cev)}
 
     if rank == 0:
         line = {
@@ -230,7 +235,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (Philox-seeded arrival streams on the reference's C3 network)",
+            "data": "synthetic (Philox-seeded arrival streams on the reference's %s network)" %
+                    a.workload.upper(),
             "config": {"workload": desc, "replicas_per_gpu": R, "global_batch": R * world,
                        "parallelism": "replica-sharded dp%d" % world, "Ks": list(Ks)},
             "events_per_sec": ev_rate,

@@ -514,12 +514,14 @@ __device__ void wave_npsum_rows(int64_t n, double end, LD&& ld, TLD&& tld, VF&& 
 #pragma unroll
             for (int s = 0; s < NV; ++s) r[s] = 0.0;
             const int lim = len - (len % 8);
-            for (int i = 0; i < lim; i += 32) {
-                const int nu = (lim - i) >> 3 < 4 ? (lim - i) >> 3 : 4;   // group-uniform
+            // a trip: up to TU rows per lane (8 TU per group), all loads in flight at once
+            constexpr int TU = 8;
+            for (int i = 0; i < lim; i += 8 * TU) {
+                const int nu = (lim - i) >> 3 < TU ? (lim - i) >> 3 : TU;   // group-uniform
                 const int64_t e0 = c0 + off + i + jj;
-                Row R[4];
+                Row R[TU];
 #pragma unroll
-                for (int u = 0; u < 4; ++u)
+                for (int u = 0; u < TU; ++u)
                     if (u < nu) R[u] = ld((uint32_t)(e0 + 8 * u));
                 double tx = end;
                 if constexpr (TNEXT) if (jj == 7) {
@@ -527,12 +529,12 @@ __device__ void wave_npsum_rows(int64_t n, double end, LD&& ld, TLD&& tld, VF&& 
                     if (ka < n) tx = tld((uint32_t)ka);
                 }
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
+                for (int u = 0; u < TU; ++u) {
                     if (u < nu) {
                         double tn = 0.0;
                         if constexpr (TNEXT) {
                             const double nb = dpp_shl1_f64(R[u].t);
-                            const double w7 = u + 1 < nu ? dpp_shr7_f64(R[u + 1 < 4 ? u + 1 : 3].t) : tx;
+                            const double w7 = u + 1 < nu ? dpp_shr7_f64(R[u + 1 < TU ? u + 1 : TU - 1].t) : tx;
                             tn = jj == 7 ? w7 : nb;
                         }
                         double v[NV];

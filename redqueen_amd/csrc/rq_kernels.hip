@@ -552,18 +552,18 @@ __global__ __launch_bounds__(LOG ? 256 : (SPL >= 4 ? 512 : 1024)) void rq_sweep(
                             if ((ownm >> q) & 1ull) {
                                 agb.own();
                                 agb.sync();
-                                osl = writelane(osl, (int)(uint32_t)agb.sumR, q);
-                                osh = writelane(osh, (int)(agb.sumR >> 32), q);
-                                oval = writelane(oval, agb.nvalid, q);
-                                oc0 = writelane(oc0, agb.cnt[0], q);
+                                osl = wlane(osl, (int)(uint32_t)agb.sumR, q);
+                                osh = wlane(osh, (int)(agb.sumR >> 32), q);
+                                oval = wlane(oval, agb.nvalid, q);
+                                oc0 = wlane(oc0, agb.cnt[0], q);
                             }
                             if (!opt && jk[k] == a.ctrl_idx)
                                 agb.own();
                             else
                                 agb.wall_m(m[k], bcast_i(deg, q), bcast_i(od, q));
                             pk[k] = agb.packed();
-                            wsl = writelane(wsl, (int)(uint32_t)agb.sumR, q);
-                            wsh = writelane(wsh, (int)(agb.sumR >> 32), q);
+                            wsl = wlane(wsl, (int)(uint32_t)agb.sumR, q);
+                            wsh = wlane(wsh, (int)(agb.sumR >> 32), q);
                         }
                     }
                     wave_sum_u32_n<8>(pk);
@@ -571,8 +571,8 @@ __global__ __launch_bounds__(LOG ? 256 : (SPL >= 4 ? 512 : 1024)) void rq_sweep(
                     for (int k = 0; k < 8; ++k) {
                         if (q0 + k < n) {
                             const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)pk[k], 63);
-                            wval = writelane(wval, (int)(tot >> 16), q0 + k);
-                            wc0 = writelane(wc0, (int)(tot & 0xFFFFu), q0 + k);
+                            wval = wlane(wval, (int)(tot >> 16), q0 + k);
+                            wc0 = wlane(wc0, (int)(tot & 0xFFFFu), q0 + k);
                         }
                     }
                 }
@@ -1104,7 +1104,7 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
                 const uint32_t u = sf.scan_or(m);                  // wall union since the segment start
                 const uint32_t tq = (hasr ? Fw : Tw) & ~u;         // top-1 set after #lane
                 cw += __popc(tq);
-                nT = (uint32_t)writelane((int)nT, __builtin_amdgcn_readlane((int)tq, last), ww);
+                nT = (uint32_t)wlane((int)nT, __builtin_amdgcn_readlane((int)tq, last), ww);
                 if (!vfull) {
                     const uint32_t Vw = (uint32_t)__builtin_amdgcn_readlane((int)agb.V, ww);
                     const uint32_t x = wave_scan_or(m);
@@ -1112,7 +1112,7 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
                     vw += __popc(vq);
                     const uint32_t xe = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xF, 0xF, false);
                     vo += __popc(Vw | xe | Fw);                     // after the post before #lane
-                    nV = (uint32_t)writelane((int)nV, __builtin_amdgcn_readlane((int)vq, last), ww);
+                    nV = (uint32_t)wlane((int)nV, __builtin_amdgcn_readlane((int)vq, last), ww);
                 }
             }
             wcnt[0] = cw;

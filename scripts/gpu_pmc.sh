@@ -1,15 +1,24 @@
 #!/bin/bash
 # PMC passes on the bench workload (one counter group per rocprofv3 run, as the
 # gfx950 slot limits require) + a kernel-trace pass; summary -> gpurun_out/pmc_TAG/summary.json
-# usage: scripts/gpu_pmc.sh TAG [bench args...]
+# usage: scripts/gpu_pmc.sh TAG [WORKLOAD [REPLICAS]]   (defaults c3 10000)
 set -o pipefail
-TAG=${1:-run}; shift
+TAG=${1:-run}
+WL=${2:-c3}
+R=${3:-$([ "$WL" = c5 ] && echo 4096 || echo 10000)}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/pmc_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd "$ROOT"
-B="bench.py --steps 3 --warmup 1 --no-cpu $*"
+B="bench.py --steps 3 --warmup 1 --no-cpu --workload $WL --replicas $R"
+# the sweep variant the plan picks (recorded with the counters; bench.py matches on it)
+V=$(timeout -k 10 120 python3 -c "
+import bench
+from redqueen_amd import engine
+so, _ = bench.workload('$WL')
+g = engine.Graph(so['src_id'], so['other_sources'], so['sink_ids'], so['edge_list'], so['end_time'])
+print(g.run('opt', q=so['q'], s=so['s'], n_rep=$R, randomize=True, plan_only=True)['variant'])") || { echo plan failed; exit 1; }
 P="--output-format csv"
 timeout -k 10 -s KILL 200 rocprofv3 --kernel-trace --stats $P -d "$OUT/kt" -o kt -- python3 $B > "$OUT/kt.log" 2>&1 || { echo kt failed; tail -5 "$OUT/kt.log"; exit 1; }
 echo "kt ok"
@@ -21,4 +30,4 @@ timeout -k 10 -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES
 echo "sq1 ok"
 timeout -k 10 -s KILL 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT $P -d "$OUT/p2" -o p2 -- python3 $B > "$OUT/p2.log" 2>&1 || { echo p2 failed; tail -5 "$OUT/p2.log"; exit 1; }
 echo "sq2 ok"
-python3 scripts/pmc_summary.py "$OUT" workload=c3 replicas=10000 variant=12 "command=scripts/gpu_pmc.sh $TAG ($B)" > "$OUT/summary.txt" && cat "$OUT/summary.txt"
+python3 scripts/pmc_summary.py "$OUT" workload=$WL replicas=$R variant=$V "command=scripts/gpu_pmc.sh $TAG ($B)" > "$OUT/summary.txt" && cat "$OUT/summary.txt"
