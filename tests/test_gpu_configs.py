@@ -2,9 +2,9 @@
 
 C5 (10k followers, 500 bursty Hawkes sources): bit-exact vs the engine oracle on
 a shortened horizon (T=100, ~5e4 events per replica: the oracle finishes in
-seconds) and, at the full T=1000 (~5e5 events per replica), size-independent
-checks: no overflow, batch == sharded sub-batches, event counts at the Hawkes
-mean.  C4 (README graph x 64 q x 4 s): the full grid at 64 replicas per point,
+seconds) and, at the full T=1000 (~5e5 events per replica), two replicas bit-exact
+against the C oracle's batch path plus size-independent checks: no overflow,
+batch == sharded sub-batches, event counts at the Hawkes mean.  C4 (README graph x 64 q x 4 s): the full grid at 64 replicas per point,
 sharded as 8 ranks would run it, equal to the unsharded grid; grid means move with
 q as RedQueen's budget law says (posts fall as q grows)."""
 import numpy as np
@@ -77,6 +77,33 @@ def test_c5_full_horizon_properties():
     assert abs(ev - 500 * 0.5 * 1000 / 0.5) < 0.02 * 500000, ev
     top = full.metrics[:, 0].cpu().numpy()
     assert np.all((top >= 0) & (top <= 1000.0))
+
+
+def test_c5_full_horizon_replicas_bit_exact():
+    """Full C5 (T=1000, ~5e5 events and ~5e7 sink updates per replica) through the
+    bench's own kernel (plan variant 3, K=1 sink bits): replicas 0 and 3 equal the
+    C oracle bit for bit -- metrics and counts from rqo_engine_batch, and the whole
+    event sequence (t, stream) from rqo_engine_run against the event-log run."""
+    torch, engine, graphs, O = _ctx()
+    so = graphs.c5()
+    g = _graph(engine, so)
+    kw = dict(q=so["q"], s=so["s"], n_rep=4, ctrl_seed=11, world_seed=11, randomize=True, Ks=(1,))
+    assert g.run("opt", plan_only=True, **kw)["variant"] == 3
+    plain = g.run("opt", **kw)
+    logd = g.run("opt", event_log=True, **kw)
+    assert int(plain.status.max().item()) == 0 and int(logd.status.max().item()) == 0
+    assert torch.equal(plain.metrics, logd.metrics) and torch.equal(plain.counts, logd.counts)
+    for r in (0, 3):
+        u = 11 + r
+        out, cnt, _ = O.engine_batch(O.Scenario(so, ("opt", 0)), 1, u, True, (1,), 1)
+        m = plain.metrics[r].cpu().numpy()
+        assert np.array_equal(m, out[0]), (r, m, out[0])
+        c = plain.counts[r].cpu().numpy()
+        assert (c[0], c[1], c[2]) == tuple(int(x) for x in cnt[0]), (r, c, cnt[0])
+        assert c[2] > 400000
+        t_o, _, s_o = O.engine_run(O.Scenario(_world_with_seeds(so, u), ("opt", u)))
+        t, s = logd.events(r)
+        assert np.array_equal(s, s_o) and np.array_equal(t, t_o), r
 
 
 def test_c4_grid_sharded():
