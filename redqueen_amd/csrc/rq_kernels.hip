@@ -413,13 +413,29 @@ __global__ __launch_bounds__(LOG ? 256 : (SPL >= 4 ? 512 : 1024)) void rq_sweep(
             tt = actw ? st_t[lane] : RQ_INF;
             tj = actw ? st_j[lane] : 0;
             wave_lds_sync();   // the staging area is rewritten by the next tile
-            // consume: sources the tile advanced reload their window
+            // consume: a source the tile advanced by c shifts its window by c in
+            // registers and loads only the c arrivals that enter it (each arrival is
+            // read from the stream buffer once)
             bool left = false;
 #pragma unroll
             for (int q = 0; q < SPL; ++q) {
-                if (cq[q] > 0) {
-                    pos[q] += cq[q];
-                    load_win(q);
+                const int c = cq[q];
+                if (c > 0) {
+                    pos[q] += c;
+                    double nw[HW];
+#pragma unroll
+                    for (int h = 0; h < HW; ++h) {
+                        double x = RQ_INF;
+#pragma unroll
+                        for (int s = h + 1; s < HW; ++s)
+                            if (c == s - h) x = wv[q][s];
+                        nw[h] = x;
+                    }
+#pragma unroll
+                    for (int h = 0; h < HW; ++h)
+                        if (h + c >= HW && pos[q] + h < len[q]) nw[h] = st[off[q] + pos[q] + h];
+#pragma unroll
+                    for (int h = 0; h < HW; ++h) wv[q][h] = nw[h];
                 }
                 left = left || pos[q] < len[q];
             }
