@@ -10,13 +10,17 @@
 // Kernels (one launch each, every dataframe of the batch in the same launch):
 //
 //   rq_rp_fast<NK, GLOBAL>   one 1024-thread workgroup per dataframe, rows in
-//       batches of 1024 (prefetched one batch ahead).  Sink ids get a dense slot
-//       from a hash table (LDS, <= 3071 unique sinks; the GLOBAL instance keeps it
-//       in HBM for wider dataframes), so no host-side factorisation is needed.
-//       Per batch: a bitonic sort of (slot, row) keys gives every row its
-//       predecessor in its sink's feed; two block max-scans give the segment start
-//       and the latest own post, so rank = pos - lastown (utils.py:43-46) for every
-//       row at once.  Each row then contributes the change of its pivot cell
+//       batches of 1024 (the next batch's loads are in flight during the current
+//       one and staged through LDS at its end).  Sink ids get a dense slot from a
+//       hash table (LDS, <= 3071 unique sinks; the GLOBAL instance keeps it in HBM
+//       for wider dataframes), so no host-side factorisation is needed.
+//       Per batch: every row takes a ticket in its sink's bucket (an LDS atomic on
+//       the sink's slot); a sink with several rows in the batch gets a list of them
+//       (one allocator atomic for the bucket), and each row scans its sink's list for
+//       the rows before it, its predecessor and the latest own rows at / before it,
+//       so rank = pos - lastown (utils.py:43-46) for every row at once, with the
+//       carried per-sink state (count, last own row, last t-group) from earlier
+//       batches.  Each row then contributes the change of its pivot cell
 //       (rank - previous rank of that sink; NaN -> value for the first row) to a
 //       block scan in row order; at the last row of every t-group the running
 //       totals ARE the pivot row (sum of the forward-filled cells, #non-NaN cells,
