@@ -128,6 +128,13 @@ def run_significance(sim_opts, significance, time_period, seeds=range(10), rando
     seeds = np.asarray(list(seeds), dtype=np.int64)
     spw = OptPWSignificance(sim_opts.src_id, 0, significance, time_period)._s_pw_for(g.n_followers)
     qv = np.asarray(qs, dtype=np.float64)
+    # a source that can post but reaches no follower with positive significance makes
+    # every reference run raise (take_one_sample's int(nan)): raise it here too
+    from .opt_model import _sig_reach_check
+    live = [kw["src_id"] for name, kw in sim_opts.other_sources
+            if name != "RealData" or any(0.0 <= t <= sim_opts.end_time for t in kw.get("times", []))]
+    for q in qv:
+        _sig_reach_check(g, sim_opts.edge_list, spw, float(q), np.asarray(live, dtype=np.int64))
     R = len(seeds)
     seed_t = torch.as_tensor(np.tile(seeds, len(qv)))
     res = g.run("sig", q=qv, s_pw=spw, period=float(time_period), n_rep=R, ctrl_seed=seed_t,

@@ -281,6 +281,26 @@ class OptPWSignificance(Broadcaster):
         return s_pw
 
 
+def _sig_reach_check(g, edge_list, s_pw, q, ev_src):
+    """OptPWSignificance raises where the reference does: an event whose source reaches
+    no follower with positive significance gives take_one_sample an all-zero
+    piecewise intensity, s_max = 0 and int(nan) (opt_model.py:557-566, :610-614).
+    The engine draws nothing for such an event; the facade raises the reference's
+    error if one was played."""
+    fol = {int(f): i for i, f in enumerate(g.followers)}
+    pw = {}
+    for a, b in edge_list:   # rank_diff counts edge multiplicity
+        if int(a) != g.src_id and int(b) in fol:
+            pw[int(a)] = pw.get(int(a), 0.0) + np.sqrt(np.asarray(s_pw[fol[int(b)]]) / q)
+    bad = {int(j) for j in g.stream_src_ids
+           if int(j) != g.src_id and not (int(j) in pw and np.max(pw[int(j)]) > 0.0)}
+    hit = [int(j) for j in np.unique(ev_src) if int(j) in bad]
+    if hit:
+        raise ValueError("cannot convert float NaN to integer (OptPWSignificance.take_one_sample: "
+                         "an event of source {} reaches no follower with positive significance)"
+                         .format(hit[0]))
+
+
 # ----------------------------------------------------------------------- Manager
 class Manager:
     def __init__(self, sources, sink_ids=None, end_time=None, edge_list=None, sim_opts=None,
@@ -375,9 +395,10 @@ class Manager:
                 s = np.ones(g.n_followers) * np.asarray(ctrl.s, dtype=float)
             res = g.run("opt", q=ctrl.q, s=s, ctrl_seed=seed, max_events=maxev, event_log=True)
         elif isinstance(ctrl, OptPWSignificance):
-            res = g.run("sig", q=ctrl.q, s_pw=ctrl._s_pw_for(g.n_followers),
-                        period=float(ctrl.time_period), ctrl_seed=seed, max_events=maxev,
-                        event_log=True)
+            s_pw = ctrl._s_pw_for(g.n_followers)
+            res = g.run("sig", q=ctrl.q, s_pw=s_pw, period=float(ctrl.time_period), ctrl_seed=seed,
+                        max_events=maxev, event_log=True)
+            _sig_reach_check(g, self.edge_list, s_pw, ctrl.q, res.events(0)[1])
         elif isinstance(ctrl, Poisson2):
             res = g.run("poisson", ctrl_seed=seed, ctrl_rate=[float(ctrl.rate)], max_events=maxev,
                         event_log=True)

@@ -274,6 +274,15 @@ def u_int_opt(df, src_id=None, end_time=None, s=None, q=None, follower_ids=None,
     if missing:
         raise KeyError("{} not in index".format(missing))
     fcol = np.asarray([pos[int(f)] for f in follower_ids], dtype=np.int32)
+    if np.ndim(s) == 0:
+        # a scalar s: the reference's `r_t[follower_ids].values.dot(np.sqrt(s / q))`
+        # scales the [n_t, F] rank block instead of reducing it, and `u_values * u_dt`
+        # then broadcasts ([n_t, n_t] for one follower, a ValueError for most F) --
+        # the same numpy expression on the GPU-built rank table, errors included
+        r = tab.cpu().numpy()[:, fcol]
+        u_values = r.dot(np.sqrt(s / q))
+        u_dt = np.diff(np.concatenate([idx.cpu().numpy(), [end_time]]))
+        return np.sum(u_values * u_dt)
     wts = np.sqrt(np.asarray(s, dtype=np.float64) / q) * np.ones(len(fcol))
     n_t = tab.shape[0]
     ws = torch.empty(max(1, n_t), dtype=torch.float64, device=_dev())

@@ -31,6 +31,8 @@ installed and there is no network) and records, as plain data:
                    df (deterministic), its metrics and final State.time
   plugin.npz       a registered static broadcaster (registerSource): df + metrics of the
                    seeded world and of randomize_other_sources(u), u = 0..15
+  errors.npz       reference behaviour on a scalar-s u_int_opt and on OptPWSignificance
+                   events that reach no follower with positive significance
   sig_runs.npz     OptPWSignificance runs (notebook "Testing out significance",
                    opt_broadcast.ipynb:5469, :5569): events + metrics
   graphs.npz       opt_runs.make_edge_list networks (C3 parameters) and a
@@ -425,6 +427,54 @@ def gen_sweepq():
     np.savez_compressed(os.path.join(HERE, "sweepq.npz"), **rec)
 
 
+def gen_errors():
+    """Reference behaviour on inputs where it does not compute what the engine would:
+    u_int_opt with a SCALAR s (utils.py:78-81: .dot(scalar) keeps the [n_t, F] rank
+    block and `u_values * u_dt` broadcasts: an [n_t, n_t] sum for one follower, an
+    error for two) and OptPWSignificance on an event that reaches no follower with
+    positive significance (take_one_sample: s_max = 0 -> int(nan), opt_model.py:557-566):
+    an edge-less source, and a source whose only follower has zero significance."""
+    rec = {}
+    rd = SimOpts(**README)
+    m = rd.create_manager_with_opt(seed=101)
+    m.run_dynamic()
+    df = m.state.get_dataframe()
+    _df_cols(rec, "ui", df)
+    rec["ui_scalar_f1"] = np.asarray([U.u_int_opt(df, src_id=1, end_time=100.0, s=1.0, q=2.0,
+                                                  follower_ids=[1])])
+    try:
+        U.u_int_opt(df, src_id=1, end_time=100.0, s=1.0, q=2.0, follower_ids=[1, 3])
+        rec["ui_scalar_f2_err"] = np.asarray(["none"])
+    except Exception as e:
+        rec["ui_scalar_f2_err"] = np.asarray([type(e).__name__])
+    worlds = {
+        "edgeless": (dict(src_id=1, end_time=20.0, q=1.0, s=np.asarray([1.0, 1.0]), sink_ids=[5001, 5002],
+                          other_sources=[("Poisson2", {"src_id": 1000, "seed": 42, "rate": 10.0}),
+                                         ("Poisson2", {"src_id": 1001, "seed": 43, "rate": 10.0})],
+                          edge_list=[(1, 5001), (1, 5002), (1000, 5001)]), None),
+        "zerosig": (dict(src_id=1, end_time=20.0, q=1.0, s=np.asarray([1.0, 1.0]), sink_ids=[5001, 5002],
+                         other_sources=[("Poisson2", {"src_id": 1000, "seed": 42, "rate": 10.0}),
+                                        ("Poisson2", {"src_id": 1001, "seed": 43, "rate": 10.0})],
+                         edge_list=[(1, 5001), (1, 5002), (1000, 5001), (1001, 5002)]),
+                    np.asarray([[1.0, 2.0, 1.0, 0.5], [0.0, 0.0, 0.0, 0.0]])),
+        "ok": (dict(src_id=1, end_time=20.0, q=1.0, s=np.asarray([1.0, 1.0]), sink_ids=[5001, 5002],
+                    other_sources=[("Poisson2", {"src_id": 1000, "seed": 42, "rate": 10.0}),
+                                   ("Poisson2", {"src_id": 1001, "seed": 43, "rate": 10.0})],
+                    edge_list=[(1, 5001), (1, 5002), (1000, 5001), (1001, 5002)]),
+               np.asarray([[1.0, 2.0, 1.0, 0.5], [0.0, 1.0, 0.0, 0.0]])),
+    }
+    for name, (w, sig) in worlds.items():
+        so = SimOpts(**w)
+        m = so.create_manager_with_significance(3, time_period=10.0, significance=sig,
+                                                num_segments=None if sig is not None else 4)
+        try:
+            m.run_dynamic()
+            rec["sig_%s_err" % name] = np.asarray(["none"])
+        except Exception as e:
+            rec["sig_%s_err" % name] = np.asarray([type(e).__name__])
+    np.savez_compressed(os.path.join(HERE, "errors.npz"), **rec)
+
+
 from realdata_worlds import realdata_worlds  # noqa: E402  (plain data, shared with the tests)
 
 
@@ -661,7 +711,7 @@ if __name__ == "__main__":
     steps = {"npsum": gen_npsum, "draws": gen_draws, "readme": gen_readme, "kats": gen_kats,
              "adv": gen_adversarial, "graphs": gen_graphs, "frac": gen_frac,
              "oracle": gen_oracle, "sweepq": gen_sweepq, "sig": gen_sig, "realdata": gen_realdata,
-             "plugin": gen_plugin}
+             "plugin": gen_plugin, "errors": gen_errors}
     if a.c3_dist:
         gen_c3_dist(a.c3_dist)
         print("done c3 dist", flush=True)

@@ -165,3 +165,17 @@ def test_sweep_q_gpu_matches_engine_oracle():
     for q, c in caps.items():
         assert np.array_equal(U.calc_q_capacity_iter(so, q), c)
     assert 0.25 < q_gpu / 0.00021575603911125744 < 4.0
+
+
+def test_u_int_scalar_s_like_reference(golden):
+    """u_int_opt with a scalar s computes the reference's numpy expression (utils.py:
+    78-81): for one follower the [n_t, n_t] broadcast sum, the reference's value bit
+    for bit; for two followers the reference's ValueError (errors.npz)."""
+    O, U = _ctx()
+    g = golden("errors.npz")
+    df = df_of(g, "ui")
+    v = U.u_int_opt(df, src_id=1, end_time=100.0, s=1.0, q=2.0, follower_ids=[1])
+    assert v == g["ui_scalar_f1"][0]
+    assert str(g["ui_scalar_f2_err"][0]) == "ValueError"
+    with pytest.raises(ValueError):
+        U.u_int_opt(df, src_id=1, end_time=100.0, s=1.0, q=2.0, follower_ids=[1, 3])

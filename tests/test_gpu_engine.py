@@ -231,6 +231,32 @@ def test_equal_time_rows(mode):
         _cmp_replica(res, 0, met_o, t_o, s_o, Ks)
 
 
+def test_tie_fallback_many_sources_event_log():
+    """More than 64 sources with an event log runs the fast general sweep first.  Two
+    Poisson2 walls with the same seed and rate post at identical times into a shared
+    sink, so equal-time rows set RQ_ST_TIE and Graph.run(check=True) reruns the batch
+    on the sequential sweep: the result equals sweep_mode=2 and the engine oracle."""
+    torch, engine, graphs, O = _ctx()
+    extra = [("Poisson", {"src_id": 100 + k, "seed": 7 + k, "rate": 0.3}) for k in range(66)]
+    so = dict(src_id=1, end_time=50.0, s=np.asarray([1.0, 2.0]), q=1.5, sink_ids=[10, 11, 12],
+              other_sources=[("Poisson2", {"src_id": 2, "seed": 5, "rate": 3.0}),
+                             ("Poisson2", {"src_id": 3, "seed": 5, "rate": 3.0})] + extra,
+              edge_list=[(1, 10), (1, 11), (2, 10), (2, 11), (3, 11), (3, 12)] +
+                        [(100 + k, 10 + k % 3) for k in range(66)])
+    g = _graph(engine, so)
+    Ks = (1,)   # K = 1: the fast sink-bit general sweep writes event logs itself
+    kw = dict(q=so["q"], s=so["s"], n_rep=2, ctrl_seed=3, Ks=Ks)
+    assert g.n_streams > 64
+    assert g.run("opt", event_log=True, plan_only=True, **kw)["variant"] % 10 != 1   # fast first
+    fast = g.run("opt", event_log=True, check=False, **kw)
+    assert int(fast.status[0].item()) & 4   # the ties were seen
+    a = g.run("opt", event_log=True, **kw)
+    b = g.run("opt", event_log=True, sweep_mode=2, **kw)
+    assert torch.equal(a.metrics, b.metrics) and torch.equal(a.counts, b.counts)
+    met_o, t_o, s_o = _oracle(O, so, ("opt", 3), Ks)
+    _cmp_replica(a, 0, met_o, t_o, s_o, Ks)
+
+
 def test_fast_sweep_equal_times_disjoint_sinks():
     """The tiled sweep's vectorised row placement on equal-time rows (forced with
     sweep_mode=1): two RealData walls on the same (distinct) times feeding

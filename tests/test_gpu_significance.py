@@ -102,3 +102,40 @@ def test_ensemble_vs_reference(golden):
         r = ref[k]
         z = (v.mean() - r.mean()) / math.sqrt(v.var() / len(v) + r.var() / len(r))
         assert abs(z) < 2.576, (k, r.mean(), v.mean(), z)
+
+
+def _err_worlds():
+    """The worlds of tests/golden/errors.npz (gen_golden.gen_errors), as plain data."""
+    base = dict(src_id=1, end_time=20.0, q=1.0, s=np.asarray([1.0, 1.0]), sink_ids=[5001, 5002],
+                other_sources=[("Poisson2", {"src_id": 1000, "seed": 42, "rate": 10.0}),
+                               ("Poisson2", {"src_id": 1001, "seed": 43, "rate": 10.0})])
+    full = [(1, 5001), (1, 5002), (1000, 5001), (1001, 5002)]
+    return {"edgeless": (dict(base, edge_list=full[:3]), None),
+            "zerosig": (dict(base, edge_list=full), np.asarray([[1.0, 2.0, 1.0, 0.5], [0.0, 0.0, 0.0, 0.0]])),
+            "ok": (dict(base, edge_list=full), np.asarray([[1.0, 2.0, 1.0, 0.5], [0.0, 1.0, 0.0, 0.0]]))}
+
+
+def test_unreached_event_raises_like_reference(golden):
+    """An event whose source reaches no follower with positive significance: the
+    reference raises (take_one_sample's int(nan), opt_model.py:557-566) -- so does the
+    facade, for a manager and for a batch; a world without one runs."""
+    torch, engine, graphs, O = _ctx()
+    from redqueen_amd import batch
+    from redqueen_amd.opt_model import SimOpts
+    g = golden("errors.npz")
+    for name, (w, sig) in _err_worlds().items():
+        ref = str(g["sig_%s_err" % name][0])
+        so = SimOpts(**w)
+        m = so.create_manager_with_significance(3, time_period=10.0, significance=sig,
+                                                num_segments=None if sig is not None else 4)
+        sig_b = sig if sig is not None else np.ones((2, 4))
+        if ref == "none":
+            m.run_dynamic()
+            assert m.state.get_num_events() > 0
+            batch.run_significance(so, sig_b, 10.0, seeds=range(4))
+        else:
+            assert ref == "ValueError"
+            with pytest.raises(ValueError):
+                m.run_dynamic()
+            with pytest.raises(ValueError):
+                batch.run_significance(so, sig_b, 10.0, seeds=range(4))
