@@ -605,12 +605,18 @@ def _c3_worker(r):
     return np.asarray([own, world, m.state.get_num_events(), top, avg])
 
 
-def gen_c3_dist(n):
+def gen_c3_dist(n, start=0, procs=0):
     """C3 (the bench network) through the reference itself: n replicas, replica r runs
     world randomize_other_sources(5000 r) and RedQueen seed 5000 r, so no two replicas
-    share a source stream (~41 s per replica per core)."""
-    with mp.Pool(os.cpu_count()) as pool:
-        res = np.asarray(pool.map(_c3_worker, range(n), chunksize=1))
+    share a source stream (~41 s per replica per core).  start > 0 appends replicas
+    start .. start + n - 1 to the existing file (which must hold exactly start rows)."""
+    path = os.path.join(HERE, "dist_c3.npz")
+    with mp.Pool(procs or os.cpu_count()) as pool:
+        res = np.asarray(pool.map(_c3_worker, range(start, start + n), chunksize=1))
+    if start:
+        old = np.load(path)["data"]
+        assert old.shape[0] == start, (old.shape, start)
+        res = np.concatenate([old, res])
     np.savez_compressed(os.path.join(HERE, "dist_c3.npz"), data=res,
                         cols=np.asarray(["posts", "world", "events", "top1", "avg"]),
                         seed_stride=np.asarray([C3_SEED_STRIDE]))
@@ -707,13 +713,15 @@ if __name__ == "__main__":
     ap.add_argument("--worlds", action="store_true", help="only dist_world.npz")
     ap.add_argument("--sig-dist", type=int, default=0, help="only dist_sig.npz with N replicas")
     ap.add_argument("--c3-dist", type=int, default=0, help="only dist_c3.npz with N replicas")
+    ap.add_argument("--c3-start", type=int, default=0, help="append to dist_c3.npz from this replica")
+    ap.add_argument("--procs", type=int, default=0)
     a = ap.parse_args()
     steps = {"npsum": gen_npsum, "draws": gen_draws, "readme": gen_readme, "kats": gen_kats,
              "adv": gen_adversarial, "graphs": gen_graphs, "frac": gen_frac,
              "oracle": gen_oracle, "sweepq": gen_sweepq, "sig": gen_sig, "realdata": gen_realdata,
              "plugin": gen_plugin, "errors": gen_errors}
     if a.c3_dist:
-        gen_c3_dist(a.c3_dist)
+        gen_c3_dist(a.c3_dist, a.c3_start, a.procs)
         print("done c3 dist", flush=True)
         a.worlds = True   # nothing else
     elif a.sig_dist:

@@ -106,6 +106,41 @@ def test_c5_full_horizon_replicas_bit_exact():
         assert np.array_equal(s, s_o) and np.array_equal(t, t_o), r
 
 
+def test_c4_full_config():
+    """C4 at its full size: 64 q x 4 s grid points x 1000 replicas (256k replicas, chunked
+    by the engine), run whole and as the 8 contiguous shards 8 GPUs would run; every
+    per-replica row and the fixed-order grid means agree; one replica per s column
+    equals the oracle."""
+    torch, engine, graphs, O = _ctx()
+    from redqueen_amd import dist
+    so = graphs.readme()
+    g = _graph(engine, so)
+    grid = graphs.c4_grid()
+    qs = np.asarray([q for q, _ in grid])
+    sm = np.asarray([[s1, s2] for _, (s1, s2) in grid])
+    n_rep = 1000
+    kw = dict(q=qs, s=sm, ctrl_seed=0, world_seed=0, randomize=True, Ks=(1,), seed_mod=n_rep)
+    full = g.run("opt", n_rep=n_rep, **kw)
+    assert full.metrics.shape[0] == len(grid) * n_rep == 256000
+    assert int(full.status.max().item()) == 0
+    parts = []
+    for rank in range(8):
+        a, b = dist.shard(len(grid) * n_rep, 8, rank)
+        parts.append(g.run("opt", n_rep=n_rep, replica0=a, n_local=b - a, **kw).metrics)
+    allm = torch.cat(parts)
+    assert torch.equal(allm, full.metrics)
+    assert torch.equal(dist.grid_means(allm, len(grid), n_rep), dist.grid_means(full.metrics, len(grid), n_rep))
+    posts = full.counts[:, 0].double().reshape(len(grid), n_rep).mean(1).cpu().numpy()
+    for si in range(4):
+        p = posts[si * 64:(si + 1) * 64]
+        assert p[0] > p[-1] and np.all(np.diff(p) <= 0.02 * p[0] + 2.0)
+    for gi, r in ((5, 999), (64 + 40, 123), (128 + 63, 0), (192 + 17, 500)):
+        dd = dict(so, q=float(qs[gi]), s=sm[gi])
+        (top, avg, r2, cnt), _ = O.engine_metrics(O.Scenario(_world_with_seeds(dd, r), ("opt", r)), (1,))
+        row = full.metrics[gi * n_rep + r].cpu().numpy()
+        assert row[0] == top[0] and row[1] == avg and row[2] == r2
+
+
 def test_c4_grid_sharded():
     torch, engine, graphs, O = _ctx()
     from redqueen_amd import dist
