@@ -234,6 +234,33 @@ struct SegFlags {
     }
 };
 
+// rank of this lane's staged arrival (ti at slot `lane`) among the tile's staged
+// times st_t[0..n) in (t, slot) order.  st_t[n..64) must hold +INF (never below a
+// finite ti).  First #{t < ti} alone (one compare and one carry-add per slot, reads
+// broadcast from LDS, 8 slots per wait); those ranks are a permutation of 0..n-1,
+// i.e. sum to n(n-1)/2, exactly when no two staged times are equal -- otherwise the
+// count is redone with the slot tie-break.
+__device__ __forceinline__ int stage_rank(const double* st_t, int n, double ti, int lane)
+{
+    int rnk = 0;
+    for (int q = 0; q < n; q += 8) {
+        double2 x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) x[u] = *reinterpret_cast<const double2*>(st_t + q + 2 * u);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) rnk += (x[u].x < ti ? 1 : 0) + (x[u].y < ti ? 1 : 0);
+    }
+    const uint32_t sum = wave_sum_u32(lane < n ? (uint32_t)rnk : 0u);
+    if (sum == (uint32_t)(n * (n - 1) / 2)) return rnk;
+    rnk = 0;
+    for (int q = 0; q < n; q += 2) {
+        const double2 x = *reinterpret_cast<const double2*>(st_t + q);
+        rnk += (x.x < ti || (x.x == ti && q < lane)) ? 1 : 0;
+        rnk += (x.y < ti || (x.y == ti && q + 1 < lane)) ? 1 : 0;
+    }
+    return rnk;
+}
+
 // min of a double over the 64 lanes (every lane gets it)
 __device__ __forceinline__ double wave_min_f64(double x)
 {

@@ -393,17 +393,13 @@ __global__ __launch_bounds__(LOG ? 256 : (SPL >= 4 ? 512 : 1024)) void rq_sweep(
                             st_j[k] = lane * SPL + q;
                             ++k;
                         }
+                if (lane >= n) st_t[lane] = RQ_INF;   // the rank loop reads whole blocks of 8
             }
             wave_lds_sync();
             const bool actw = lane < n;
             const double ti = actw ? st_t[lane] : RQ_INF;
             const int ji = actw ? st_j[lane] : 0;
-            int rnk = 0;
-            for (int q = 0; q < n; q += 2) {
-                const double2 tq = *reinterpret_cast<const double2*>(st_t + q);
-                rnk += (tq.x < ti || (tq.x == ti && q < lane)) ? 1 : 0;
-                rnk += (q + 1 < n && (tq.y < ti || (tq.y == ti && q + 1 < lane))) ? 1 : 0;
-            }
+            const int rnk = stage_rank(st_t, n, ti, lane);
             wave_lds_sync();
             if (actw) {
                 st_t[rnk] = ti;
@@ -1015,23 +1011,14 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
                 st_t[off + q] = v[q];
                 st_j[off + q] = lane;
             }
+        if (lane >= n) st_t[lane] = RQ_INF;   // the rank loop reads whole blocks of 8
         wave_lds_sync();
         const bool act = lane < n;
         const double ti = act ? st_t[lane] : RQ_INF;
         const int ji = act ? st_j[lane] : 0;
-        // rank = #staged arrivals before this one in (t, stream) order; the staged
-        // times are read back from LDS two at a time (a broadcast ds_read_b128: every
-        // lane reads the same address) instead of two v_readlanes per element
-        int rnk = 0;
-        if (a.dbg != 4) {   // profiling only: 4 = skip the rank sort
-            for (int q = 0; q < n; q += 2) {
-                const double2 tq = *reinterpret_cast<const double2*>(st_t + q);
-                rnk += (tq.x < ti || (tq.x == ti && q < lane)) ? 1 : 0;
-                rnk += (q + 1 < n && (tq.y < ti || (tq.y == ti && q + 1 < lane))) ? 1 : 0;
-            }
-        } else {
-            rnk = lane;
-        }
+        // rank = #staged arrivals before this one in (t, stream) order (stage_rank:
+        // broadcast LDS reads, 8 slots per wait); profiling only: dbg 4 skips it
+        const int rnk = a.dbg != 4 ? stage_rank(st_t, n, ti, lane) : lane;
         wave_lds_sync();
         if (act) {
             st_t[rnk] = ti;

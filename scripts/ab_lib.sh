@@ -1,0 +1,10 @@
+#!/bin/bash
+# same-box A/B of two builds on the C3 bench: ab_lib.sh LIB_A LIB_B [rounds]
+set -o pipefail
+A=$1; B=$2; N=${3:-3}
+for i in $(seq 1 $N); do
+  for L in $A $B; do
+    RQ_SO_PATH=$GRAFT_REPO_ROOT/$L timeout -k 10 120 python3 bench.py --steps 10 --warmup 2 --no-cpu > gpurun_out/ab.log 2>&1 || { echo "$L failed"; tail -3 gpurun_out/ab.log; exit 1; }
+    python3 -c "import json; l=json.loads(open('gpurun_out/ab.log').read().strip().splitlines()[-1]); print('$L', round(l['ms_per_step'],3), {k: round(v,3) for k,v in l['kernels_ms_per_launch'].items()})"
+  done
+done
