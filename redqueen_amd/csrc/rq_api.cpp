@@ -352,7 +352,9 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
         int best = -1;
         const int c16 = p->bits ? 1 : (g->n_sinks <= 65535 ? 1 : 0);
         if (pw && !c16) p->fw = false;   // OptPWSignificance fused instances: uint16 columns
-        const size_t colb = p->bits ? 4 * (size_t)g->n_str * p->mstride
+        // BITS: sink bitsets [n_str + 1][mstride] (row n_str all zero: the mask of a
+        // lane without a wall event) replace the columns
+        const size_t colb = p->bits ? 4 * (size_t)(g->n_str + 1) * p->mstride
                                     : (c16 ? 2 * g->csr_col.size() : 0);
         size_t sh = 0;
         const size_t o_col = sh;  sh = align_up(sh + colb, 16);
@@ -367,7 +369,8 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
             if (pw && W != 16) continue;
             const int H = W / 2;
             const size_t r_off = align_up(8 * (size_t)g->n_str, 16);
-            const size_t w_off = align_up(r_off + (p->bits ? 0 : 2 * (size_t)p->n_sinks_pad), 16);
+            // per wave: BITS -> (F, T) word pairs [nw]; else int16 sink ranks
+            const size_t w_off = align_up(r_off + (p->bits ? 8 * (size_t)((g->nw + 1) & ~1) : 2 * (size_t)p->n_sinks_pad), 16);
             const size_t s_off = align_up(w_off + 8 * (size_t)g->n_str * (W + 1), 16);
             const size_t stride = align_up(s_off + 64 * 12, 16);
             for (int wpb : {16, 12, 10, 8, 6, 5, 4, 3, 2, 1}) {

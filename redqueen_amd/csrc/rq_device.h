@@ -175,6 +175,12 @@ __device__ __forceinline__ uint32_t dpp0(uint32_t v)
 {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, RM, 0xF, false);
 }
+// full row mask + bound_ctrl: every lane is written (its source or 0)
+template <int CTRL>
+__device__ __forceinline__ uint32_t dppz(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, true);
+}
 __device__ __forceinline__ uint32_t wave_scan_add(uint32_t v)
 {
     v += dpp0<0x111, 0xF>(v);
@@ -211,6 +217,8 @@ struct SegFlags {
         c3 = f - 1u;  f |= dpp0<0x118, 0xF>(f);
         c4 = f - 1u;  f |= dpp0<0x142, 0xA>(f);
         c5 = f - 1u;
+        // opaque masks: keeps `x & c` a single v_and_or_b32 instead of a lane-mask select
+        __asm__("" : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(c4), "+v"(c5));
     }
     __device__ __forceinline__ uint32_t scan_or(uint32_t v) const
     {
@@ -220,6 +228,28 @@ struct SegFlags {
         v |= dpp0<0x118, 0xF>(v) & c3;
         v |= dpp0<0x142, 0xA>(v) & c4;
         v |= dpp0<0x143, 0xC>(v) & c5;
+        return v;
+    }
+    // the same scan with bound_ctrl on the row shifts (an out-of-row source reads 0
+    // either way), so each of those steps folds into one v_and_b32_dpp + v_or_b32
+    // The row-broadcast steps take the previous step's shifted word t as the DPP
+    // `old` of the rows they leave unwritten, so no zeroing move is needed: a window
+    // that holds no segment head at step k held none at step k-1 (c_k != 0 implies
+    // c_{k-1} != 0), so t & c_k is already contained in v and OR-ing it is a no-op.
+    __device__ __forceinline__ uint32_t scan_or_z(uint32_t m) const
+    {
+        uint32_t t = dppz<0x111>(m);
+        uint32_t v = m | (t & c0);
+        t = dppz<0x112>(v);
+        v |= t & c1;
+        t = dppz<0x114>(v);
+        v |= t & c2;
+        t = dppz<0x118>(v);
+        v |= t & c3;
+        t = (uint32_t)__builtin_amdgcn_update_dpp((int)t, (int)v, 0x142, 0xA, 0xF, false);
+        v |= t & c4;
+        t = (uint32_t)__builtin_amdgcn_update_dpp((int)t, (int)v, 0x143, 0xC, 0xF, false);
+        v |= t & c5;
         return v;
     }
     __device__ __forceinline__ uint32_t scan_add(uint32_t v) const

@@ -108,6 +108,7 @@ hipError_t rq_launch_scan(const ScanArgs& a, int nK, hipStream_t s);
 int rq_sweep_blocks_per_cu(int spl, int nK, int col16, int W, int log, int bits, int wpb, size_t lds);
 hipError_t rq_launch_sweep_fw(const SweepArgs& a, int nK, int col16, int W, int bits, hipStream_t s);
 int rq_fw_blocks_per_cu(int nK, int col16, int W, int bits, int wpb, size_t lds, int pw);
+int rq_cu_count();   // CUs of the current device (256 on MI355X when the query fails)
 
 // ---- dataframe replay (rq_replay.hip) ----
 // per-dataframe status, in the workspace

@@ -827,413 +827,6 @@ __global__ __launch_bounds__(LOG ? 256 : (SPL >= 4 ? 512 : 1024)) void rq_sweep(
 }
 
 // ============================================================================
-// 2b. fused windowed sweep (n_str <= 64).  Lane j owns stream j and GENERATES its
-//     arrivals (SrcGen) into an LDS ring -- no stream buffer, no generator
-//     kernel.  A tile is every pending arrival earlier than a cut tau, found from
-//     the next H arrivals of each ring held in registers (a ring's unseen
-//     arrivals are >= its H-th, so tau <= min over rings of the H-th keeps the
-//     tile complete); tau adapts so a tile holds <= 64 arrivals.  The tile is
-//     staged in source order and rank-sorted into (t, stream) order -- the
-//     reference's (time, src_id) order (opt_model.py:279-281).  Phase B is the
-//     same controller; phase C for K = 1 runs lane-parallel over the tile's
-//     events: per sink-bitset word, segmented prefix ORs (segments start at the
-//     posts) give each event's top-1 set, plain prefix ORs its valid set.
-// ============================================================================
-template <int NK, class COL, int W, int H, bool BITS, bool PW = false>
-__global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
-{
-    static_assert((W & (W - 1)) == 0 && H <= W, "ring");
-    extern __shared__ double lds_g[];
-    char* base = reinterpret_cast<char*>(lds_g);
-    const int lane = lane_id();
-    const int w = threadIdx.x >> 6;
-    int* cptr = reinterpret_cast<int*>(base + a.lds_ptr);
-    int* odf = reinterpret_cast<int*>(base + a.lds_odf);
-    int* cbf = reinterpret_cast<int*>(base + a.lds_cbf);
-    constexpr bool col_lds = sizeof(COL) == 2;
-    COL* col_l = reinterpret_cast<COL*>(base + a.lds_col);
-    const int* col_g = a.csr_col;
-    if (col_lds && !BITS)
-        for (int e = threadIdx.x; e < a.n_csr; e += blockDim.x) col_l[e] = (COL)a.csr_col[e];
-    uint32_t* msk = reinterpret_cast<uint32_t*>(base + a.lds_mask);
-    const int ms = a.mstride;
-    if (BITS)
-        for (int e = threadIdx.x; e < a.n_str * ms; e += blockDim.x) {
-            const int jj = e / ms, ww = e - jj * ms;
-            msk[e] = ww < a.nw ? a.masks[jj * a.nw + ww] : 0u;
-        }
-    for (int j = threadIdx.x; j <= a.n_str; j += blockDim.x) cptr[j] = a.csr_ptr[j];
-    for (int j = threadIdx.x; j < a.n_str; j += blockDim.x) {
-        odf[j] = a.outdeg_f[j];
-        // the controller (a dynamic source) posts before a wall event at the same time
-        // when that source is static (run_dynamic plays a static time only if it is
-        // strictly earlier, opt_model.py:289-290) or has a larger src_id (the sorted
-        // (t_delta, src_id) of the dynamic sources, :279-281)
-        const int kj = a.gen.kind[j];
-        cbf[j] = kj == RQ_SRC_POISSON2 || kj == RQ_SRC_PWCONST || kj == RQ_SRC_REALDATA ||
-                 a.ctrl_src_id < a.src_id[j];
-    }
-    __syncthreads();   // block-shared tables ready; no block barrier below this line
-    char* wb = base + a.lds_wave + (size_t)w * a.lds_wave_stride;
-    double* invc = reinterpret_cast<double*>(wb);
-    int16_t* rank = reinterpret_cast<int16_t*>(wb + a.lds_rank_off);   // saturating, exact vs K-1
-    double* ring = reinterpret_cast<double*>(wb + a.lds_win_off) + lane * (W + 1);   // odd stride
-    double* st_t = reinterpret_cast<double*>(wb + a.lds_stage_off);
-    int* st_j = reinterpret_cast<int*>(st_t + 64);
-    // first replica: the wave's static slot; with a work queue (a.wq) the wave then takes
-    // replicas nslot, nslot + 1, ... in queue order until the chunk is exhausted (every
-    // wave leaves once the counter passes n_chunk)
-    const int64_t nslot = (int64_t)gridDim.x * a.wpb;
-    for (int64_t rl = (int64_t)blockIdx.x * a.wpb + w; rl < a.n_chunk;) {
-    const int64_t o = a.chunk0 + rl;
-    const int64_t i = a.rep0 + o;
-    const int g = (int)(i / a.n_rep);
-    for (int j = lane; j < a.n_str; j += 64) invc[j] = a.inv_c[(int64_t)g * a.n_str + j];
-    if (!BITS)
-        for (int c = lane; c < a.n_sinks; c += 64) rank[c] = -1;   // NaN: no row yet
-    wave_lds_sync();
-
-#ifdef RQ_PHASE_CLOCK
-    unsigned long long ck[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    unsigned long long tk = __builtin_amdgcn_s_memtime();
-#define RQ_CLK(q)                                                   \
-    do {                                                            \
-        const unsigned long long t2 = __builtin_amdgcn_s_memtime(); \
-        ck[q] += t2 - tk;                                           \
-        tk = t2;                                                    \
-    } while (0)
-#else
-#define RQ_CLK(q) \
-    do {          \
-    } while (0)
-#endif
-    SrcGen gen;
-    if (lane < a.n_str) gen.init(a.gen, lane, i);
-    else gen.none();
-    int pos = 0, fil = 0;   // arrivals consumed / generated by this lane's source
-
-    const bool opt = a.ctrl_kind == RQ_SRC_OPT || a.ctrl_kind == RQ_SRC_OPTPW;
-    // OptPWSignificance only in the PW instances: the thinning loop's registers stay out
-    // of the RedQueen controller's allocation
-    const double* pwc = PW ? a.pw_c + (size_t)g * a.n_str * a.n_seg : nullptr;
-    const double* pwm = PW ? a.pw_max + (size_t)g * a.n_str : nullptr;
-    double opt_next = opt ? a.start : RQ_INF;
-    const int64_t k = a.seed_mod > 0 ? i % a.seed_mod : i;
-    const uint32_t oseed = a.ctrl_seed ? a.ctrl_seed[i] : a.ctrl_seed0 + (uint32_t)k;
-    uint64_t ndraw = 0;   // wall events seen so far = the controller's draw index
-    auto colat = [&](int e) -> int { return col_lds ? (int)col_l[e] : col_g[e]; };
-    const int fol0 = cptr[a.ctrl_idx];
-    auto folat = [&](int f) -> int { return colat(fol0 + f); };
-
-    Agg<NK> ag;
-    ag.init(a.Ks);
-    AggB agb;
-    if (BITS) agb.init(msk, a.nw, ms, a.ctrl_idx, lane);
-    RowStage<NK> rs;
-    const int64_t rbase = rl * a.cap_rows;
-    rs.init(a.rows_t + rbase, a.rows_sum + rbase, a.rows_valid + rbase, a.rows_cnt + rbase * NK,
-            a.cap_rows);
-
-    int64_t n_events = 0, posts = 0, world = 0;
-    int status = 0;
-    double span = -1.0;   // adaptive tile width in time (< 0: not estimated yet)
-    bool stop = false;
-    for (;;) {
-        // ---- A1: every unfinished ring shows >= H arrivals (refill all to W at once) ----
-        if (__ballot(!gen.done && fil - pos < H)) {
-            while (__ballot(!gen.done && fil - pos < W)) {
-                if (!gen.done && fil - pos < W) {
-                    double tv;
-                    if (gen.step(&tv, a.end)) {
-                        ring[fil & (W - 1)] = tv;
-                        ++fil;
-                    }
-                }
-            }
-        }
-        RQ_CLK(0);   // A1: ring refills (arrival generation)
-        const int avail = fil - pos;
-        double v[H];
-#pragma unroll
-        for (int q = 0; q < H; ++q) v[q] = q < avail ? ring[(pos + q) & (W - 1)] : RQ_INF;
-        const bool more = !gen.done || avail > H;        // arrivals past the window exist
-        const double tfirst = wave_min_f64(v[0]);
-        if (!(tfirst < RQ_INF)) break;                   // everything consumed
-        const double tmax = wave_min_f64(more ? v[H - 1] : RQ_INF);
-
-        // ---- A2: the cut (exclusive): complete below tmax, <= 64 arrivals ----
-        int c = 0, n = 0;
-        bool trunc = !(tmax > tfirst);   // a ring's window is all at tfirst: equal-time prefix
-        if (!trunc) {
-            double cut = tmax;
-            if (span > 0.0 && tfirst + span < cut) cut = tfirst + span;
-            if (!(cut > tfirst)) cut = next_up(tfirst);
-            for (;;) {
-                c = 0;
-#pragma unroll
-                for (int q = 0; q < H; ++q) c += v[q] < cut ? 1 : 0;
-                n = (int)wave_sum_u32((uint32_t)c);
-                if (n <= 64) break;
-                const double nc = tfirst + (cut - tfirst) * 0.5;
-                const double lo = next_up(tfirst);
-                if (nc > tfirst && nc < cut) {
-                    cut = nc < lo ? lo : nc;
-                } else if (cut != lo) {
-                    cut = lo;
-                } else {
-                    trunc = true;   // > 64 arrivals share tfirst
-                    break;
-                }
-            }
-            if (!trunc) span = (cut - tfirst) * (a.tile_target / (double)(n > 8 ? n : 8));
-        }
-        if (trunc) {
-            // the arrivals equal to tfirst, in stream order, up to the first ring whose
-            // window may continue at tfirst, at most 64
-            c = 0;
-#pragma unroll
-            for (int q = 0; q < H; ++q) c += v[q] == tfirst ? 1 : 0;
-            const uint64_t bl = __ballot(more && v[H - 1] == tfirst);
-            const int lb = bl ? __ffsll((unsigned long long)bl) - 1 : 64;
-            if (lane > lb) c = 0;
-        }
-        const int off = (int)wave_scan_add((uint32_t)c) - c;
-        if (trunc) {
-            c = off >= 64 ? 0 : (c < 64 - off ? c : 64 - off);
-            n = (int)wave_sum_u32((uint32_t)c);
-        }
-
-        RQ_CLK(1);   // window + A2 cut
-        // ---- A3: stage in stream order, rank-sort into (t, stream) order ----
-#pragma unroll
-        for (int q = 0; q < H; ++q)
-            if (q < c) {
-                st_t[off + q] = v[q];
-                st_j[off + q] = lane;
-            }
-        if (lane >= n) st_t[lane] = RQ_INF;   // the rank loop reads whole blocks of 8
-        wave_lds_sync();
-        const bool act = lane < n;
-        const double ti = act ? st_t[lane] : RQ_INF;
-        const int ji = act ? st_j[lane] : 0;
-        // rank = #staged arrivals before this one in (t, stream) order (stage_rank:
-        // broadcast LDS reads, 8 slots per wait); profiling only: dbg 4 skips it
-        const int rnk = a.dbg != 4 ? stage_rank(st_t, n, ti, lane) : lane;
-        wave_lds_sync();
-        if (act) {
-            st_t[rnk] = ti;
-            st_j[rnk] = ji;
-        }
-        wave_lds_sync();
-        const double tt = act ? st_t[lane] : RQ_INF;
-        const int tj = act ? st_j[lane] : 0;
-        pos += c;
-        const bool fin = !__ballot(!gen.done || pos < fil);
-
-        int e0 = 0, e1 = 0, od = 0;
-        if (act) {
-            e0 = cptr[tj];
-            e1 = cptr[tj + 1];
-            od = odf[tj];
-        }
-        RQ_CLK(2);   // A3 stage + rank sort
-        // ---- B: RedQueen controller over the tile ----
-        uint64_t ownm = 0;
-        double ot = RQ_INF;
-        if (opt && a.dbg != 3) controller_tile<PW>(n, act, tt, tj, invc, cbf, oseed, ndraw, opt_next, ownm, ot, pwc, pwm, a.n_seg,
-                            a.period);
-
-        RQ_CLK(3);   // B controller
-        // ---- C: aggregates after each event ----
-        const bool own_b = act && ((ownm >> lane) & 1ull);       // controller post before #lane
-        if (a.ev_t) {
-            // event log (t, stream): lane q's post (if any) then its arrival, in tile order
-            const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-            const int64_t pp = n_events + lane + __popcll(ownm & below);
-            const int64_t pw = pp + (own_b ? 1 : 0);
-            double* Et = a.ev_t + o * a.ev_cap;
-            int32_t* Es = a.ev_src + o * a.ev_cap;
-            if (own_b && pp < a.ev_cap) {
-                Et[pp] = ot;
-                Es[pp] = a.ctrl_idx;
-            }
-            if (act && pw < a.ev_cap) {
-                Et[pw] = tt;
-                Es[pw] = tj;
-            }
-            if (n_events + n + __popcll(ownm) > a.ev_cap) status |= RQ_ST_ROWS_OVERFLOW;
-        }
-        const bool strm_own = act && !opt && tj == a.ctrl_idx;   // controlled stream's arrival
-        const bool has_o = own_b && a.n_fol > 0;
-        const bool has_w = act && e1 > e0;
-        int64_t osum = 0, wsum = 0;
-        int oval = 0, wval = 0;
-        int ocnt[NK], wcnt[NK];
-#pragma unroll
-        for (int kq = 0; kq < NK; ++kq) ocnt[kq] = wcnt[kq] = 0;
-        if (a.dbg == 1) {
-            // profiling only: skip phase C
-        } else if (BITS) {
-            // segments of the tile start at its own events (posts / own-stream arrivals)
-            const bool rst = own_b || strm_own;
-            const uint64_t rm = __ballot(rst);
-            const bool hasr = (rm & (~0ull >> (63 - lane))) != 0;   // own event at or before #lane
-            const bool wl = act && !strm_own;                        // a wall event
-            const int deg = wl ? e1 - e0 : 0;
-            const int odv = wl ? od : 0;
-            SegFlags sf;
-            sf.init(rst);
-            // sumR / sumF: wall adds deg / odf, an own event drops sumF from sumR
-            const int pdeg = (int)wave_scan_add((uint32_t)deg);
-            const int64_t sfq = (int64_t)(int)sf.scan_add((uint32_t)odv) + (hasr ? 0 : agb.sumF);
-            int64_t dec = 0;
-            for (uint64_t b = rm; b; b &= b - 1) {
-                const int r = __ffsll((unsigned long long)b) - 1;
-                const int64_t D = r == 0 ? agb.sumF : bcast_i64(sfq, r - 1);
-                if (lane >= r) dec += D;
-            }
-            wsum = agb.sumR + pdeg - dec;
-            osum = agb.sumR + (pdeg - deg) - dec;
-            // sink bitsets, one word at a time, every event of the tile at once
-            const bool vfull = agb.nvalid == a.n_sinks;
-            const int last = n - 1;
-            const uint32_t* mr = msk + (wl ? tj : 0) * ms;
-            int cw = 0, vw = 0, vo = 0;
-            uint32_t nT = agb.T, nV = agb.V;
-            for (int ww = 0; ww < a.nw; ++ww) {
-                const uint32_t Fw = (uint32_t)__builtin_amdgcn_readlane((int)agb.F, ww);
-                const uint32_t Tw = (uint32_t)__builtin_amdgcn_readlane((int)agb.T, ww);
-                const uint32_t m = wl ? mr[ww] : 0u;
-                const uint32_t u = sf.scan_or(m);                  // wall union since the segment start
-                const uint32_t tq = (hasr ? Fw : Tw) & ~u;         // top-1 set after #lane
-                cw += __popc(tq);
-                nT = (uint32_t)wlane((int)nT, __builtin_amdgcn_readlane((int)tq, last), ww);
-                if (!vfull) {
-                    const uint32_t Vw = (uint32_t)__builtin_amdgcn_readlane((int)agb.V, ww);
-                    const uint32_t x = wave_scan_or(m);
-                    const uint32_t vq = Vw | x | (hasr ? Fw : 0u);  // valid set after #lane
-                    vw += __popc(vq);
-                    const uint32_t xe = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xF, 0xF, false);
-                    vo += __popc(Vw | xe | Fw);                     // after the post before #lane
-                    nV = (uint32_t)wlane((int)nV, __builtin_amdgcn_readlane((int)vq, last), ww);
-                }
-            }
-            wcnt[0] = cw;
-            ocnt[0] = a.n_fol;   // a post puts every follower at rank 0
-            wval = vfull ? a.n_sinks : vw;
-            oval = vfull ? a.n_sinks : vo;
-            if (n > 0) {
-                agb.T = nT;
-                if (!vfull) {
-                    agb.V = nV;
-                    agb.nvalid = bcast_i(vw, last);
-                }
-                agb.sumR = bcast_i64(wsum, last);
-                agb.sumF = bcast_i64(sfq, last);
-            }
-        } else {
-            for (int q = 0; q < n; ++q) {
-                if ((ownm >> q) & 1ull) {
-                    ag.own(rank, folat, a.n_fol, lane);
-                    if (lane == q) {
-                        osum = ag.sumR;
-                        oval = ag.nvalid;
-#pragma unroll
-                        for (int kq = 0; kq < NK; ++kq) ocnt[kq] = ag.cnt[kq];
-                    }
-                }
-                const int jw = bcast_i(tj, q);
-                if (!opt && jw == a.ctrl_idx)
-                    ag.own(rank, folat, a.n_fol, lane);
-                else
-                    ag.wall(rank, colat, bcast_i(e0, q), bcast_i(e1, q), bcast_i(od, q), lane);
-                if (lane == q) {
-                    wsum = ag.sumR;
-                    wval = ag.nvalid;
-#pragma unroll
-                    for (int kq = 0; kq < NK; ++kq) wcnt[kq] = ag.cnt[kq];
-                }
-            }
-        }
-        RQ_CLK(4);   // C aggregates
-        const uint64_t mo = __ballot(has_o), ma = mo | __ballot(has_w);
-        n_events += n + __popcll(ownm);
-        posts += __popcll(mo) + __popcll(__ballot(has_w && strm_own));
-        world += __popcll(__ballot(has_w && !strm_own));
-        if (ma && place_rows<NK>(rs, ma, has_o, has_w, ot, tt, osum, oval, ocnt, wsum, wval, wcnt, status))
-            stop = true;
-        RQ_CLK(5);   // rows
-        if (stop || fin) break;
-    }
-#ifdef RQ_PHASE_CLOCK
-    if (lane == 0 && a.clk)
-        for (int q = 0; q < 6; ++q) atomicAdd(&a.clk[q], ck[q]);
-#endif
-    // the controller's last post after the final arrival
-    if (!stop && opt && opt_next <= a.end) {
-        if (a.ev_t && lane == 0) {
-            if (n_events < a.ev_cap) {
-                a.ev_t[o * a.ev_cap + n_events] = opt_next;
-                a.ev_src[o * a.ev_cap + n_events] = a.ctrl_idx;
-            } else {
-                status |= RQ_ST_ROWS_OVERFLOW;
-            }
-        }
-        ++n_events;
-        if (BITS) {
-            agb.own();
-            agb.sync();
-            ag.sumR = agb.sumR;
-            ag.nvalid = agb.nvalid;
-            ag.cnt[0] = agb.cnt[0];
-        } else {
-            ag.own(rank, folat, a.n_fol, lane);
-        }
-        if (a.n_fol > 0) {
-            ++posts;
-            int64_t rr = rs.nrow;
-            if (rs.nrow > 0 && opt_next == rs.last_t) {
-                status |= RQ_ST_TIE;
-                rr = rs.nrow - 1;
-            } else if (rs.nrow >= rs.cap) {
-                status |= RQ_ST_ROWS_OVERFLOW;
-                rr = -1;
-            } else {
-                ++rs.nrow;
-                rs.s0 = rs.nrow;
-                rs.last_t = opt_next;
-            }
-            if (rr >= 0 && lane == 0) {
-                rs.Rt[rr] = opt_next;
-                rs.Rs[rr] = (double)ag.sumR;
-                rs.Rv[rr] = (uint32_t)ag.nvalid;
-#pragma unroll
-                for (int kq = 0; kq < NK; ++kq) rs.Rc[rr * NK + kq] = (uint32_t)ag.cnt[kq];
-            }
-        }
-    }
-    if (BITS) {
-        agb.sync();
-        ag.nvalid = agb.nvalid;
-    }
-    if (lane == 0) {
-        int64_t* cnto = a.counts + o * 4;
-        cnto[0] = posts;
-        cnto[1] = world;
-        cnto[2] = n_events;
-        cnto[3] = rs.nrow;
-        a.sall[rl] = ag.nvalid;
-        if (rs.nrow == 0) status |= RQ_ST_EMPTY;
-        if (status) atomicOr(&a.status[o], status);
-    }
-    if (!a.wq) break;
-    int nx = 0;
-    if (lane == 0) nx = atomicAdd(a.wq, 1);
-    rl = nslot + __builtin_amdgcn_readfirstlane(nx);
-    }   // replica loop
-}
-
-// ============================================================================
 // 3. scan: numpy-order integrals over the pivot rows, one wavefront per replica
 // ============================================================================
 template <int NK, int WPE>
@@ -1300,7 +893,7 @@ __global__ __launch_bounds__(256, WPE) void rq_scan(ScanArgs a)
 // ============================================================================
 // launch wrappers
 // ============================================================================
-static int rq_cu_count()
+int rq_cu_count()
 {
     static int n = 0;
     if (n <= 0) {
@@ -1429,81 +1022,6 @@ int rq_sweep_blocks_per_cu(int spl, int nK, int col16, int W, int log, int bits,
     case 4: return occ_c<4>(nK, col16, W, bits, wpb, lds);
     default: return occ_c<8>(nK, col16, W, bits, wpb, lds);
     }
-}
-
-// fused windowed sweep: (W, H) in {(16, 8), (8, 4)}; OptPWSignificance (PW) instances
-// exist for uint16 columns and W = 16 only (make_plan keeps other PW runs off this path)
-template <int NK, class COL, int W, bool BITS, bool PW = false>
-static int occ_fw_t(int wpb, size_t lds);
-template <int NK, class COL, int W, bool BITS, bool PW = false>
-static hipError_t launch_fw_t(const SweepArgs& a, hipStream_t s)
-{
-    unsigned blocks = (unsigned)((a.n_chunk + a.wpb - 1) / a.wpb);
-    if (a.wq) {
-        // persistent grid: every resident wave slot once, the rest from the queue
-        static int nb_c = 0, wpb_c = 0;
-        static size_t lds_c = 0;
-        if (wpb_c != a.wpb || lds_c != a.lds_total) {
-            nb_c = occ_fw_t<NK, COL, W, BITS, PW>(a.wpb, a.lds_total);
-            wpb_c = a.wpb;
-            lds_c = a.lds_total;
-        }
-        const int nb = nb_c;
-        const unsigned cap = (unsigned)(nb > 0 ? nb : 1) * (unsigned)rq_cu_count();
-        if (cap < blocks) blocks = cap;
-    }
-    hipLaunchKernelGGL((rq_sweep_fw<NK, COL, W, W / 2, BITS, PW>), dim3(blocks), dim3(64 * a.wpb), a.lds_total, s, a);
-    return hipGetLastError();
-}
-template <class COL, int W, bool PW = false>
-static hipError_t launch_fw_k(const SweepArgs& a, int nK, hipStream_t s)
-{
-    switch (nK) {
-    case 1: return launch_fw_t<1, COL, W, false, PW>(a, s);
-    case 2: return launch_fw_t<2, COL, W, false, PW>(a, s);
-    case 3: return launch_fw_t<3, COL, W, false, PW>(a, s);
-    default: return launch_fw_t<4, COL, W, false, PW>(a, s);
-    }
-}
-hipError_t rq_launch_sweep_fw(const SweepArgs& a, int nK, int col16, int W, int bits, hipStream_t s)
-{
-    if (a.n_chunk <= 0) return hipSuccess;
-    if (a.pw_c) {
-        if (!col16 || W != 16) return hipErrorInvalidValue;
-        return bits ? launch_fw_t<1, uint16_t, 16, true, true>(a, s) : launch_fw_k<uint16_t, 16, true>(a, nK, s);
-    }
-    if (bits) return W == 16 ? launch_fw_t<1, uint16_t, 16, true>(a, s) : launch_fw_t<1, uint16_t, 8, true>(a, s);
-    if (W == 16) return col16 ? launch_fw_k<uint16_t, 16>(a, nK, s) : launch_fw_k<int, 16>(a, nK, s);
-    return col16 ? launch_fw_k<uint16_t, 8>(a, nK, s) : launch_fw_k<int, 8>(a, nK, s);
-}
-template <int NK, class COL, int W, bool BITS, bool PW>
-static int occ_fw_t(int wpb, size_t lds)
-{
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rq_sweep_fw<NK, COL, W, W / 2, BITS, PW>, 64 * wpb,
-                                                      lds) != hipSuccess)
-        return 0;
-    return nb;
-}
-template <class COL, int W, bool PW = false>
-static int occ_fw_k(int nK, int wpb, size_t lds)
-{
-    switch (nK) {
-    case 1: return occ_fw_t<1, COL, W, false, PW>(wpb, lds);
-    case 2: return occ_fw_t<2, COL, W, false, PW>(wpb, lds);
-    case 3: return occ_fw_t<3, COL, W, false, PW>(wpb, lds);
-    default: return occ_fw_t<4, COL, W, false, PW>(wpb, lds);
-    }
-}
-int rq_fw_blocks_per_cu(int nK, int col16, int W, int bits, int wpb, size_t lds, int pw)
-{
-    if (pw) {
-        if (!col16 || W != 16) return -1;
-        return bits ? occ_fw_t<1, uint16_t, 16, true, true>(wpb, lds) : occ_fw_k<uint16_t, 16, true>(nK, wpb, lds);
-    }
-    if (bits) return W == 16 ? occ_fw_t<1, uint16_t, 16, true>(wpb, lds) : occ_fw_t<1, uint16_t, 8, true>(wpb, lds);
-    if (W == 16) return col16 ? occ_fw_k<uint16_t, 16>(nK, wpb, lds) : occ_fw_k<int, 16>(nK, wpb, lds);
-    return col16 ? occ_fw_k<uint16_t, 8>(nK, wpb, lds) : occ_fw_k<int, 8>(nK, wpb, lds);
 }
 
 template <int NK, int WPE>

@@ -16,4 +16,5 @@ for k in range(2):
     rc = lib.rq_phase_clock(out)
     tot = sum(out[:6])
     names = ["A1 generation", "window + cut", "stage + rank sort", "B controller", "C aggregates", "rows"]
-    print(rc, {n: round(out[q] / tot, 3) for q, n in enumerate(names)}, "per wave Mticks", tot / 1e4 / 1e6)
+    print(rc, {n: round(out[q] / tot, 3) for q, n in enumerate(names)}, "per replica Mticks", tot / 1e4 / 1e6)
+    print("refill iterations per replica %.1f, lanes stepping per iteration %.2f" % (out[6] / 1e4, out[7] / max(out[6], 1)))
