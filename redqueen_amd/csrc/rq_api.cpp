@@ -363,11 +363,12 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
         const size_t o_cbf = sh;  sh = align_up(sh + 4 * g->n_str, 16);
         int only_w = 0;
         if (const char* e = getenv("RQ_FW_W")) only_w = atoi(e);   // tuning only
-        for (int W : {16, 8}) {
+        for (int W : {32, 16, 8}) {
             if (!p->fw) break;
             if (only_w && W != only_w) continue;
             if (pw && W != 16) continue;
-            const int H = W / 2;
+            if (W == 32 && !p->bits) continue;   // 32-deep rings: K = 1 bitset instance only
+            const int H = W > 16 ? 8 : W / 2;    // register window
             const size_t r_off = align_up(8 * (size_t)g->n_str, 16);
             // per wave: BITS -> (F, T) word pairs [nw]; else int16 sink ranks
             const size_t w_off = align_up(r_off + (p->bits ? 8 * (size_t)((g->nw + 1) & ~1) : 2 * (size_t)p->n_sinks_pad), 16);
@@ -379,7 +380,7 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
                 int blocks = rq_fw_blocks_per_cu(p->nK, c16, W, p->bits, wpb, tot, pw);
                 if (blocks <= 0) blocks = (int)std::min<size_t>(kLdsMax / tot, 16 / wpb);
                 const int waves = blocks * wpb;
-                const int score = waves * 4 + (W == 16 ? 1 : 0);
+                const int score = waves * 4 + (W == 16 ? 2 : W == 32 ? 1 : 0);
                 if (score > best) {
                     best = score;
                     p->gwin = W; p->fw_h = H; p->gwpb = wpb; p->gcol_lds = c16; p->gcol16 = c16;

@@ -292,6 +292,17 @@ __device__ __forceinline__ int stage_rank(const double* st_t, int n, double ti, 
 }
 
 // min of a double over the 64 lanes (every lane gets it)
+// v_min_f64 without the compiler's sNaN canonicalisation of both inputs (operands
+// here are times or +INF, never NaN).  The trailing s_nop covers the two wait
+// states a following DPP read of the result needs (the hazard recognizer does not
+// look into inline asm).
+__device__ __forceinline__ double min_raw(double a, double b)
+{
+    double r;
+    __asm__("v_min_f64 %0, %1, %2\n\ts_nop 1" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 __device__ __forceinline__ double wave_min_f64(double x)
 {
 #define RQ_MIN_STAGE(CTRL, RM)                                                                     \
@@ -301,7 +312,7 @@ __device__ __forceinline__ double wave_min_f64(double x)
                                                                   0xF, false);                     \
         const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0x7FF00000, (int)(uint32_t)(b >> 32), \
                                                                   CTRL, RM, 0xF, false);           \
-        x = fmin(x, rq_bits_dbl(((uint64_t)hi << 32) | lo));                                       \
+        x = min_raw(x, rq_bits_dbl(((uint64_t)hi << 32) | lo));                                    \
     }
     RQ_MIN_STAGE(0xB1, 0xF)
     RQ_MIN_STAGE(0x4E, 0xF)
@@ -314,6 +325,43 @@ __device__ __forceinline__ double wave_min_f64(double x)
 }
 
 // the next double above finite x
+// inclusive prefix min over the 64 lanes (times / +INF): row shifts 1, 2, 4, 8 then
+// row broadcasts 15, 31.  A lane a step does not write keeps the DPP `old`, here
+// the previous step's shifted value t, which is >= the lane's running min already,
+// so min(v, t) leaves it unchanged (step 1 takes v itself).
+__device__ __forceinline__ double wave_scan_min_f64(double v)
+{
+    uint64_t b = rq_dbl_bits(v);
+    uint32_t tlo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)b, (int)(uint32_t)b, 0x111, 0xF, 0xF, false);
+    uint32_t thi = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(b >> 32), (int)(uint32_t)(b >> 32), 0x111,
+                                                          0xF, 0xF, false);
+    v = min_raw(v, rq_bits_dbl(((uint64_t)thi << 32) | tlo));
+#define RQ_SCANMIN_STAGE(CTRL, RM)                                                                      \
+    {                                                                                                   \
+        b = rq_dbl_bits(v);                                                                             \
+        tlo = (uint32_t)__builtin_amdgcn_update_dpp((int)tlo, (int)(uint32_t)b, CTRL, RM, 0xF, false);  \
+        thi = (uint32_t)__builtin_amdgcn_update_dpp((int)thi, (int)(uint32_t)(b >> 32), CTRL, RM, 0xF, \
+                                                    false);                                             \
+        v = min_raw(v, rq_bits_dbl(((uint64_t)thi << 32) | tlo));                                       \
+    }
+    RQ_SCANMIN_STAGE(0x112, 0xF)
+    RQ_SCANMIN_STAGE(0x114, 0xF)
+    RQ_SCANMIN_STAGE(0x118, 0xF)
+    RQ_SCANMIN_STAGE(0x142, 0xA)
+    RQ_SCANMIN_STAGE(0x143, 0xC)
+#undef RQ_SCANMIN_STAGE
+    return v;
+}
+// the value of lane l - 1 (+INF at lane 0): DPP wave_shr:1
+__device__ __forceinline__ double wave_shr1_inf_f64(double v)
+{
+    const uint64_t b = rq_dbl_bits(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, 0x138, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0x7FF00000, (int)(uint32_t)(b >> 32), 0x138, 0xF, 0xF,
+                                                              false);
+    return rq_bits_dbl(((uint64_t)hi << 32) | lo);
+}
+
 __device__ __forceinline__ double next_up(double x)
 {
     if (x == 0.0) return rq_bits_dbl(1ull);

@@ -475,15 +475,9 @@ __device__ __forceinline__ void controller_tile(int n, bool act, double tt, int 
     int s0 = 0;
     double cur = opt_next;
     for (;;) {
-        double inc = (lane >= s0 && act) ? c : RQ_INF;
-#pragma unroll
-        for (int sh = 1; sh < 64; sh <<= 1) {
-            const double u = __shfl_up(inc, sh, 64);
-            if (lane >= sh) inc = fmin(inc, u);
-        }
-        double ex = __shfl_up(inc, 1, 64);
-        if (lane == 0) ex = RQ_INF;
-        const double m = fmin(cur, ex);
+        // prefix min of the candidates from lane s0 on (DPP), then shifted one lane
+        const double inc = wave_scan_min_f64((lane >= s0 && act) ? c : RQ_INF);
+        const double m = min_raw(cur, wave_shr1_inf_f64(inc));
         const uint64_t b = __ballot(lane >= s0 && act && (m < tt || (m == tt && cb)));
         if (b == 0) {
             if (n > 0) cur = fmin(cur, bcast_d(inc, n - 1));

@@ -479,7 +479,7 @@ static hipError_t launch_fw_t(const SweepArgs& a, hipStream_t s)
         const unsigned cap = (unsigned)(nb > 0 ? nb : 1) * (unsigned)rq_cu_count();
         if (cap < blocks) blocks = cap;
     }
-    hipLaunchKernelGGL((rq_sweep_fw<NK, COL, W, W / 2, BITS, PW>), dim3(blocks), dim3(64 * a.wpb), a.lds_total, s, a);
+    hipLaunchKernelGGL((rq_sweep_fw<NK, COL, W, (W > 16 ? 8 : W / 2), BITS, PW>), dim3(blocks), dim3(64 * a.wpb), a.lds_total, s, a);
     return hipGetLastError();
 }
 template <class COL, int W, bool PW = false>
@@ -499,7 +499,9 @@ hipError_t rq_launch_sweep_fw(const SweepArgs& a, int nK, int col16, int W, int 
         if (!col16 || W != 16) return hipErrorInvalidValue;
         return bits ? launch_fw_t<1, uint16_t, 16, true, true>(a, s) : launch_fw_k<uint16_t, 16, true>(a, nK, s);
     }
-    if (bits) return W == 16 ? launch_fw_t<1, uint16_t, 16, true>(a, s) : launch_fw_t<1, uint16_t, 8, true>(a, s);
+    if (bits)
+        return W == 32 ? launch_fw_t<1, uint16_t, 32, true>(a, s)
+             : W == 16 ? launch_fw_t<1, uint16_t, 16, true>(a, s) : launch_fw_t<1, uint16_t, 8, true>(a, s);
     if (W == 16) return col16 ? launch_fw_k<uint16_t, 16>(a, nK, s) : launch_fw_k<int, 16>(a, nK, s);
     return col16 ? launch_fw_k<uint16_t, 8>(a, nK, s) : launch_fw_k<int, 8>(a, nK, s);
 }
@@ -507,7 +509,7 @@ template <int NK, class COL, int W, bool BITS, bool PW>
 static int occ_fw_t(int wpb, size_t lds)
 {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rq_sweep_fw<NK, COL, W, W / 2, BITS, PW>, 64 * wpb,
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rq_sweep_fw<NK, COL, W, (W > 16 ? 8 : W / 2), BITS, PW>, 64 * wpb,
                                                       lds) != hipSuccess)
         return 0;
     return nb;
@@ -528,7 +530,9 @@ int rq_fw_blocks_per_cu(int nK, int col16, int W, int bits, int wpb, size_t lds,
         if (!col16 || W != 16) return -1;
         return bits ? occ_fw_t<1, uint16_t, 16, true, true>(wpb, lds) : occ_fw_k<uint16_t, 16, true>(nK, wpb, lds);
     }
-    if (bits) return W == 16 ? occ_fw_t<1, uint16_t, 16, true>(wpb, lds) : occ_fw_t<1, uint16_t, 8, true>(wpb, lds);
+    if (bits)
+        return W == 32 ? occ_fw_t<1, uint16_t, 32, true>(wpb, lds)
+             : W == 16 ? occ_fw_t<1, uint16_t, 16, true>(wpb, lds) : occ_fw_t<1, uint16_t, 8, true>(wpb, lds);
     if (W == 16) return col16 ? occ_fw_k<uint16_t, 16>(nK, wpb, lds) : occ_fw_k<int, 16>(nK, wpb, lds);
     return col16 ? occ_fw_k<uint16_t, 8>(nK, wpb, lds) : occ_fw_k<int, 8>(nK, wpb, lds);
 }
