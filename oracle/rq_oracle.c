@@ -780,7 +780,7 @@ static int engine_stream(const rqo_source* s, uint32_t salt, double start, doubl
                 double v = pnext(&p);
                 double tc = t + x * inv;
                 if (!(tc <= end)) return 0;
-                double decay = rq_exp(nbeta * (tc - tau));
+                double decay = rq_exp_t(nbeta * (tc - tau), rq_exp_tab);
                 double rate = l0 + eta * decay;
                 if (v * B < rate) {   /* engine: division-free thinning test */
                     eta = eta * decay + alpha;
@@ -966,7 +966,7 @@ done:
 /* Batched CPU baseline (engine model + Appendix-B metrics, pthreads)         */
 /* ------------------------------------------------------------------------ */
 double rqo_spec_log(double x) { return rq_log(x); }
-double rqo_spec_exp(double x) { return rq_exp(x); }
+double rqo_spec_exp(double x) { return rq_exp_t(x, rq_exp_tab); }
 
 typedef struct {
     const rqo_scenario* sc; int64_t r0, r1; uint32_t seed0; int randomize; const double* rates;

@@ -134,7 +134,7 @@ struct Plan {
     bool log = false, bits = false;
     // K=1 on per-wave LDS sink bits for graphs past the bitset variant (> 64 sources)
     bool bl = false;
-    size_t g_fb = 0;
+    size_t g_fb = 0, g_etab = 0;
     // fused windowed sweep (n_str <= 64): arrivals generated in-kernel, window depth fw_h
     bool fw = false;
     int fw_h = 8, mstride = 1;
@@ -361,6 +361,7 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
         const size_t o_ptr = sh;  sh = align_up(sh + 4 * (g->n_str + 1), 16);
         const size_t o_odf = sh;  sh = align_up(sh + 4 * g->n_str, 16);
         const size_t o_cbf = sh;  sh = align_up(sh + 4 * g->n_str, 16);
+        const size_t o_etab = sh; sh = align_up(sh + 64 * 8, 16);   // rq_exp's table
         int only_w = 0;
         if (const char* e = getenv("RQ_FW_W")) only_w = atoi(e);   // tuning only
         for (int W : {32, 16, 8}) {
@@ -387,6 +388,7 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
                     p->g_col = o_col; p->g_ptr = o_ptr; p->g_odf = o_odf; p->g_cbf = o_cbf;
                     p->g_wave = sh; p->g_wave_stride = stride; p->g_rank_off = r_off;
                     p->g_win_off = w_off; p->g_stage_off = s_off; p->g_x_off = 0; p->g_total = tot;
+                    p->g_etab = o_etab;
                 }
             }
         }
@@ -891,6 +893,7 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             sa.fbits = g->d_fbits.p;
             sa.nwl = (g->n_sinks + 31) / 32;
             sa.lds_fbits = p.g_fb;
+            sa.lds_etab = p.g_etab;
             if (const char* d = getenv("RQ_SWEEP_DBG")) sa.dbg = atoi(d);   // profiling only
             sa.tile_target = 58.0;   // measured on C3: 40 -> 895k, 48 -> 943k, 58 -> 964k, 62 -> 956k replicas/s
             if (const char* e = getenv("RQ_FW_TILE")) sa.tile_target = atof(e);   // tuning only

@@ -35,19 +35,22 @@ struct SrcGen {
     double tau, eta, B;     // Hawkes: last accepted time, excitation at tau, bound
     double inv;             // 1 / rate (Poisson), 1 / max rate (PWConst), 1 / B (Hawkes)
     double p0, p1, nbeta;   // rate | (l_0, alpha, -beta)
+    const uint64_t* etab;   // rq_exp's table (RQ_EXP_TAB_INIT): LDS or __constant__ copy
     const double* ta;       // PWConst change times / RealData times
     const double* tb;       // PWConst rates
     int na, ri;
 
     __device__ __forceinline__ void none()
     {
+        etab = nullptr;
         kind = RQ_SRC_NONE;
         done = true;
         d = 0u;
     }
 
-    __device__ __forceinline__ void init(const GenArgs& a, int j, int64_t i)
+    __device__ __forceinline__ void init(const GenArgs& a, int j, int64_t i, const uint64_t* etab_)
     {
+        etab = etab_;
         const bool is_ctrl = j == a.ctrl_idx;
         kind = is_ctrl ? a.ctrl_stream_kind : a.kind[j];
         const int64_t k = a.seed_mod > 0 ? i % a.seed_mod : i;
@@ -152,7 +155,7 @@ struct SrcGen {
             return true;
         }
         if (kind == RQ_SRC_HAWKES) {
-            const double decay = rq_exp(nbeta * (tc - tau));
+            const double decay = rq_exp_t(nbeta * (tc - tau), etab);
             const double rate = p0 + eta * decay;
             if (u2 * B < rate) {   // u2 < rate / B without the f64 division
                 eta = eta * decay + p1;

@@ -47,7 +47,7 @@ __global__ __launch_bounds__(256) void rq_gen_streams(GenArgs a)
     const int64_t o = a.chunk0 + rl;      // local output index
     const int64_t i = a.rep0 + o;         // global replica id (seeds)
     SrcGen gen;
-    gen.init(a, j, i);
+    gen.init(a, j, i, rq_exp_tab_c);
 
     double* out = a.streams + rl * a.capsum + a.st_off[j];   // 64-byte aligned (host pads)
     const int cap = a.cap[j];                                   // multiple of 8

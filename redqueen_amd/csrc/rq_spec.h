@@ -2,8 +2,9 @@
  * rq_spec.h -- arithmetic that DEFINES the engine's simulation semantics.
  *
  * Everything in here is evaluated bit-identically by the gfx950 kernels
- * (hipcc) and by the CPU oracle (gcc): only IEEE-754 double +, -, *, / and
- * integer/bit operations, no libm, and the translation units that include it
+ * (hipcc) and by the CPU oracle (gcc): only IEEE-754 double +, -, *, /, fused
+ * multiply-add (fma(): one rounding on both sides) and integer/bit operations, no
+ * other libm function, constant tables from rq_tables.h, and the translation units that include it
  * are compiled with -ffp-contract=off (the pragma below repeats that for
  * clang).  This is what makes "GPU event log == oracle event log, bit for bit"
  * a testable statement even though the GPU has no correctly rounded log/exp.
@@ -12,11 +13,11 @@
  *    same construction numpy's legacy RandomState uses for random_sample()
  *    (reference draws: opt_model.py:329 RandomState(seed); used at :433,
  *    :481, :484, :540).
- *  - rq_log()/rq_exp(): argument reduction + minimax polynomials in the
- *    classic fdlibm style (log: x = 2^k (1+f), Remez series in s = f/(2+f);
- *    exp: x = k ln2 + r, rational Remez form).  Both are within 1 ulp of the
- *    correctly rounded result over the ranges the engine uses; the oracle
- *    tests pin that against glibc.
+ *  - rq_log(): argument reduction + minimax polynomial in the classic fdlibm
+ *    style (x = 2^k (1+f), Remez series in s = f/(2+f)); rq_exp_t(): table-driven
+ *    (2^(j/32) from rq_tables.h, degree-6 Taylor polynomial, no division).  Both
+ *    are within 1 ulp of the correctly rounded result over the ranges the engine
+ *    uses; the oracle tests pin that against glibc.
  *  - rq_std_exponential(u) = -log(1-u): numpy legacy_standard_exponential.
  *
  * This header is plain C99 so the oracle (C) can include it; the HIP build
@@ -26,12 +27,16 @@
 #define RQ_SPEC_H
 
 #include <stdint.h>
+#include <math.h>
+#include "rq_tables.h"
 
 #if defined(__HIPCC__)
 #define RQ_HD __host__ __device__ __forceinline__
+#define RQ_HD_COLD static __host__ __device__ __attribute__((noinline))
 #pragma clang fp contract(off)
 #else
 #define RQ_HD static inline
+#define RQ_HD_COLD static
 #endif
 
 RQ_HD uint64_t rq_dbl_bits(double x)
@@ -101,41 +106,49 @@ RQ_HD double rq_log(double x)
     return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
 }
 
-/* e^x for finite x; large negative -> 0, large positive -> +inf. */
-RQ_HD double rq_exp(double x)
+/* e^x, table-driven (no division): x = k ln2/32 + r with k = round(32 x / ln2) from the
+ * 1.5 * 2^52 shift, |r| <= ln2/64; e^x = 2^(k>>5) * s_j * (1 + tail_j) * e^r with
+ * s_j = 2^(j/32) (j = k & 31, rq_tables.h) and e^r - 1 = r + r^2 (1/2 + r/6 + r^2/24 +
+ * r^3/120 + r^4/720) (truncation < 2^-58).  Products go through fma (one rounding,
+ * identical on gfx950 and in C's fma()).  `adj` is added to the scale's bits (the
+ * out-of-range path pre-scales by 2^+-1000).  `tab` is RQ_EXP_TAB_INIT (kernels pass
+ * an LDS or __constant__ copy). */
+RQ_HD double rq_exp_core(double x, const uint64_t* tab, uint64_t adj)
 {
-    const double ln2HI = 6.93147180369123816490e-01;
-    const double ln2LO = 1.90821492927058770002e-10;
-    const double invln2 = 1.44269504088896338700e+00;
-    const double P1 = 1.66666666666666019037e-01;
-    const double P2 = -2.77777777770155933842e-03;
-    const double P3 = 6.61375632143793436117e-05;
-    const double P4 = -1.65339022054652515390e-06;
-    const double P5 = 4.13813679705723846039e-08;
+    const double kd0 = x * RQ_EXP_INVLN2N + 0x1.8p52;
+    const uint64_t ki = rq_dbl_bits(kd0);
+    const double kd = kd0 - 0x1.8p52;
+    double r = fma(kd, -RQ_EXP_LN2HI, x);
+    r = fma(kd, -RQ_EXP_LN2LO, r);
+    const uint32_t j = (uint32_t)ki & 31u;
+    const double tail = rq_bits_dbl(tab[2 * j]);
+    const double sc = rq_bits_dbl(tab[2 * j + 1] + (ki << 47) + adj);
+    const double r2 = r * r;
+    const double p = fma(r, fma(r, fma(r, fma(r, 1.0 / 720.0, 1.0 / 120.0), 1.0 / 24.0), 1.0 / 6.0), 0.5);
+    const double tmp = fma(r2, p, r) + tail;
+    return fma(sc, tmp, sc);
+}
 
+/* NaN -> NaN, x > 709.78 -> +inf, x < -745.14 -> 0; otherwise outside [-708, 709]
+ * the scale 2^(k>>5) is applied in two steps (2^+-1000 first) */
+RQ_HD_COLD double rq_exp_special(double x, const uint64_t* tab)
+{
     if (x != x) return x + x;
     if (x > 709.782712893383973096) return rq_bits_dbl(0x7ff0000000000000ull);
-    if (x < -745.13321910194110842) return 0.0;         /* underflow */
-    if (x > -3.7252902984e-09 && x < 3.7252902984e-09) return 1.0 + x;
-
-    /* k = round(x / ln2) */
-    double kd = x * invln2;
-    int32_t k = (int32_t)(kd < 0.0 ? kd - 0.5 : kd + 0.5);
-    double hi = x - (double)k * ln2HI;
-    double lo = (double)k * ln2LO;
-    double r = hi - lo;
-    double t = r * r;
-    double c = r - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))));
-    double y = 1.0 - ((lo - (r * c) / (2.0 - c)) - hi);
-
-    /* y * 2^k, with a two-step scale so k in [-1074, 1024] stays exact */
-    if (k >= -1021) {
-        if (k == 1024) return y * 2.0 * rq_bits_dbl((uint64_t)(1023 + 1023) << 52);
-        return y * rq_bits_dbl((uint64_t)(k + 1023) << 52);
-    }
-    return y * rq_bits_dbl((uint64_t)(k + 1000 + 1023) << 52) *
-           rq_bits_dbl((uint64_t)(-1000 + 1023) << 52);
+    if (x < -745.13321910194110842) return 0.0;
+    if (x < 0.0) return rq_exp_core(x, tab, 1000ull << 52) * rq_bits_dbl((uint64_t)(1023 - 1000) << 52);
+    return rq_exp_core(x, tab, (uint64_t)0 - (1000ull << 52)) * rq_bits_dbl((uint64_t)(1023 + 1000) << 52);
 }
+
+RQ_HD double rq_exp_t(double x, const uint64_t* tab)
+{
+    if (!(x >= -708.0 && x <= 709.0)) return rq_exp_special(x, tab);
+    return rq_exp_core(x, tab, 0);
+}
+
+#if !defined(__HIPCC__)
+static const uint64_t rq_exp_tab[64] = RQ_EXP_TAB_INIT;
+#endif
 
 /* numpy legacy_standard_exponential: -log(1 - U) */
 RQ_HD double rq_std_exponential(double u)
