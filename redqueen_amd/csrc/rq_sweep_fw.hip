@@ -141,21 +141,31 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
     int status = 0;
     double span = -1.0;   // adaptive tile width in time (< 0: not estimated yet)
     bool stop = false;
-    for (;;) {
-        // ---- A1: every unfinished ring shows >= H arrivals (refill all to W at once) ----
-        if (__ballot(!gen.done && fil - pos < H)) {
-            while (__ballot(!gen.done && fil - pos < W)) {
+    // A refill pass steps every ring below W once, so its cost is set by the neediest
+    // ring; passes taken only while >= thr rings are below W keep the lanes busy.
+    const int thr = a.n_str >= 6 ? (a.n_str + 2) / 3 : 2;
+    auto refill_pass = [&]() __attribute__((always_inline)) {
 #ifdef RQ_PHASE_CLOCK
-                ck[6] += 1;   // refill iterations
-                ck[7] += __popcll(__ballot(!gen.done && fil - pos < W));   // lanes stepping
+        ck[6] += 1;   // refill passes
+        ck[7] += __popcll(__ballot(!gen.done && fil - pos < W));   // lanes stepping
 #endif
-                if (!gen.done && fil - pos < W) {
-                    double tv;
-                    if (gen.step(&tv, a.end)) {
-                        ring[fil & (W - 1)] = tv;
-                        ++fil;
-                    }
-                }
+        if (!gen.done && fil - pos < W) {
+            double tv;
+            if (gen.step(&tv, a.end)) {
+                ring[fil & (W - 1)] = tv;
+                ++fil;
+            }
+        }
+    };
+    for (;;) {
+        // ---- A1: opportunistic passes while >= thr rings are below W; then, if some
+        //      unfinished ring shows < H arrivals, passes until every ring is full ----
+        {
+            const bool hard = __ballot(!gen.done && fil - pos < H) != 0;
+            for (;;) {
+                const uint64_t need = __ballot(!gen.done && fil - pos < W);
+                if (!need || (!hard && __popcll(need) < thr)) break;
+                refill_pass();
             }
         }
         RQ_CLK(0);   // A1: ring refills (arrival generation)
