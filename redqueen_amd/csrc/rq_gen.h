@@ -30,7 +30,7 @@ struct SrcGen {
     uint32_t w2, w3;        // second half of the last call
     uint32_t d;             // next draw index (< 2^32 draws per source)
     int kind;
-    bool done, needB;
+    bool done;
     double t;               // candidate base time
     double tau, eta, B;     // Hawkes: last accepted time, excitation at tau, bound
     double inv;             // 1 / rate (Poisson), 1 / max rate (PWConst), 1 / B (Hawkes)
@@ -68,7 +68,6 @@ struct SrcGen {
         w2 = w3 = 0u;
         d = 0u;
         done = false;
-        needB = true;
         t = a.start;
         tau = a.start;
         eta = 0.0;
@@ -85,6 +84,9 @@ struct SrcGen {
             p0 = a.p0[j];
             p1 = a.p1[j];
             nbeta = -a.p2[j];
+            B = p0;   // lambda at start (no excitation yet)
+            if (B > 0.0) inv = 1.0 / B;
+            else done = true;
         } else if (kind == RQ_SRC_PWCONST) {
             na = a.arr_n[j];
             ta = a.arr_a + a.arr_off[j];
@@ -120,16 +122,6 @@ struct SrcGen {
             done = ri >= na;
             return true;
         }
-        if (kind == RQ_SRC_HAWKES && needB) {
-            B = p0 + eta;
-            if (!(B > 0.0)) {
-                done = true;
-                return false;
-            }
-            inv = 1.0 / B;
-            t = tau;
-            needB = false;
-        }
         double u1, u2 = 0.0;
         if ((d & 1u) == 0u) {
             const uint32_t call = d >> 1;
@@ -157,18 +149,22 @@ struct SrcGen {
         if (kind == RQ_SRC_HAWKES) {
             const double decay = rq_exp_t(nbeta * (tc - tau), etab);
             const double rate = p0 + eta * decay;
-            if (u2 * B < rate) {   // u2 < rate / B without the f64 division
+            const bool acc = u2 * B < rate;   // u2 < rate / B without the f64 division
+            // accepted: the next candidate starts at tc under B = lambda just after it;
+            // rejected: lambda only decays until the next arrival, so lambda(tc) bounds it
+            // from here on -- thinning continues at the refreshed (lower) bound.  One
+            // division on the merged path (the two branches diverge within a wave).
+            if (acc) {
                 eta = eta * decay + p1;
                 tau = tc;
-                needB = true;
-                *out = tc;
-                return true;
+                B = p0 + eta;
+            } else {
+                B = rate;
             }
-            // rejected: lambda only decays until the next arrival, so lambda(tc) bounds
-            // it from here on -- thinning continues at the refreshed (lower) bound
-            B = rate;
-            inv = 1.0 / rate;
-            return false;
+            if (B > 0.0) inv = 1.0 / B;
+            else done = true;   // lambda == 0 from here on: no further arrival
+            if (acc) *out = tc;
+            return acc;
         }
         // PiecewiseConst: rate(t) = rates[bisect_right(change_times, t) - 1]
         int lo = 0, hi = na;

@@ -72,6 +72,11 @@ __global__ __launch_bounds__(256) void k(double* out, int iters)
                 philox4x32_10(c, 0x1234u, 0x5678u);
                 x[q] += rq_uniform53(c[0], c[1]) + rq_uniform53(c[2], c[3]);
                 s[q] = c[3];
+            } else if (V == 7) {   // Philox4x32-10 with a per-lane key (the generator's (seed, salt))
+                uint32_t c[4] = {(uint32_t)i, 0u, 0u, 0u};
+                philox4x32_10(c, s[q], 0x52510000u | (threadIdx.x & 7));
+                x[q] += rq_uniform53(c[0], c[1]) + rq_uniform53(c[2], c[3]);
+                s[q] = c[3];
             } else if (V == 1) {   // -log(1 - u)
                 x[q] = rq_std_exponential(x[q] * 0.5);
             } else if (V == 2) {   // exp of a negative argument (fdlibm)
@@ -105,8 +110,9 @@ int main()
     hipEventCreate(&a);
     hipEventCreate(&b);
     const char* names[] = {"philox4x32-10 + 2 uniform53", "rq_std_exponential (rq_log)", "rq_exp (fdlibm)",
-                           "f64 division", "f64 mul+add", "rq_exp_t (__constant__ table)", "rq_exp_t (LDS table)"};
-    for (int v = 0; v < 7; ++v) {
+                           "f64 division", "f64 mul+add", "rq_exp_t (__constant__ table)", "rq_exp_t (LDS table)",
+                           "philox4x32-10, per-lane key"};
+    for (int v = 0; v < 8; ++v) {
         float best = 1e30f;
         for (int rep = 0; rep < 3; ++rep) {
             hipEventRecord(a);
@@ -117,7 +123,8 @@ int main()
             case 3: hipLaunchKernelGGL(k<3>, dim3(blocks), dim3(threads), 0, 0, out, iters); break;
             case 4: hipLaunchKernelGGL(k<4>, dim3(blocks), dim3(threads), 0, 0, out, iters); break;
             case 5: hipLaunchKernelGGL(k<5>, dim3(blocks), dim3(threads), 0, 0, out, iters); break;
-            default: hipLaunchKernelGGL(k<6>, dim3(blocks), dim3(threads), 0, 0, out, iters); break;
+            case 6: hipLaunchKernelGGL(k<6>, dim3(blocks), dim3(threads), 0, 0, out, iters); break;
+            default: hipLaunchKernelGGL(k<7>, dim3(blocks), dim3(threads), 0, 0, out, iters); break;
             }
             hipEventRecord(b);
             hipEventSynchronize(b);
