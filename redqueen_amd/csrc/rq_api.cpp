@@ -897,6 +897,14 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             if (const char* d = getenv("RQ_SWEEP_DBG")) sa.dbg = atoi(d);   // profiling only
             sa.tile_target = 58.0;   // measured on C3: 40 -> 895k, 48 -> 943k, 58 -> 964k, 62 -> 956k replicas/s
             if (const char* e = getenv("RQ_FW_TILE")) sa.tile_target = atof(e);   // tuning only
+            // refill policy (C3, sweep ms): forced passes only when a ring shows < 2 arrivals
+            // (the cut is bounded by each ring's last visible arrival), opportunistic passes
+            // while >= n_str / 2 rings are below W -- (H, n/3) 4.12, (2, n/3) 3.86,
+            // (2, n/2) 3.79, (2, 0.64 n) 3.89, (1, n/2) 3.84-3.88
+            sa.fw_hmin = std::min(2, p.fw_h);
+            if (const char* e = getenv("RQ_FW_HMIN")) sa.fw_hmin = std::max(1, std::min(p.fw_h, atoi(e)));   // tuning only
+            sa.fw_thr = g->n_str >= 6 ? (g->n_str + 1) / 2 : 2;
+            if (const char* e = getenv("RQ_FW_THR")) sa.fw_thr = std::max(1, atoi(e));   // tuning only
 #ifdef RQ_PHASE_CLOCK
             {
                 static unsigned long long* clk = nullptr;

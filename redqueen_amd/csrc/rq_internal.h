@@ -81,6 +81,8 @@ struct SweepArgs {
     int dbg;                 // profiling: 1 skip phase C, 2 skip sink updates, 3 skip phase B
     unsigned long long* clk; // RQ_PHASE_CLOCK builds only: per-phase s_memtime sums [8]
     double tile_target;      // fused sweep: arrivals a tile aims at (the cut adapts to it)
+    int fw_hmin;             // fused sweep: a ring showing fewer arrivals forces refill passes (1..H)
+    int fw_thr;              // fused sweep: opportunistic refill passes while >= fw_thr rings are below W
     int* wq;                 // fused sweep: replica work queue (zeroed per launch; null = one replica per wave)
     int col_in_lds, win;     // general sweep: CSR copied to LDS; arrival-ring depth
     size_t lds_col, lds_ptr, lds_odf, lds_cbf, lds_wave, lds_wave_stride, lds_rank_off, lds_win_off, lds_x_off, lds_mask,

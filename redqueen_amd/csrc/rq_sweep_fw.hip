@@ -141,9 +141,11 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
     int status = 0;
     double span = -1.0;   // adaptive tile width in time (< 0: not estimated yet)
     bool stop = false;
-    // A refill pass steps every ring below W once, so its cost is set by the neediest
-    // ring; passes taken only while >= thr rings are below W keep the lanes busy.
-    const int thr = a.n_str >= 6 ? (a.n_str + 2) / 3 : 2;
+    // A refill pass steps every ring below W once and costs the same however few lanes
+    // step; passes taken only while >= thr rings are below W keep the lanes busy, and a
+    // ring is forced full only when it shows fewer than fw_hmin arrivals (the cut below
+    // is bounded by each ring's last visible arrival, so a short ring only narrows it).
+    const int thr = a.fw_thr;
     auto refill_pass = [&]() __attribute__((always_inline)) {
 #ifdef RQ_PHASE_CLOCK
         ck[6] += 1;   // refill passes
@@ -159,9 +161,9 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
     };
     for (;;) {
         // ---- A1: opportunistic passes while >= thr rings are below W; then, if some
-        //      unfinished ring shows < H arrivals, passes until every ring is full ----
+        //      unfinished ring shows < hmin arrivals, passes until every ring is full ----
         {
-            const bool hard = __ballot(!gen.done && fil - pos < H) != 0;
+            const bool hard = __ballot(!gen.done && fil - pos < a.fw_hmin) != 0;
             for (;;) {
                 const uint64_t need = __ballot(!gen.done && fil - pos < W);
                 if (!need || (!hard && __popcll(need) < thr)) break;
@@ -174,9 +176,14 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
 #pragma unroll
         for (int q = 0; q < H; ++q) v[q] = q < avail ? ring[(pos + q) & (W - 1)] : RQ_INF;
         const bool more = !gen.done || avail > H;        // arrivals past the window exist
+        // the last arrival the window shows (avail >= hmin >= 1 for an unfinished ring):
+        // this ring's unseen arrivals are >= it, so it bounds the cut
+        double vb = v[0];
+#pragma unroll
+        for (int q = 1; q < H; ++q) vb = q < avail ? v[q] : vb;
         const double tfirst = wave_min_f64(v[0]);
         if (!(tfirst < RQ_INF)) break;                   // everything consumed
-        const double tmax = wave_min_f64(more ? v[H - 1] : RQ_INF);
+        const double tmax = wave_min_f64(more ? vb : RQ_INF);
 
         // ---- A2: the cut (exclusive): complete below tmax, <= 64 arrivals ----
         int c = 0, n = 0;
@@ -210,7 +217,7 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
             c = 0;
 #pragma unroll
             for (int q = 0; q < H; ++q) c += v[q] == tfirst ? 1 : 0;
-            const uint64_t bl = __ballot(more && v[H - 1] == tfirst);
+            const uint64_t bl = __ballot(more && vb == tfirst);
             const int lb = bl ? __ffsll((unsigned long long)bl) - 1 : 64;
             if (lane > lb) c = 0;
         }
