@@ -134,7 +134,8 @@ struct Plan {
     bool log = false, bits = false;
     // K=1 on per-wave LDS sink bits for graphs past the bitset variant (> 64 sources)
     bool bl = false;
-    size_t g_fb = 0, g_etab = 0;
+    size_t g_fb = 0, g_etab = 0, g_inv = 0;
+    bool g_inv_sh = false;   // general sweep: 1/c_j in the block's shared LDS (one grid point)
     // fused windowed sweep (n_str <= 64): arrivals generated in-kernel, window depth fw_h
     bool fw = false;
     int fw_h = 8, mstride = 1;
@@ -301,6 +302,9 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
             const size_t o_odf = sh;  sh = align_up(sh + 4 * g->n_str, 16);
             const size_t o_cbf = sh;  sh = align_up(sh + 4 * g->n_str, 16);
             const size_t o_fb = sh;   if (p->bl) sh = align_up(sh + 4 * (size_t)nwl, 16);
+            // one grid point: the 1/c_j table once per block instead of once per wave
+            const bool inv_sh = b->n_grid == 1;
+            const size_t o_inv = sh;  if (inv_sh) sh = align_up(sh + 8 * (size_t)g->n_str, 16);
             const int spl = p->spl;
             int only_w = 0;
             if (const char* e = getenv("RQ_G_W")) only_w = atoi(e);   // tuning only
@@ -308,7 +312,7 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
             for (int W : {8, 4}) {
                 if (p->log != (W == 8)) continue;
                 if (only_w && W != only_w) continue;
-                const size_t r_off = align_up(8 * (size_t)g->n_str, 16);
+                const size_t r_off = inv_sh ? 0 : align_up(8 * (size_t)g->n_str, 16);
                 const size_t rank_b = p->log ? 4 : (p->bits ? 0 : 2);   // fast: int16 saturating
                 // BL: two bits per sink (T, V words) in place of the int16 ranks
                 const size_t w_off = p->bl ? align_up(r_off + 8 * (size_t)nwl, 16)
@@ -337,6 +341,7 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
                         p->g_col = o_col; p->g_ptr = o_ptr; p->g_odf = o_odf; p->g_cbf = o_cbf;
                         p->g_wave = sh; p->g_wave_stride = stride; p->g_rank_off = r_off;
                         p->g_win_off = w_off; p->g_x_off = x_off; p->g_total = tot; p->g_fb = o_fb;
+                        p->g_inv = o_inv; p->g_inv_sh = inv_sh;
                     }
                 }
             }
@@ -894,6 +899,8 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             sa.nwl = (g->n_sinks + 31) / 32;
             sa.lds_fbits = p.g_fb;
             sa.lds_etab = p.g_etab;
+            sa.lds_invc = p.g_inv;
+            sa.invc_shared = !p.fw && p.g_inv_sh;
             if (const char* d = getenv("RQ_SWEEP_DBG")) sa.dbg = atoi(d);   // profiling only
             sa.tile_target = 58.0;   // measured on C3: 40 -> 895k, 48 -> 943k, 58 -> 964k, 62 -> 956k replicas/s
             if (const char* e = getenv("RQ_FW_TILE")) sa.tile_target = atof(e);   // tuning only

@@ -82,6 +82,8 @@ struct SweepArgs {
     unsigned long long* clk; // RQ_PHASE_CLOCK builds only: per-phase s_memtime sums [8]
     double tile_target;      // fused sweep: arrivals a tile aims at (the cut adapts to it)
     int fw_hmin;             // fused sweep: a ring showing fewer arrivals forces refill passes (1..H)
+    size_t lds_invc;         // general sweep, one grid point: 1/c_j [n_str] in the block's shared LDS
+    int invc_shared;         //   (else each wave loads its replica's grid point at the start of its wave region)
     int fw_thr;              // fused sweep: opportunistic refill passes while >= fw_thr rings are below W
     int* wq;                 // fused sweep: replica work queue (zeroed per launch; null = one replica per wave)
     int col_in_lds, win;     // general sweep: CSR copied to LDS; arrival-ring depth

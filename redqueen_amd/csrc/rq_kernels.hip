@@ -144,9 +144,14 @@ __global__ __launch_bounds__(LOG ? 256 : (SPL >= 4 ? 512 : 1024)) void rq_sweep(
     uint32_t* fbl = reinterpret_cast<uint32_t*>(base + a.lds_fbits);
     if (BL)
         for (int k = threadIdx.x; k < a.nwl; k += blockDim.x) fbl[k] = a.fbits[k];
+    // one grid point: the controller's 1/c_j table is the same for every replica, so the
+    // block holds one copy (its LDS goes to the sink columns instead of 8 per-wave copies)
+    double* invc_sh = reinterpret_cast<double*>(base + a.lds_invc);
+    if (a.invc_shared)
+        for (int j = threadIdx.x; j < a.n_str; j += blockDim.x) invc_sh[j] = a.inv_c[j];
     __syncthreads();   // block-shared tables ready; no block barrier below this line
     char* wb = base + a.lds_wave + (size_t)w * a.lds_wave_stride;
-    double* invc = reinterpret_cast<double*>(wb);
+    double* invc = a.invc_shared ? invc_sh : reinterpret_cast<double*>(wb);
     // ranks: exact int for the LOG variant (pivot cells average them); the fast
     // sweep only compares them with K-1, so int16 saturating at 32767 is exact
     using RT = typename std::conditional<LOG, int, int16_t>::type;
@@ -164,7 +169,8 @@ __global__ __launch_bounds__(LOG ? 256 : (SPL >= 4 ? 512 : 1024)) void rq_sweep(
         uint32_t* tb = reinterpret_cast<uint32_t*>(wb + a.lds_rank_off);
         agl.init(tb, tb + a.nwl, fbl, a.nwl, lane, a.n_sinks);
     }
-    for (int j = lane; j < a.n_str; j += 64) invc[j] = a.inv_c[(int64_t)g * a.n_str + j];
+    if (!a.invc_shared)
+        for (int j = lane; j < a.n_str; j += 64) invc[j] = a.inv_c[(int64_t)g * a.n_str + j];
     if (!BITS && !BL)
         for (int c = lane; c < a.n_sinks; c += 64) rank[c] = -1;   // NaN: no row yet
     wave_lds_sync();
