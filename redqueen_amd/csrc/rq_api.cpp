@@ -912,6 +912,10 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             if (const char* e = getenv("RQ_FW_HMIN")) sa.fw_hmin = std::max(1, std::min(p.fw_h, atoi(e)));   // tuning only
             sa.fw_thr = g->n_str >= 6 ? (g->n_str + 1) / 2 : 2;
             if (const char* e = getenv("RQ_FW_THR")) sa.fw_thr = std::max(1, atoi(e));   // tuning only
+            // a forced run (some ring < fw_hmin) ends once every ring shows H arrivals, not W:
+            // (C3 sweep ms) fill to 16 3.85, 12 3.78, 8 3.69-3.71, 6 3.69, 4 3.71
+            sa.fw_hfill = p.fw_h;
+            if (const char* e = getenv("RQ_FW_HFILL")) sa.fw_hfill = std::max(1, std::min(p.gwin, atoi(e)));   // tuning only
 #ifdef RQ_PHASE_CLOCK
             {
                 static unsigned long long* clk = nullptr;

@@ -85,6 +85,7 @@ struct SweepArgs {
     size_t lds_invc;         // general sweep, one grid point: 1/c_j [n_str] in the block's shared LDS
     int invc_shared;         //   (else each wave loads its replica's grid point at the start of its wave region)
     int fw_thr;              // fused sweep: opportunistic refill passes while >= fw_thr rings are below W
+    int fw_hfill;            // fused sweep: a forced refill run ends once every ring shows >= fw_hfill
     int* wq;                 // fused sweep: replica work queue (zeroed per launch; null = one replica per wave)
     int col_in_lds, win;     // general sweep: CSR copied to LDS; arrival-ring depth
     size_t lds_col, lds_ptr, lds_odf, lds_cbf, lds_wave, lds_wave_stride, lds_rank_off, lds_win_off, lds_x_off, lds_mask,

@@ -160,14 +160,16 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
         }
     };
     for (;;) {
-        // ---- A1: opportunistic passes while >= thr rings are below W; then, if some
-        //      unfinished ring shows < hmin arrivals, passes until every ring is full ----
+        // ---- A1: opportunistic passes while >= thr rings are below W; if some unfinished
+        //      ring shows < hmin arrivals, passes until every ring shows >= hfill ----
         {
-            const bool hard = __ballot(!gen.done && fil - pos < a.fw_hmin) != 0;
+            bool hard = __ballot(!gen.done && fil - pos < a.fw_hmin) != 0;
             for (;;) {
                 const uint64_t need = __ballot(!gen.done && fil - pos < W);
                 if (!need || (!hard && __popcll(need) < thr)) break;
                 refill_pass();
+                // a forced run lasts until every ring shows >= fw_hfill arrivals
+                if (hard) hard = __ballot(!gen.done && fil - pos < a.fw_hfill) != 0;
             }
         }
         RQ_CLK(0);   // A1: ring refills (arrival generation)
