@@ -21,6 +21,7 @@
 
 #include "../../include/rq.h"
 #include "rq_internal.h"
+#include "rq_tables.h"
 
 namespace {
 
@@ -366,7 +367,7 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
         const size_t o_ptr = sh;  sh = align_up(sh + 4 * (g->n_str + 1), 16);
         const size_t o_odf = sh;  sh = align_up(sh + 4 * g->n_str, 16);
         const size_t o_cbf = sh;  sh = align_up(sh + 4 * g->n_str, 16);
-        const size_t o_etab = sh; sh = align_up(sh + 64 * 8, 16);   // rq_exp's table
+        const size_t o_etab = sh; sh = align_up(sh + RQ_EXP_TAB_N * 8, 16);   // rq_exp's table
         int only_w = 0;
         if (const char* e = getenv("RQ_FW_W")) only_w = atoi(e);   // tuning only
         for (int W : {32, 16, 8}) {

@@ -22,7 +22,7 @@
 namespace rq {
 
 // rq_exp's table (rq_tables.h) in constant memory; the fused sweep stages a copy in LDS
-static __constant__ uint64_t rq_exp_tab_c[64] = RQ_EXP_TAB_INIT;
+static __constant__ uint64_t rq_exp_tab_c[RQ_EXP_TAB_N] = RQ_EXP_TAB_INIT;
 
 __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1)
 {

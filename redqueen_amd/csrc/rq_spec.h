@@ -112,7 +112,7 @@ RQ_HD double rq_log(double x)
  * r^3/120 + r^4/720) (truncation < 2^-58).  Products go through fma (one rounding,
  * identical on gfx950 and in C's fma()).  `adj` is added to the scale's bits (the
  * out-of-range path pre-scales by 2^+-1000).  `tab` is RQ_EXP_TAB_INIT (kernels pass
- * an LDS or __constant__ copy). */
+ * an LDS or __constant__ copy; its words 64..67 are the polynomial's coefficients). */
 RQ_HD double rq_exp_core(double x, const uint64_t* tab, uint64_t adj)
 {
     const double kd0 = x * RQ_EXP_INVLN2N + 0x1.8p52;
@@ -124,7 +124,9 @@ RQ_HD double rq_exp_core(double x, const uint64_t* tab, uint64_t adj)
     const double tail = rq_bits_dbl(tab[2 * j]);
     const double sc = rq_bits_dbl(tab[2 * j + 1] + (ki << 47) + adj);
     const double r2 = r * r;
-    const double p = fma(r, fma(r, fma(r, fma(r, 1.0 / 720.0, 1.0 / 120.0), 1.0 / 24.0), 1.0 / 6.0), 0.5);
+    const double c6 = rq_bits_dbl(tab[64]), c24 = rq_bits_dbl(tab[65]);     /* 1/6, 1/24 */
+    const double c120 = rq_bits_dbl(tab[66]), c720 = rq_bits_dbl(tab[67]);  /* 1/120, 1/720 */
+    const double p = fma(r, fma(r, fma(r, fma(r, c720, c120), c24), c6), 0.5);
     const double tmp = fma(r2, p, r) + tail;
     return fma(sc, tmp, sc);
 }
@@ -147,7 +149,7 @@ RQ_HD double rq_exp_t(double x, const uint64_t* tab)
 }
 
 #if !defined(__HIPCC__)
-static const uint64_t rq_exp_tab[64] = RQ_EXP_TAB_INIT;
+static const uint64_t rq_exp_tab[RQ_EXP_TAB_N] = RQ_EXP_TAB_INIT;
 #endif
 
 /* numpy legacy_standard_exponential: -log(1 - U) */

@@ -58,7 +58,7 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
             msk[e] = (jj < a.n_str && ww < a.nw) ? a.masks[jj * a.nw + ww] : 0u;
         }
     uint64_t* etab = reinterpret_cast<uint64_t*>(base + a.lds_etab);
-    for (int e = threadIdx.x; e < 64; e += blockDim.x) etab[e] = rq_exp_tab_c[e];
+    for (int e = threadIdx.x; e < RQ_EXP_TAB_N; e += blockDim.x) etab[e] = rq_exp_tab_c[e];
     for (int j = threadIdx.x; j <= a.n_str; j += blockDim.x) cptr[j] = a.csr_ptr[j];
     for (int j = threadIdx.x; j < a.n_str; j += blockDim.x) {
         odf[j] = a.outdeg_f[j];

@@ -11,7 +11,7 @@
 
 using namespace rq;
 
-static __constant__ uint64_t etab_c[64] = RQ_EXP_TAB_INIT;
+static __constant__ uint64_t etab_c[RQ_EXP_TAB_N] = RQ_EXP_TAB_INIT;
 
 /* fdlibm exp (the round-1/2 engine's rq_exp), for comparison */
 RQ_HD double rq_exp_fdlibm(double x)
@@ -54,8 +54,8 @@ template <int V>
 __global__ __launch_bounds__(256) void k(double* out, int iters)
 {
     constexpr int C = 8;
-    __shared__ uint64_t etab_l[64];
-    if (threadIdx.x < 64) etab_l[threadIdx.x] = etab_c[threadIdx.x];
+    __shared__ uint64_t etab_l[RQ_EXP_TAB_N];
+    if (threadIdx.x < RQ_EXP_TAB_N) etab_l[threadIdx.x] = etab_c[threadIdx.x];
     __syncthreads();
     double x[C], acc = 0.0;
     uint32_t s[C];
