@@ -29,6 +29,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.29 TB/s measured copy
+N_CU = 256              # MI355X: 8 XCDs x 32 CUs
 # algorithmic bytes per unit (DESIGN.md "Roofline accounting")
 SWEEP_B_PER_WALL_EVENT = 8      # read one arrival time
 SWEEP_B_PER_ROW = 24            # write t f64 + sumR f64 + nvalid u32 + cnt[K=1] u32
@@ -60,8 +61,34 @@ def cpu_baseline(so, n_threads, sample, Ks=(1,)):
     return sample / el, tot / el, el
 
 
-def pmc_summary_path(workload):
-    return os.path.join(ROOT, "profiles", "r02_%s_pmc_summary.json" % workload)
+def pmc_summary_paths(workload):
+    """Committed PMC summaries of this workload, newest round first."""
+    import glob
+    return sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_%s_pmc_summary.json" % workload)),
+                  reverse=True)
+
+
+def ref_cpu_baseline(workload):
+    """The reference itself (pure Python, multiprocessing over replicas) timed in the
+    build container by scripts/ref_cpu_baseline.py -- /root/reference does not exist on
+    the GPU box, so the measured line is read from the committed profile."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_ref_cpu_baseline.jsonl")),
+                       reverse=True):
+        for ln in open(path):
+            try:
+                d = json.loads(ln)
+            except ValueError:
+                continue
+            if d.get("config") == workload:
+                return {"value": d["replicas_per_s"], "unit": "replicas/s", "cores": d["procs"],
+                        "kind": "reference",
+                        "sample": "%d %s replicas of the reference's Manager.run_dynamic + "
+                                  "time_in_top_k/average_rank, multiprocessing.Pool(%d), %.0f s "
+                                  "(measured in the build container, %s)" %
+                                  (d["replicas"], workload.upper(), d["procs"], d["wall_s"],
+                                   os.path.relpath(path, ROOT))}
+    return None
 
 
 def pmc_traffic(workload, R, plan):
@@ -70,22 +97,30 @@ def pmc_traffic(workload, R, plan):
     the gfx950 correction + WRITE_SIZE), when workload, replicas and plan match AND
     its build stamp is the loaded library's (librq.so + sources sha256)."""
     from redqueen_amd import _lib as L
-    path = pmc_summary_path(workload)
-    try:
-        d = json.load(open(path))
-    except (OSError, ValueError):
-        return None, None, None
-    meta = d.get("_meta", {})
-    if meta.get("workload") != workload or meta.get("replicas") != R or \
-            meta.get("variant") != plan["variant"]:
-        return None, None, None
     stamp = L.build_stamp()
-    if any(meta.get(k) != v for k, v in stamp.items()):
-        return None, None, None
-    for k, v in d.items():
-        if k.startswith("rq_sweep") and "hbm_write_bytes" in v and "hbm_read_bytes" in v:
-            issue = {q: v[q] for q in ("frac_active_inst", "frac_wait_any", "frac_wait_inst") if q in v}
-            return v["hbm_read_bytes"] + v["hbm_write_bytes"], os.path.relpath(path, ROOT), issue
+    for path in pmc_summary_paths(workload):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        meta = d.get("_meta", {})
+        if meta.get("workload") != workload or meta.get("replicas") != R or \
+                meta.get("variant") != plan["variant"]:
+            continue
+        if any(meta.get(k) != v for k, v in stamp.items()):
+            continue
+        for k, v in d.items():
+            if k.startswith("rq_sweep") and "hbm_write_bytes" in v and "hbm_read_bytes" in v:
+                issue = {q: v[q] for q in ("frac_active_inst", "frac_wait_any", "frac_wait_inst") if q in v}
+                c = v.get("counters", {})
+                # VALU issue ceiling: one wave64 VALU instruction per 2 cycles per SIMD
+                # (MI355X_MICROARCH.md), 4 SIMDs per CU, over the launch's cycles on one
+                # XCD (GRBM_GUI_ACTIVE is summed over the 8 XCDs)
+                if c.get("SQ_INSTS_VALU") and c.get("GRBM_GUI_ACTIVE"):
+                    cyc = c["GRBM_GUI_ACTIVE"] / 8.0
+                    issue["valu_insts"] = c["SQ_INSTS_VALU"]
+                    issue["issue_frac"] = c["SQ_INSTS_VALU"] / (N_CU * 4 * cyc / 2.0)
+                return v["hbm_read_bytes"] + v["hbm_write_bytes"], os.path.relpath(path, ROOT), issue
     return None, None, None
 
 
@@ -144,13 +179,18 @@ def main():
     mask = L.ST_ROWS_OVERFLOW | L.ST_STREAM_OVERFLOW
 
     def accumulate(res, acc):
-        # per step: one reduction of the count columns, one of the overflow bits
+        # per step: one reduction of the count columns, one of the overflow bits, one
+        # count of the replicas the fast sweep flagged RQ_ST_TIE (equal event times:
+        # check=True would rerun them on the exact sequential sweep; never taken by
+        # the continuous-time bench worlds, and reported so that it shows if it is)
         acc[0] += res.counts.sum(0)
         torch.maximum(acc[1], (res.status & mask).max(), out=acc[1])
+        acc[2] += ((res.status & L.ST_TIE) != 0).sum()
 
     def new_acc():
         return [torch.zeros(4, dtype=torch.int64, device=dev),
-                torch.zeros((), dtype=torch.int32, device=dev)]
+                torch.zeros((), dtype=torch.int32, device=dev),
+                torch.zeros((), dtype=torch.int64, device=dev)]
 
     # the warmup runs the exact timed body: HIP loads a kernel's code object on its first
     # launch (tens of ms for torch's), which must not land in the timed region
@@ -170,7 +210,7 @@ def main():
     for k in range(a.steps):
         res, means = step(k)
         accumulate(res, acc)
-    csum, status = acc
+    csum, status, ties = acc
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -211,6 +251,10 @@ def main():
         if gen_ms > 0 else None
 
     traffic, traffic_src, issue = pmc_traffic(a.workload, R, plan)
+    if issue and "issue_frac" in issue:
+        # the same ceiling over this run's own HIP-event launch time at the PMC run's clock
+        issue["issue_frac_2400mhz_bench_time"] = issue["valu_insts"] / (
+            N_CU * 4 * 2.4e9 / 2.0 * sweep_ms * 1e-3)
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
@@ -242,20 +286,24 @@ def main():
             "events_per_sec": ev_rate,
             "events_per_replica": local_ev / replicas,
             "overflow": int(status.item()),
+            "tie_replicas": int(ties.item()),
             "kernels_ms_per_launch": {"gen_streams": gen_ms, "sweep": sweep_ms, "scan": scan_ms},
             "sweep_plan": plan,
             "roofline": {"bound": "hbm", "kernel": "rq_sweep", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic,
                          "traffic_source": traffic_src,
-                         # what does bound it: SQ issue / wait shares of the wave cycles (same PMC run)
+                         # what does bound it: SQ issue / wait shares of the wave cycles and
+                         # issue_frac = VALU instructions / the VALU issue ceiling (same PMC run)
                          "issue": issue,
+                         "issue_frac": issue.get("issue_frac") if issue else None,
                          "note": "sweep is latency/issue-bound (serial event chain per replica); "
                                  "algorithmic bytes = 24 B/pivot row written%s" %
                                  ("" if fused else " + 8 B/wall event read")},
             "scan_gbs": scan_gbs,
             "gen_gbs": gen_gbs,
             "cpu_baseline": cpu,
+            "cpu_baseline_reference": ref_cpu_baseline(a.workload),
         }
         print(json.dumps(line), flush=True)
     if world > 1:

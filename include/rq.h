@@ -237,7 +237,9 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out,
  *   counts                 : device [n_df][4]       num_tweets_of(src_id), world events
  *                            (-1 without event ids or if event_id decreases), pivot rows
  *                            (0: empty df; RQ_EUNSORTED: 't' decreases; RQ_EOVERFLOW: the df
- *                            needs the RQ_REPLAY_LARGE workspace), unique sinks
+ *                            needs the RQ_REPLAY_LARGE workspace; RQ_EINVAL: its df_off range
+ *                            is malformed -- negative, decreasing, past n_rows or >= 2^31 rows),
+ *                            unique sinks
  * Workspace: rq_replay_workspace_size; the small one serves dataframes with <= 3071
  * unique sinks (the per-sink state lives in LDS), RQ_REPLAY_LARGE any width.
  * Per dataframe: < 2^31 rows. */
@@ -293,8 +295,11 @@ int rq_u_int(const double* table, const double* index, int64_t n_t, int32_t n_co
  * counts[i][2] = events of replica i), ev_cap their row stride.
  * rq_log_rows writes row_off[n_rep + 1] (device): replica i owns rows
  * [row_off[i], row_off[i+1]).  rq_log_expand then fills the five reference columns
- * (device, row_off[n_rep] rows each): event_id (100 + event index), time_delta
- * (t_k - t_{k-1}, t_{-1} = start_time), src_id, t, sink_id. */
+ * (device, row_off[n_rep] rows each): event_id (100 + event index), time_delta, src_id,
+ * t, sink_id.  time_delta follows the reference's accumulated State.time
+ * (opt_model.py:68, :304): time_delta_k = t_k - time_{k-1}, time_k = time_{k-1} +
+ * time_delta_k, time_{-1} = start_time -- which differs from t_k - t_{k-1} in the last
+ * bit wherever the running sum has rounded. */
 int rq_log_rows(rq_graph_t g, const int32_t* ev_src, const int64_t* counts, int64_t n_rep,
                 int64_t ev_cap, int64_t* row_off, void* hip_stream);
 int rq_log_expand(rq_graph_t g, const double* ev_t, const int32_t* ev_src, const int64_t* counts,

@@ -128,15 +128,22 @@ def run_significance(sim_opts, significance, time_period, seeds=range(10), rando
     seeds = np.asarray(list(seeds), dtype=np.int64)
     spw = OptPWSignificance(sim_opts.src_id, 0, significance, time_period)._s_pw_for(g.n_followers)
     qv = np.asarray(qs, dtype=np.float64)
-    # a source that can post but reaches no follower with positive significance makes
-    # every reference run raise (take_one_sample's int(nan)): raise it here too
-    from .opt_model import _sig_reach_check
-    live = [kw["src_id"] for name, kw in sim_opts.other_sources
-            if name != "RealData" or any(0.0 <= t <= sim_opts.end_time for t in kw.get("times", []))]
+    # the reference raises (take_one_sample's int(nan)) in a run in which a source that
+    # reaches no follower with positive significance actually posts: when such sources
+    # exist, the batch keeps its event logs and every replica's log is checked
+    from .opt_model import _sig_bad_sources, _sig_reach_check
+    bad = set()
     for q in qv:
-        _sig_reach_check(g, sim_opts.edge_list, spw, float(q), np.asarray(live, dtype=np.int64))
+        bad |= _sig_bad_sources(g, sim_opts.edge_list, spw, float(q))
     R = len(seeds)
     seed_t = torch.as_tensor(np.tile(seeds, len(qv)))
     res = g.run("sig", q=qv, s_pw=spw, period=float(time_period), n_rep=R, ctrl_seed=seed_t,
-                world_seed=seed_t, randomize=randomize, Ks=Ks, max_events=max_events)
+                world_seed=seed_t, randomize=randomize, Ks=Ks, max_events=max_events,
+                event_log=bool(bad))
+    if bad:
+        n = res.counts[:, 2].cpu().numpy()
+        src = res.ev_src.cpu().numpy()
+        ids = g.stream_src_ids
+        for i in range(src.shape[0]):
+            _sig_reach_check(g, sim_opts.edge_list, spw, 1.0, ids[src[i, :n[i]]], bad=bad)
     return _frame(res, np.tile(seeds, len(qv)), np.repeat(qv, R), "OptPW", Ks)

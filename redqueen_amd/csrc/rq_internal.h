@@ -3,6 +3,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <map>
+#include <mutex>
+#include <tuple>
+
 #include "../../include/rq.h"
 
 struct GenArgs {
@@ -116,6 +120,25 @@ hipError_t rq_launch_sweep_fw(const SweepArgs& a, int nK, int col16, int W, int 
 int rq_fw_blocks_per_cu(int nK, int col16, int W, int bits, int wpb, size_t lds, int pw);
 int rq_cu_count();   // CUs of the current device (256 on MI355X when the query fails)
 
+// Blocks per CU a kernel reaches at `threads` threads and `lds` bytes of dynamic LDS
+// (the runtime's occupancy: VGPR, SGPR and LDS limits), cached per (kernel, threads,
+// lds).  rq_run_batch may be called from several threads at once (rq.h), so the cache
+// is mutex-guarded; 0 when the query fails (no device).
+template <class K>
+int rq_occupancy(K kernel, int threads, size_t lds)
+{
+    static std::mutex mu;
+    static std::map<std::tuple<const void*, int, size_t>, int> cache;
+    const auto key = std::make_tuple(reinterpret_cast<const void*>(kernel), threads, lds);
+    std::lock_guard<std::mutex> lock(mu);
+    const auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, threads, lds) != hipSuccess) nb = 0;
+    cache.emplace(key, nb);
+    return nb;
+}
+
 // ---- dataframe replay (rq_replay.hip) ----
 // per-dataframe status, in the workspace
 struct RpInfo {
@@ -130,6 +153,7 @@ struct RpInfo {
 #define RP_EIDBAD 8      // event_id decreases: the event counts are unknown
 #define RP_BIG 16        // needs the large workspace (or exceeds it)
 #define RP_EMPTYDF 32    // no rows
+#define RP_BADOFF 64     // df_off[d] .. df_off[d + 1] is not a valid row range (< 2^31 rows)
 enum { RP_PHASE_FAST = 0, RP_PHASE_GLOBAL = 1, RP_PHASE_KEYS = 2, RP_PHASE_SEQ = 3, RP_PHASE_SCAN = 4 };
 
 struct RpArgs {

@@ -901,13 +901,14 @@ __global__ __launch_bounds__(256, WPE) void rq_scan(ScanArgs a)
 // ============================================================================
 int rq_cu_count()
 {
-    static int n = 0;
-    if (n <= 0) {
-        int dev = 0;
+    // thread-safe one-time query (function-local static initialisation)
+    static const int n = [] {
+        int dev = 0, c = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-            n = 256;
-    }
+            hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
+            c = 256;
+        return c;
+    }();
     return n;
 }
 template <int SPL, int NK, class COL, int W, bool LOG, bool BITS = false, bool BL = false>
@@ -918,13 +919,7 @@ static hipError_t launch_sweep_t(const SweepArgs& a, hipStream_t s)
     unsigned blocks = (unsigned)((a.n_chunk + a.wpb - 1) / a.wpb);
     if (a.wq) {
         // persistent grid: every resident wave slot once, the rest from the queue
-        static int nb_c = 0, wpb_c = 0;
-        static size_t lds_c = 0;
-        if (wpb_c != a.wpb || lds_c != a.lds_total) {
-            nb_c = occ_t<SPL, NK, COL, W, LOG, BITS, BL>(a.wpb, a.lds_total);
-            wpb_c = a.wpb;
-            lds_c = a.lds_total;
-        }
+        const int nb_c = occ_t<SPL, NK, COL, W, LOG, BITS, BL>(a.wpb, a.lds_total);
         const unsigned cap = (unsigned)(nb_c > 0 ? nb_c : 1) * (unsigned)rq_cu_count();
         if (cap < blocks) blocks = cap;
     }
@@ -990,11 +985,7 @@ hipError_t rq_launch_sweep(const SweepArgs& a, int spl, int nK, int col16, int l
 template <int SPL, int NK, class COL, int W, bool LOG, bool BITS, bool BL>
 static int occ_t(int wpb, size_t lds)
 {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rq_sweep<SPL, NK, COL, W, LOG, BITS, BL>, 64 * wpb,
-                                                      lds) != hipSuccess)
-        return 0;
-    return nb;
+    return rq_occupancy(rq_sweep<SPL, NK, COL, W, LOG, BITS, BL>, 64 * wpb, lds);
 }
 template <int SPL, class COL, int W, bool LOG>
 static int occ_k(int nK, int wpb, size_t lds)
@@ -1035,9 +1026,7 @@ static unsigned scan_blocks(const ScanArgs& a, size_t lds)
 {
     unsigned blocks = (unsigned)((a.n_chunk + 3) / 4);
     if (a.wq) {   // persistent grid: every resident block once
-        static int nb = -1;
-        if (nb < 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rq_scan<NK, WPE>, 256, lds) != hipSuccess)
-            nb = 0;
+        const int nb = rq_occupancy(rq_scan<NK, WPE>, 256, lds);
         const unsigned cap = (unsigned)(nb > 0 ? nb : 1) * (unsigned)rq_cu_count();
         if (cap < blocks) blocks = cap;
     }

@@ -206,6 +206,18 @@ __global__ __launch_bounds__(RP_B) void rq_rp_fast(RpArgs a)
     if (GLOBAL && !(inf->flags & RP_GLOBAL)) return;   // only the dataframes the LDS pass gave up
     const int64_t r0 = df_begin(a, d), r1 = df_end(a, d);
     const int64_t nd = r1 - r0;
+    // a malformed caller range (decreasing / negative offsets, past n_rows, >= 2^31 rows:
+    // the row positions below are int) touches no workspace; rq_rp_scan reports RQ_EINVAL
+    if (r0 < 0 || r1 < r0 || r1 > a.n_rows || nd >= ((int64_t)1 << 31)) {
+        if (!GLOBAL && tid == 0) {
+            inf->flags = RP_BADOFF;
+            inf->n_piv = 0;
+            inf->n_own = 0;
+            inf->n_world = 0;
+            inf->S = 0;
+        }
+        return;
+    }
 
     extern __shared__ __align__(16) unsigned char rp_smem[];
     unsigned char* sp = rp_smem;
@@ -842,11 +854,12 @@ __global__ __launch_bounds__(256) void rq_rp_scan(RpArgs a)
     double* out = a.metrics + d * NV;
     int64_t* cnt = a.counts + d * 4;
     const bool eid_ok = a.eid && !(inf.flags & RP_EIDBAD);
-    const int bad = inf.flags & (RP_UNSORTED | RP_GLOBAL | RP_BIG | RP_EMPTYDF);
+    const int bad = inf.flags & (RP_UNSORTED | RP_GLOBAL | RP_BIG | RP_EMPTYDF | RP_BADOFF);
     if (lane == 0) {
         cnt[0] = eid_ok ? inf.n_own : -1;
         cnt[1] = eid_ok ? inf.n_world : -1;
-        cnt[2] = (inf.flags & RP_UNSORTED) ? RQ_EUNSORTED
+        cnt[2] = (inf.flags & RP_BADOFF) ? RQ_EINVAL
+                 : (inf.flags & RP_UNSORTED) ? RQ_EUNSORTED
                  : (inf.flags & (RP_GLOBAL | RP_BIG)) ? RQ_EOVERFLOW
                  : (inf.flags & RP_EMPTYDF) ? 0 : inf.n_piv;
         cnt[3] = inf.S;

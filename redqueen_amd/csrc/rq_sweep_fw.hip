@@ -489,14 +489,7 @@ static hipError_t launch_fw_t(const SweepArgs& a, hipStream_t s)
     unsigned blocks = (unsigned)((a.n_chunk + a.wpb - 1) / a.wpb);
     if (a.wq) {
         // persistent grid: every resident wave slot once, the rest from the queue
-        static int nb_c = 0, wpb_c = 0;
-        static size_t lds_c = 0;
-        if (wpb_c != a.wpb || lds_c != a.lds_total) {
-            nb_c = occ_fw_t<NK, COL, W, BITS, PW>(a.wpb, a.lds_total);
-            wpb_c = a.wpb;
-            lds_c = a.lds_total;
-        }
-        const int nb = nb_c;
+        const int nb = occ_fw_t<NK, COL, W, BITS, PW>(a.wpb, a.lds_total);
         const unsigned cap = (unsigned)(nb > 0 ? nb : 1) * (unsigned)rq_cu_count();
         if (cap < blocks) blocks = cap;
     }
@@ -529,11 +522,7 @@ hipError_t rq_launch_sweep_fw(const SweepArgs& a, int nK, int col16, int W, int 
 template <int NK, class COL, int W, bool BITS, bool PW>
 static int occ_fw_t(int wpb, size_t lds)
 {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rq_sweep_fw<NK, COL, W, (W > 16 ? 8 : W / 2), BITS, PW>, 64 * wpb,
-                                                      lds) != hipSuccess)
-        return 0;
-    return nb;
+    return rq_occupancy(rq_sweep_fw<NK, COL, W, (W > 16 ? 8 : W / 2), BITS, PW>, 64 * wpb, lds);
 }
 template <class COL, int W, bool PW = false>
 static int occ_fw_k(int nK, int wpb, size_t lds)

@@ -163,7 +163,8 @@ class Broadcaster:
 def plugin_times(obj, start_time, sink_ids, edge_list, end_time):
     """Times of a registered static broadcaster instance, as run_dynamic collects
     them (init_state + initialize + get_all_times, opt_model.py:256-264), sorted and
-    clipped to [start_time, end_time] (events past end_time never play)."""
+    clipped at end_time (events past end_time never play); a time before start_time
+    raises ValueError (the reference would play it with a negative time_delta)."""
     if getattr(obj, "is_dynamic", True):
         raise NotImplementedError(
             "broadcaster %s is dynamic (get_next_interval per event): only static plugin "
@@ -172,7 +173,14 @@ def plugin_times(obj, start_time, sink_ids, edge_list, end_time):
     obj.init_state(start_time, list(sink_ids), followers, end_time)
     obj.initialize()
     t = np.sort(np.asarray(obj.get_all_times(), dtype=np.float64).ravel())
-    return t[(t >= start_time) & (t <= end_time)]
+    if t.size and t[0] < start_time:
+        # run_dynamic would play it first with a negative time_delta (the built-in
+        # RealData drops such times itself, opt_model.py:727); the engine's streams
+        # start at start_time, so refuse instead of dropping it silently
+        raise ValueError("broadcaster %s (src_id %r) returned a time %r before start_time %r: "
+                         "not supported by the GPU engine" %
+                         (type(obj).__name__, obj.src_id, float(t[0]), start_time))
+    return t[t <= end_time]
 
 
 class Poisson(Broadcaster):
@@ -281,19 +289,25 @@ class OptPWSignificance(Broadcaster):
         return s_pw
 
 
-def _sig_reach_check(g, edge_list, s_pw, q, ev_src):
-    """OptPWSignificance raises where the reference does: an event whose source reaches
-    no follower with positive significance gives take_one_sample an all-zero
-    piecewise intensity, s_max = 0 and int(nan) (opt_model.py:557-566, :610-614).
-    The engine draws nothing for such an event; the facade raises the reference's
-    error if one was played."""
+def _sig_bad_sources(g, edge_list, s_pw, q):
+    """Stream src_ids whose events reach no follower with positive significance: for
+    them take_one_sample sees an all-zero piecewise intensity, s_max = 0 and int(nan)
+    (opt_model.py:557-566, :610-614).  The engine draws nothing for such an event."""
     fol = {int(f): i for i, f in enumerate(g.followers)}
     pw = {}
     for a, b in edge_list:   # rank_diff counts edge multiplicity
         if int(a) != g.src_id and int(b) in fol:
             pw[int(a)] = pw.get(int(a), 0.0) + np.sqrt(np.asarray(s_pw[fol[int(b)]]) / q)
-    bad = {int(j) for j in g.stream_src_ids
-           if int(j) != g.src_id and not (int(j) in pw and np.max(pw[int(j)]) > 0.0)}
+    return {int(j) for j in g.stream_src_ids
+            if int(j) != g.src_id and not (int(j) in pw and np.max(pw[int(j)]) > 0.0)}
+
+
+def _sig_reach_check(g, edge_list, s_pw, q, ev_src, bad=None):
+    """OptPWSignificance raises where the reference does: in a run in which an event
+    of a source from _sig_bad_sources is actually played (ev_src = the run's event
+    sources)."""
+    if bad is None:
+        bad = _sig_bad_sources(g, edge_list, s_pw, q)
     hit = [int(j) for j in np.unique(ev_src) if int(j) in bad]
     if hit:
         raise ValueError("cannot convert float NaN to integer (OptPWSignificance.take_one_sample: "

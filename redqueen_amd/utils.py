@@ -129,6 +129,17 @@ def replay_frames(dfs, src_id, end_time, Ks=(1,)):
     world_events per input df."""
     import pandas as pd
     import torch
+    cols = ["top_" + str(k) for k in Ks] + ["avg_rank", "r_2", "num_events", "world_events",
+                                            "pivot_rows", "sinks"]
+    dfs = list(dfs)
+    if not dfs:
+        return pd.DataFrame({c: [] for c in cols})
+    has_eid = ["event_id" in d.columns for d in dfs]
+    if any(has_eid) and not all(has_eid):
+        # world_events needs every dataframe's event ids (num_tweets_of / add_perf count
+        # distinct event_id values): refuse rather than drop them for all dataframes
+        raise ValueError("replay_frames: %d of %d dataframes lack an 'event_id' column" %
+                         (has_eid.count(False), len(dfs)))
     dev = torch.device("cuda", torch.cuda.current_device())
     lens = np.asarray([len(d) for d in dfs], dtype=np.int64)
     off = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)])).to(dev)
@@ -136,7 +147,7 @@ def replay_frames(dfs, src_id, end_time, Ks=(1,)):
     def cat(name, dt):
         return torch.from_numpy(np.ascontiguousarray(
             np.concatenate([d[name].values for d in dfs]) if len(dfs) else np.zeros(0), dtype=dt)).to(dev)
-    eid = cat("event_id", np.int64) if all("event_id" in d.columns for d in dfs) else None
+    eid = cat("event_id", np.int64) if all(has_eid) else None
     o, c = replay_columns(cat("t", np.float64), cat("src_id", np.int64), cat("sink_id", np.int64),
                           eid, off, src_id, end_time, Ks)
     o, c = o.cpu().numpy(), c.cpu().numpy()

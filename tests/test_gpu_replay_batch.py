@@ -215,3 +215,26 @@ def test_c3_exported_frames_replay_to_engine_metrics():
     assert torch.equal(m, res.metrics)
     assert torch.equal(c[:, 0], res.counts[:, 0]) and torch.equal(c[:, 1], res.counts[:, 1])
     assert torch.equal(c[:, 2], res.counts[:, 3])   # pivot rows = the sweep's row count
+
+
+def test_malformed_df_offsets_rejected(golden):
+    """A df_off range that is negative, decreasing or past n_rows touches no workspace
+    and reports RQ_EINVAL in counts[d][2]; the well-formed dataframes of the same call
+    keep the reference's values."""
+    torch, O, L, U = _ctx()
+    d = golden("readme_runs.npz")
+    so = graphs.readme()
+    df = _readme_df(O, d, "101", so)
+    n = len(df)
+    exp = d["met_101"]
+    cat = lambda c, k: np.concatenate([df[c].values] * k)  # noqa: E731
+    t = _dev(torch, cat("t", 2), np.float64)
+    src = _dev(torch, cat("src_id", 2), np.int64)
+    sink = _dev(torch, cat("sink_id", 2), np.int64)
+    eid = _dev(torch, cat("event_id", 2), np.int64)
+    for bad in ([0, n, n - 5, 2 * n], [0, n, 2 * n + 7, 2 * n], [0, n, -3, 2 * n]):
+        off = _dev(torch, bad, np.int64)
+        o, c = U.replay_columns(t, src, sink, eid, off, so["src_id"], so["end_time"], KS)
+        o, c = o.cpu().numpy(), c.cpu().numpy()
+        assert np.array_equal(o[0], exp) and c[0, 2] > 0, bad
+        assert c[1, 2] == L.RQ_EINVAL and np.isnan(o[1]).all(), (bad, c[1])

@@ -139,3 +139,22 @@ def test_unreached_event_raises_like_reference(golden):
                 m.run_dynamic()
             with pytest.raises(ValueError):
                 batch.run_significance(so, sig_b, 10.0, seeds=range(4))
+
+
+def test_silent_unreached_source_does_not_raise():
+    """A source that reaches no follower with positive significance but never posts
+    (rate 0 here) raises nothing in the reference -- take_one_sample only runs for an
+    event that is played -- so the batch raises nothing either; the same world with
+    that source posting raises (test_unreached_event_raises_like_reference)."""
+    torch, engine, graphs, O = _ctx()
+    from redqueen_amd import batch
+    from redqueen_amd.opt_model import SimOpts
+    w, sig = _err_worlds()["zerosig"]
+    w = dict(w, other_sources=[("Poisson2", {"src_id": 1000, "seed": 42, "rate": 10.0}),
+                               ("Poisson2", {"src_id": 1001, "seed": 43, "rate": 0.0})])
+    so = SimOpts(**w)
+    out = batch.run_significance(so, sig, 10.0, seeds=range(4))
+    assert len(out) == 4 and (out.status == 0).all()
+    m = so.create_manager_with_significance(3, time_period=10.0, significance=sig)
+    m.run_dynamic()
+    assert m.state.get_num_events() > 0
