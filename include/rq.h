@@ -63,7 +63,7 @@
 extern "C" {
 #endif
 
-#define RQ_ABI_VERSION 3
+#define RQ_ABI_VERSION 4
 #define RQ_MAX_K 4 /* at most 4 K values (perf_opts.Ks, opt_runs.py:31-38) per run */
 
 typedef enum {
@@ -181,11 +181,20 @@ typedef struct rq_batch_desc {
     const int64_t* rd_cap;       /* host [n_rd]: the most times any replica gives source k       */
     const double* rd_times;      /* device                                                       */
     const int64_t* rd_off;       /* device [n_grid * n_rep * n_rd + 1]                           */
+    /* Per-grid-point replica window (ABI v4): this call's replica space is the
+       n_grid x rep_cnt grid of global ids i = g * n_rep + rep_lo + rr, rr < rep_cnt,
+       flattened as g * rep_cnt + rr; replica0 / n_local then select a contiguous part
+       of THAT space and outputs are indexed by it.  A multi-GPU shard that takes the
+       same replica window of every grid point sees every grid point (every q), so
+       shards cost the same however the work per replica varies with q.
+       rep_cnt = 0: the whole grid (rep_lo = 0, rep_cnt = n_rep). */
+    int64_t rep_lo;
+    int64_t rep_cnt;
 } rq_batch_desc;
 #define RQ_MAX_RD 64
 
 typedef struct rq_outputs {
-    double* metrics;   /* device [R][nK + 2]: top_K..., avg_rank, r_2  (R = n_local or n_grid*n_rep) */
+    double* metrics;   /* device [R][nK + 2]: top_K..., avg_rank, r_2  (R = n_local or n_grid*rep_cnt) */
     int64_t* counts;   /* device [R][4]: num_events (own posts that reached a sink = the   */
                        /* reference 'capacity'), world_events, n_events (all), pivot rows   */
     int32_t* status;   /* device [R]: RQ_ST_* bits                                            */
@@ -212,7 +221,8 @@ int rq_workspace_size(rq_graph_t g, const rq_batch_desc* b, size_t* bytes);
 int rq_event_capacity(rq_graph_t g, const rq_batch_desc* b, int64_t* cap);
 /* how rq_run_batch will run this batch (diagnostics / occupancy reporting):
  * info[0] sweep variant (0 fast tiled, 1 sequential exact, 2 fast tiled on K=1 sink
- * bitsets, 3 fast tiled on K=1 per-wave LDS sink bits; +10 fused), [1] sources per lane,
+ * bitsets, 3 fast tiled on K=1 per-wave LDS sink bits, 4 sequential exact with the
+ * per-sink state in global memory; +10 fused), [1] sources per lane,
  * [2] arrival-ring depth W, [3] waves per block, [4] blocks per CU (runtime occupancy,
  * 0 without a device), [5] sink columns in LDS (1) or global (0), [6] dynamic LDS
  * bytes per block, [7] replicas per chunk */

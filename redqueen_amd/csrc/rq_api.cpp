@@ -109,6 +109,13 @@ struct rq_graph {
     std::vector<int> csr_col_el;     // sink columns in edge-list order for every stream
     DevBuf<int> d_csr_col_el;
     std::vector<int> col_to_fol;     // sink column -> follower position or -1
+    // duplicate (source, sink) edges (a multigraph, opt_model.py:169-175 accepts them): the
+    // sweep's CSR row of a source holds its distinct sinks first (layer 0), then the 2nd
+    // occurrences (layer 1), ...; every layer has distinct sinks.  lay_end[lay_ptr[j] ..
+    // lay_ptr[j+1]) are the CSR ends of stream j's layers.  multi: some row has > 1 layer.
+    bool multi = false, ctrl_dup = false;
+    std::vector<int> lay_ptr, lay_end;
+    DevBuf<int> d_lay_ptr, d_lay_end;
     // per-stream sink bitsets (32 sinks per word) for the K=1 bitset sweep, n_sinks <= 2048
     int nw = 0;
     std::vector<uint32_t> masks;
@@ -128,6 +135,7 @@ namespace {
 struct Plan {
     int nK = 1, spl = 1, wpb = 4, n_sinks_pad = 0;
     int64_t R = 0, chunk = 0, capsum = 0, cap_rows = 0;
+    int64_t rep_lo = 0, rep_cnt = 0;   // per-grid-point replica window (rq_batch_desc.rep_lo/rep_cnt)
     std::vector<int> cap;
     std::vector<int64_t> st_off;
     std::vector<int> rd_k;   // stream -> per-replica RealData source k (rq_batch_desc.rd_*) or -1
@@ -137,6 +145,8 @@ struct Plan {
     bool bl = false;
     size_t g_fb = 0, g_etab = 0, g_inv = 0;
     bool g_inv_sh = false;   // general sweep: 1/c_j in the block's shared LDS (one grid point)
+    bool gs = false;         // LOG sweep: per-sink state in global memory, gs_slots wave slots
+    int64_t gs_slots = 0, gs_stride = 0;
     // fused windowed sweep (n_str <= 64): arrivals generated in-kernel, window depth fw_h
     bool fw = false;
     int fw_h = 8, mstride = 1;
@@ -147,7 +157,7 @@ struct Plan {
     size_t tables_bytes = 0;
     size_t off_pwc = 0, off_pwmax = 0;
     size_t off_invc = 0, off_streams = 0, off_slen = 0, off_rt = 0, off_rs = 0, off_rv = 0,
-           off_rc = 0, off_sall = 0, off_wq = 0, off_stoff = 0, off_cap = 0, off_rdk = 0,
+           off_rc = 0, off_sall = 0, off_wq = 0, off_stoff = 0, off_cap = 0, off_rdk = 0, off_gs = 0,
            total = 0;
 };
 
@@ -216,7 +226,12 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     if ((ck == RQ_SRC_PWCONST) && g->ctrl_arr_n < 1) return RQ_EINVAL;
     const double scale = b->cap_scale >= 1.0 ? b->cap_scale : 1.0;
     p->nK = b->nK;
-    const int64_t Rall = (int64_t)b->n_grid * b->n_rep;
+    // the call's replica space: the [rep_lo, rep_lo + rep_cnt) window of every grid point
+    if (b->rep_cnt < 0 || (b->rep_cnt > 0 && (b->rep_lo < 0 || b->rep_lo + b->rep_cnt > b->n_rep)))
+        return RQ_EINVAL;
+    p->rep_lo = b->rep_cnt > 0 ? b->rep_lo : 0;
+    p->rep_cnt = b->rep_cnt > 0 ? b->rep_cnt : b->n_rep;
+    const int64_t Rall = (int64_t)b->n_grid * p->rep_cnt;
     if (b->replica0 < 0 || b->n_local < 0 || b->replica0 + b->n_local > Rall) return RQ_EINVAL;
     p->R = b->n_local > 0 ? b->n_local : Rall - b->replica0;
     if (p->R < 1) return RQ_EINVAL;
@@ -262,12 +277,15 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     if (b->max_events >= 0) rows = std::min(rows, (double)b->max_events + 1.0);
     // a multiple of 32 rows: replica row bases stay aligned to the scan's 32-row trips
     p->cap_rows = (std::max<int64_t>(64, (int64_t)rows) + 31) & ~(int64_t)31;
+    // Opt / OptPWSignificance with a duplicated controlled edge: the reference's follower
+    // vectors (sqrt_s_by_q, old_ranks: one entry per edge) no longer match the ranks (one
+    // per distinct follower) and its first non-own event raises ValueError
+    if (g->ctrl_dup && (ck == RQ_SRC_OPT || ck == RQ_SRC_OPTPW)) return RQ_EINVAL;
+    if (g->n_str > RQ_MAX_STREAMS) return RQ_EUNSUPPORTED;
     p->spl = g->n_str <= 64 ? 1 : g->n_str <= 128 ? 2 : g->n_str <= 256 ? 4 : 8;
-    if (g->n_str > 512) return RQ_EUNSUPPORTED;
     p->n_sinks_pad = (g->n_sinks + 1) | 1;   // odd stride: spreads replicas over LDS banks
     const size_t per_wave = (size_t)p->n_sinks_pad * 4;
     p->wpb = per_wave * 4 <= 64 * 1024 ? 4 : per_wave * 2 <= 80 * 1024 ? 2 : 1;
-    if (per_wave > 150 * 1024) return RQ_EUNSUPPORTED;
 
     // the sequential exact variant also whenever equal event times are likely:
     // RealData streams (recorded times repeat); the fast sweep flags RQ_ST_TIE
@@ -277,14 +295,26 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     p->log = b->max_events >= 0 ||
              b->sweep_mode == 2 || (has_rd && b->sweep_mode != 1 && b->sweep_mode != 5);
     for (int q = 0; q < b->nK; ++q) p->log = p->log || b->Ks[q] > 32767;   // int16 ranks
-    if (p->log) p->spl = g->n_str <= 64 ? 1 : 8;
+    // a multigraph (duplicate edges make fractional pivot cells, the exact sequential
+    // sweep's business) and > 512 sources (the fast instances own <= 8 per lane)
+    p->log = p->log || g->multi || g->n_str > 512;
+    const int nwl = (g->n_sinks + 31) / 32;
 
+  replan:
+    if (p->log) p->spl = g->n_str <= 64 ? 1 : g->n_str <= 512 ? 8 : g->n_str <= 1024 ? 16 : 32;
     p->mstride = g->nw | 1;   // odd row stride: one LDS bank per stream for a given word
     p->bits = !p->log && p->nK == 1 && b->Ks[0] == 1 && g->nw > 0 && b->sweep_mode != 3 &&
               (size_t)g->n_str * p->mstride * 4 <= 64 * 1024;
     if (p->bits) p->spl = g->n_str <= 64 ? 1 : g->n_str <= 128 ? 2 : g->n_str <= 256 ? 4 : 8;
     p->bl = !p->log && !p->bits && p->nK == 1 && b->Ks[0] == 1 && p->spl >= 2 && b->sweep_mode != 3;
-    const int nwl = (g->n_sinks + 31) / 32;
+    // K = 1 with too many sinks for int16 ranks in LDS (> 24k): per-wave sink BITS, which
+    // exist for 2+ sources per lane (lanes past the sources idle)
+    if (!p->log && !p->bits && !p->bl && p->nK == 1 && b->Ks[0] == 1 && b->sweep_mode != 3 &&
+        2 * (size_t)p->n_sinks_pad > 48 * 1024) {
+        p->spl = std::max(p->spl, 2);
+        p->bl = true;
+    }
+    p->gs = false;
 
     // general sweep: pick (ring depth W, waves per block) for the most waves per CU
     {
@@ -292,7 +322,9 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
         // sink columns live in LDS as uint16 when they fit, else they are read from
         // global memory as int (the kernel's COL type selects the path at compile time)
         // both placements are scored: LDS columns only win at equal waves per CU
-        for (int col_lds = g->n_sinks <= 65535 ? 1 : 0; col_lds >= 0; --col_lds) {
+        // LOG: the per-sink state in LDS, or (gs) in global memory for more sinks than fit
+        for (int gs = 0; gs <= (p->log ? 1 : 0); ++gs)
+        for (int col_lds = g->n_sinks <= 65535 && !(p->log && p->spl >= 16) ? 1 : 0; col_lds >= 0; --col_lds) {
             const int c16 = col_lds;
             // BITS: sink bitsets [n_str][nw] replace the columns (and the per-wave ranks)
             const size_t colb = p->bits ? 4 * (size_t)g->n_str * p->mstride
@@ -309,21 +341,23 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
             const int spl = p->spl;
             int only_w = 0;
             if (const char* e = getenv("RQ_G_W")) only_w = atoi(e);   // tuning only
-            // LOG: LDS rings of W = 8 per source; the fast sweep: a register window of 4
+            // LOG: LDS rings of W = 8 per source (4 at 32 sources per lane); the fast sweep:
+            // a register window of 4
             for (int W : {8, 4}) {
-                if (p->log != (W == 8)) continue;
+                if ((p->log ? (spl >= 32 ? 4 : 8) : 4) != W) continue;
                 if (only_w && W != only_w) continue;
                 const size_t r_off = inv_sh ? 0 : align_up(8 * (size_t)g->n_str, 16);
-                const size_t rank_b = p->log ? 4 : (p->bits ? 0 : 2);   // fast: int16 saturating
+                const size_t rank_b = p->log ? (gs ? 0 : 4) : (p->bits ? 0 : 2);   // fast: int16 saturating
                 // BL: two bits per sink (T, V words) in place of the int16 ranks
                 const size_t w_off = p->bl ? align_up(r_off + 8 * (size_t)nwl, 16)
                                            : align_up(r_off + rank_b * (size_t)p->n_sinks_pad, 16);
                 // LOG: rings of W arrivals for each real source; fast: the tile's staging
                 size_t stride = p->log ? align_up(w_off + 8 * (size_t)g->n_str * W, 16)
                                        : align_up(w_off + 64 * 12, 16);
-                // LOG: per-sink gtag/gcnt/gsum + a wave_npsum<1> scratch (304 doubles)
+                // LOG: per-sink gtag/gcnt/gsum (gs: in global memory) + a wave_npsum<1>
+                // scratch (304 doubles)
                 const size_t x_off = stride;
-                if (p->log) stride = align_up(x_off + 12 * (size_t)p->n_sinks_pad + 8 * 304, 16);
+                if (p->log) stride = align_up(x_off + (gs ? 0 : 12 * (size_t)p->n_sinks_pad) + 8 * 304, 16);
                 for (int wpb : {16, 12, 10, 8, 6, 5, 4, 3, 2, 1}) {
                     if (p->log && wpb > 4) continue;   // LOG instances: 256-thread blocks
                     if (!p->log && spl >= 4 && wpb > 8) continue;   // 512-thread instances
@@ -331,13 +365,17 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
                     if (tot > kLdsMax) continue;
                     // resident waves per CU: the runtime's occupancy for this instance
                     // (VGPR/SGPR/LDS); without a device, the LDS bound capped at 16
-                    int blocks = rq_sweep_blocks_per_cu(spl, p->nK, c16, W, p->log, p->bl ? 2 : p->bits, wpb, tot);
+                    int blocks = rq_sweep_blocks_per_cu(spl, p->nK, c16, W, p->log ? 1 + gs : 0,
+                                                        p->bl ? 2 : p->bits, wpb, tot);
                     if (blocks <= 0) blocks = (int)std::min<size_t>(kLdsMax / tot, 16 / wpb);
                     const int waves = blocks * wpb;
-                    // LDS columns skip the global latency
-                    const int score = waves * 8 + col_lds * 2;
+                    // LDS columns skip the global latency; LDS sink state wherever it fits
+                    const int score = waves * 8 + col_lds * 2 + (gs ? 0 : 100000);
                     if (score > best) {
                         best = score;
+                        p->gs = gs;
+                        p->gs_slots = std::min<int64_t>((int64_t)align_up((size_t)p->chunk, (size_t)wpb),
+                                                        (int64_t)blocks * wpb * rq_cu_count());
                         p->gwin = W; p->gwpb = wpb; p->gcol_lds = col_lds; p->gcol16 = c16;
                         p->g_col = o_col; p->g_ptr = o_ptr; p->g_odf = o_odf; p->g_cbf = o_cbf;
                         p->g_wave = sh; p->g_wave_stride = stride; p->g_rank_off = r_off;
@@ -347,13 +385,17 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
                 }
             }
         }
-        if (best < 0) return RQ_EUNSUPPORTED;
+        if (best < 0) {
+            if (p->log) return RQ_EUNSUPPORTED;
+            p->log = true;   // no fast instance fits this graph: the exact sequential sweep
+            goto replan;
+        }
     }
 
     // fused windowed sweep: one stream per lane, rings of W arrivals generated in LDS,
     // a window of H per ring in registers; (W, H, waves per block) for the most waves per CU
     const bool pw = b->ctrl_kind == RQ_SRC_OPTPW;
-    p->fw = !p->log && g->n_str <= 64 && b->sweep_mode != 4 && b->sweep_mode != 5;
+    p->fw = !p->log && !p->bl && g->n_str <= 64 && b->sweep_mode != 4 && b->sweep_mode != 5;
     if (p->fw) {
         int best = -1;
         const int c16 = p->bits ? 1 : (g->n_sinks <= 65535 ? 1 : 0);
@@ -423,6 +465,9 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     p->off_rc = o;      o = align_up(o + sizeof(uint32_t) * (size_t)C * p->cap_rows * p->nK, A);
     p->off_sall = o;    o = align_up(o + sizeof(int) * (size_t)C, A);
     p->off_wq = o;      o = align_up(o + 2 * sizeof(int), A);   // [0] sweep, [1] scan queue
+    // LOG + gs: per resident wave, rank int + gtag/gcnt/gsum int per sink
+    p->gs_stride = p->gs ? (int64_t)align_up(16 * (size_t)p->n_sinks_pad, A) : 0;
+    p->off_gs = o;      o = align_up(o + (size_t)(p->gs ? p->gs_slots : 0) * p->gs_stride, A);
     p->total = o;
     return RQ_OK;
 }
@@ -556,16 +601,12 @@ int rq_graph_build(const rq_graph_desc* d, rq_graph_t* out)
         rows[si->second].push_back(ci->second);
     }
     g->n_edges = d->n_edges;
-    for (int j = 0; j < g->n_str; ++j) {
-        std::vector<int> r = rows[j];
-        std::sort(r.begin(), r.end());
-        // duplicate (source, sink) edges make fractional pivot cells: replay handles them,
-        // the simulation engine does not
-        if (std::adjacent_find(r.begin(), r.end()) != r.end()) return RQ_EUNSUPPORTED;
-    }
-    // followers of the controlled source: sorted sink order (Opt.sink_ids, opt_model.py:341)
+    // followers of the controlled source: sorted distinct sink order (Opt.sink_ids,
+    // opt_model.py:341, as the State's follower ranks key them)
     std::vector<int> fcols = rows[g->ctrl_idx];
     std::sort(fcols.begin(), fcols.end());
+    g->ctrl_dup = std::adjacent_find(fcols.begin(), fcols.end()) != fcols.end();
+    fcols.erase(std::unique(fcols.begin(), fcols.end()), fcols.end());
     g->n_fol = (int)fcols.size();
     g->col_to_fol.assign(g->n_sinks, -1);
     for (int f = 0; f < g->n_fol; ++f) {
@@ -574,17 +615,35 @@ int rq_graph_build(const rq_graph_desc* d, rq_graph_t* out)
     }
     g->fol = fcols;
     g->csr_ptr.push_back(0);
+    g->lay_ptr.push_back(0);
+    std::vector<int> seen(g->n_sinks, 0);
     for (int j = 0; j < g->n_str; ++j) {
-        const std::vector<int>& r = j == g->ctrl_idx ? fcols : rows[j];
-        int of = 0;
-        for (int c : r) {
-            g->csr_col.push_back(c);
-            of += g->col_to_fol[c] >= 0;
+        // layer k holds the (k+1)-th occurrence of each sink, in edge-list order; the
+        // controlled row's layer 0 is the sorted follower list the sweep indexes by
+        // follower position
+        std::vector<std::vector<int>> layers;
+        for (int c : rows[j]) {
+            const int k = seen[c]++;
+            if ((int)layers.size() <= k) layers.emplace_back();
+            layers[k].push_back(c);
         }
+        for (int c : rows[j]) seen[c] = 0;
+        if (j == g->ctrl_idx && !layers.empty()) layers[0] = fcols;
+        g->multi = g->multi || layers.size() > 1;
+        int of = 0;
+        for (const std::vector<int>& l : layers) {
+            for (int c : l) {
+                g->csr_col.push_back(c);
+                of += g->col_to_fol[c] >= 0;
+            }
+            g->lay_end.push_back((int)g->csr_col.size());
+        }
+        if (layers.empty()) g->lay_end.push_back((int)g->csr_col.size());
+        g->lay_ptr.push_back((int)g->lay_end.size());
         g->outdeg_f.push_back(of);
         g->csr_ptr.push_back((int)g->csr_col.size());
-        // dataframe export: every stream's sinks in edge-list order (the controlled row
-        // above is the sorted follower list the sweep indexes by follower position)
+        // dataframe export: every stream's sinks in edge-list order (duplicates included:
+        // Event.sink_ids, opt_model.py:306-307)
         for (int c : rows[j]) g->csr_col_el.push_back(c);
     }
 
@@ -613,6 +672,8 @@ int rq_graph_build(const rq_graph_desc* d, rq_graph_t* out)
         (rc = g->d_p2.upload(g->p2)) || (rc = g->d_arr_a.upload(g->arr_a)) ||
         (rc = g->d_arr_b.upload(g->arr_b)) || (rc = g->d_sink_ids.upload(g->sink_ids)) ||
         (rc = g->d_csr_col_el.upload(g->csr_col_el)))
+        return rc;
+    if (g->multi && ((rc = g->d_lay_ptr.upload(g->lay_ptr)) || (rc = g->d_lay_end.upload(g->lay_end))))
         return rc;
     *out = guard.release();
     return RQ_OK;
@@ -665,14 +726,14 @@ int rq_plan_info(rq_graph_t g, const rq_batch_desc* b, int64_t* info)
     Plan p;
     const int rc = make_plan(g, b, &p);
     if (rc) return rc;
-    info[0] = (p.log ? 1 : (p.bits ? 2 : (p.bl ? 3 : 0))) + (p.fw ? 10 : 0);
+    info[0] = (p.log ? (p.gs ? 4 : 1) : (p.bits ? 2 : (p.bl ? 3 : 0))) + (p.fw ? 10 : 0);
     info[1] = p.spl;
     info[2] = p.gwin;
     info[3] = p.gwpb;
     info[4] = p.fw ? rq_fw_blocks_per_cu(p.nK, p.gcol16, p.gwin, p.bits, p.gwpb, p.g_total,
                                           b->ctrl_kind == RQ_SRC_OPTPW)
-                   : rq_sweep_blocks_per_cu(p.spl, p.nK, p.gcol16, p.gwin, p.log, p.bl ? 2 : p.bits, p.gwpb,
-                                            p.g_total);
+                   : rq_sweep_blocks_per_cu(p.spl, p.nK, p.gcol16, p.gwin, p.log ? 1 + p.gs : 0,
+                                            p.bl ? 2 : p.bits, p.gwpb, p.g_total);
     info[5] = p.gcol_lds;
     info[6] = (int64_t)p.g_total;
     info[7] = p.chunk;
@@ -711,8 +772,9 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             for (int j = 0; j < g->n_str; ++j) {
                 if (j == g->ctrl_idx) continue;
                 double c = 0.0;
+                // edge-list order (duplicate edges count once each), as the oracle sums
                 for (int e = g->csr_ptr[j]; e < g->csr_ptr[j + 1]; ++e) {
-                    const int f = g->col_to_fol[g->csr_col[e]];
+                    const int f = g->col_to_fol[g->csr_col_el[e]];
                     if (f >= 0) c = c + w[f];
                 }
                 invc[(size_t)gi * g->n_str + j] = c > 0.0 ? 1.0 / c : 0.0;
@@ -733,7 +795,7 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
                 if (j == g->ctrl_idx) continue;
                 double* row = &pwc[((size_t)gi * g->n_str + j) * S];
                 for (int e = g->csr_ptr[j]; e < g->csr_ptr[j + 1]; ++e) {
-                    const int f = g->col_to_fol[g->csr_col[e]];
+                    const int f = g->col_to_fol[g->csr_col_el[e]];
                     if (f < 0) continue;
                     const double* sp = b->s_pw + ((size_t)gi * g->n_fol + f) * S;
                     for (int k = 0; k < S; ++k) row[k] = row[k] + std::sqrt(sp[k] / b->q[gi]);
@@ -790,6 +852,9 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
         ga.n_chunk = C;
         ga.chunk0 = c0;
         ga.rep0 = b->replica0;
+        ga.n_rep = b->n_rep;
+        ga.rep_lo = p.rep_lo;
+        ga.rep_cnt = p.rep_cnt;
         ga.n_str = g->n_str;
         ga.ctrl_idx = g->ctrl_idx;
         ga.ctrl_stream_kind = ctrl_stream_kind;
@@ -892,6 +957,13 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             sa.lds_rank_off = p.g_rank_off;
             sa.lds_win_off = p.g_win_off;
             sa.lds_x_off = p.g_x_off;
+            sa.lay_ptr = g->multi ? g->d_lay_ptr.p : nullptr;
+            sa.lay_end = g->multi ? g->d_lay_end.p : nullptr;
+            if (p.gs) {
+                sa.gs = ws + p.off_gs;
+                sa.gs_stride = p.gs_stride;
+                sa.gs_slots = (int)p.gs_slots;
+            }
             sa.lds_mask = p.g_col;   // BITS: the bitsets take the columns' place
             sa.masks = g->d_mask.p;
             sa.nw = g->nw;
@@ -939,7 +1011,8 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             }
             TimedLaunch tl(K_SWEEP, s);
             const hipError_t e = p.fw ? rq_launch_sweep_fw(sa, p.nK, p.gcol16, p.gwin, p.bits, s)
-                                      : rq_launch_sweep(sa, p.spl, p.nK, p.gcol16, p.log, p.bl ? 2 : p.bits, s);
+                                      : rq_launch_sweep(sa, p.spl, p.nK, p.gcol16, p.log ? 1 + p.gs : 0,
+                                                        p.bl ? 2 : p.bits, s);
             if (e != hipSuccess) return RQ_EHIP;
         }
 

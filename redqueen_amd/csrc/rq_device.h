@@ -110,6 +110,15 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// the same for per-wave state in GLOBAL memory that lanes of one wave hand to each
+// other (a lane reads what another lane stored): workgroup-scope release / acquire,
+// i.e. the wave's stores complete before any lane's next load
+__device__ __forceinline__ void wave_mem_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
 
 __device__ __forceinline__ int popc(uint64_t m) { return __popcll(m); }
 

@@ -9,8 +9,17 @@
 
 #include "../../include/rq.h"
 
+// global replica id of position s of a call's replica space (rq_batch_desc.rep_lo /
+// rep_cnt): the n_grid x rep_cnt window of every grid point's n_rep replicas
+__host__ __device__ __forceinline__ int64_t rq_global_replica(int64_t s, int64_t n_rep, int64_t rep_lo,
+                                                               int64_t rep_cnt)
+{
+    return rep_cnt == n_rep ? s : (s / rep_cnt) * n_rep + rep_lo + s % rep_cnt;
+}
+
 struct GenArgs {
-    int64_t n_chunk, chunk0, rep0;   // local replica = chunk0 + rl, global = rep0 + local
+    int64_t n_chunk, chunk0, rep0;   // local replica = chunk0 + rl, space position = rep0 + local
+    int64_t n_rep, rep_lo, rep_cnt;  // global id = rq_global_replica(rep0 + local, ...)
     int n_str, ctrl_idx, ctrl_stream_kind, randomize;
     int64_t seed_mod;
     const uint32_t* ctrl_seed;
@@ -38,7 +47,7 @@ struct GenArgs {
     const int64_t* rd_off;
 };
 
-#define RQ_MAX_STREAMS 512
+#define RQ_MAX_STREAMS 2048   // 512 per fast instance (8 per lane); LOG instances 16 / 32 per lane
 
 struct SweepArgs {
     int64_t n_chunk, chunk0, n_rep, rep0;
@@ -95,6 +104,15 @@ struct SweepArgs {
     size_t lds_col, lds_ptr, lds_odf, lds_cbf, lds_wave, lds_wave_stride, lds_rank_off, lds_win_off, lds_x_off, lds_mask,
         lds_total, lds_stage_off;
     GenArgs gen;             // fused sweep: arrival generation parameters
+    // duplicate edges: stream j's CSR row is layers of distinct sinks, ending at
+    // lay_end[lay_ptr[j] .. lay_ptr[j+1]) (null: one layer per row, a simple graph)
+    const int* lay_ptr;
+    const int* lay_end;
+    // LOG sweep with the per-sink state in global memory (more sinks than LDS holds):
+    // gs_slots wave slots of gs_stride bytes (rank int + gtag/gcnt/gsum per sink)
+    char* gs;
+    int64_t gs_stride;
+    int gs_slots;
 };
 
 struct ScanArgs {
@@ -113,6 +131,8 @@ struct ScanArgs {
 };
 
 hipError_t rq_launch_gen(const GenArgs& a, hipStream_t s);
+// log: 0 fast tiled sweep, 1 sequential (LOG) sweep, 2 LOG with the per-sink state in
+// global memory (SweepArgs.gs)
 hipError_t rq_launch_sweep(const SweepArgs& a, int spl, int nK, int col16, int log, int bits, hipStream_t s);
 hipError_t rq_launch_scan(const ScanArgs& a, int nK, hipStream_t s);
 int rq_sweep_blocks_per_cu(int spl, int nK, int col16, int W, int log, int bits, int wpb, size_t lds);

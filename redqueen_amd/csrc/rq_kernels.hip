@@ -45,7 +45,7 @@ __global__ __launch_bounds__(256) void rq_gen_streams(GenArgs a)
     const int j = blockIdx.y;
     if (rl >= a.n_chunk) return;
     const int64_t o = a.chunk0 + rl;      // local output index
-    const int64_t i = a.rep0 + o;         // global replica id (seeds)
+    const int64_t i = rq_global_replica(a.rep0 + o, a.n_rep, a.rep_lo, a.rep_cnt);   // global id (seeds)
     SrcGen gen;
     gen.init(a, j, i, rq_exp_tab_c);
 
@@ -104,8 +104,10 @@ __global__ __launch_bounds__(256) void rq_gen_streams(GenArgs a)
 //       each event's aggregates are parked in its lane and the pivot rows
 //       (equal-time rows merged) are placed and stored by all lanes at once.
 //    LOG = the event log / max_events variant: phase C goes event by event.
+//    GS  = LOG with the per-sink state (rank, pivot-cell group) in global memory, one
+//          slot per resident wave (SweepArgs.gs): any number of sinks.
 // ============================================================================
-template <int SPL, int NK, class COL, int W, bool LOG, bool BITS, bool BL>
+template <int SPL, int NK, class COL, int W, bool LOG, bool BITS, bool BL, bool GS = false>
 __global__ __launch_bounds__(LOG ? 256 : (SPL >= 4 ? 512 : 1024)) void rq_sweep(SweepArgs a)
 {
     extern __shared__ double lds_g[];
@@ -155,14 +157,16 @@ __global__ __launch_bounds__(LOG ? 256 : (SPL >= 4 ? 512 : 1024)) void rq_sweep(
     // ranks: exact int for the LOG variant (pivot cells average them); the fast
     // sweep only compares them with K-1, so int16 saturating at 32767 is exact
     using RT = typename std::conditional<LOG, int, int16_t>::type;
-    RT* rank = reinterpret_cast<RT*>(wb + a.lds_rank_off);
+    // GS: this wave's slot of the global per-sink state (the grid never exceeds the slots)
+    char* gsb = GS ? a.gs + (size_t)(blockIdx.x * a.wpb + w) * (size_t)a.gs_stride : nullptr;
+    RT* rank = GS ? reinterpret_cast<RT*>(gsb) : reinterpret_cast<RT*>(wb + a.lds_rank_off);
     double* win = reinterpret_cast<double*>(wb + a.lds_win_off);
     // first replica: the wave's static slot; with a work queue (a.wq) the wave then
     // takes replicas nslot, nslot + 1, ... until the chunk is exhausted
     const int64_t nslot = (int64_t)gridDim.x * a.wpb;
     for (int64_t rl = (int64_t)blockIdx.x * a.wpb + w; rl < a.n_chunk;) {
     const int64_t o = a.chunk0 + rl;
-    const int64_t i = a.rep0 + o;
+    const int64_t i = rq_global_replica(a.rep0 + o, a.n_rep, a.gen.rep_lo, a.gen.rep_cnt);
     const int g = (int)(i / a.n_rep);
     AggL agl;
     if (BL) {
@@ -174,6 +178,7 @@ __global__ __launch_bounds__(LOG ? 256 : (SPL >= 4 ? 512 : 1024)) void rq_sweep(
     if (!BITS && !BL)
         for (int c = lane; c < a.n_sinks; c += 64) rank[c] = -1;   // NaN: no row yet
     wave_lds_sync();
+    if (GS) wave_mem_sync();
 
     // ---- arrivals: lane owns sources [lane*SPL, lane*SPL+SPL) ----
     const double* st = a.streams + rl * a.capsum;
@@ -267,10 +272,32 @@ __global__ __launch_bounds__(LOG ? 256 : (SPL >= 4 ? 512 : 1024)) void rq_sweep(
     bool pend = false;      // an equal-time group is open
     double pend_t = 0.0;
     if (LOG) {
-        int* xs = reinterpret_cast<int*>(wb + a.lds_x_off);
-        xlds = reinterpret_cast<double*>(wb + a.lds_x_off + 12 * (size_t)a.n_sinks_pad);
+        int* xs = GS ? reinterpret_cast<int*>(gsb + 4 * (size_t)a.n_sinks_pad)
+                     : reinterpret_cast<int*>(wb + a.lds_x_off);
+        xlds = reinterpret_cast<double*>(wb + a.lds_x_off + (GS ? 0 : 12 * (size_t)a.n_sinks_pad));
         ax.init(a.Ks, reinterpret_cast<int*>(rank), xs, a.n_sinks_pad, a.n_sinks, lane);
+        if (GS) wave_mem_sync();
     }
+    // one event's rows: every layer of stream j's CSR row (a layer's sinks are distinct;
+    // duplicate edges put a sink's k-th occurrence in layer k-1, opt_model.py:306-307);
+    // the controlled row's first layer is the follower list (folat)
+    auto touch_row = [&](int j, bool own, int e0, int e1) __attribute__((always_inline)) {
+        int l0 = 0, l1 = 0;
+        if (a.lay_ptr) {
+            l0 = a.lay_ptr[j];
+            l1 = a.lay_ptr[j + 1];
+            e1 = a.lay_end[l0];
+        }
+        if (own) ax.touch(folat, 0, a.n_fol, true, lane);
+        else ax.touch(colat, e0, e1, false, lane);
+        if (GS) wave_mem_sync();
+        for (int l = l0 + 1; l < l1; ++l) {
+            const int e2 = a.lay_end[l];
+            ax.touch(colat, e1, e2, own, lane);
+            if (GS) wave_mem_sync();
+            e1 = e2;
+        }
+    };
     auto close_row = [&]() __attribute__((always_inline)) -> bool {
         pend = false;
         return rs.put(pend_t, ax.row_sum(a.n_sinks, xlds), ax.nvalid, ax.cnt, lane, status);
@@ -291,10 +318,10 @@ __global__ __launch_bounds__(LOG ? 256 : (SPL >= 4 ? 512 : 1024)) void rq_sweep(
                 pend_t = tev;
             }
             if (own) {
-                ax.touch(folat, 0, a.n_fol, true, lane);
+                touch_row(a.ctrl_idx, true, 0, 0);
                 ++posts;
             } else {
-                ax.touch(colat, e0, e1, false, lane);
+                touch_row(jw, false, e0, e1);
                 ++world;
             }
         }
@@ -911,30 +938,35 @@ int rq_cu_count()
     }();
     return n;
 }
-template <int SPL, int NK, class COL, int W, bool LOG, bool BITS = false, bool BL = false>
+template <int SPL, int NK, class COL, int W, bool LOG, bool BITS = false, bool BL = false, bool GS = false>
 static int occ_t(int wpb, size_t lds);
-template <int SPL, int NK, class COL, int W, bool LOG, bool BITS = false, bool BL = false>
+template <int SPL, int NK, class COL, int W, bool LOG, bool BITS = false, bool BL = false, bool GS = false>
 static hipError_t launch_sweep_t(const SweepArgs& a, hipStream_t s)
 {
     unsigned blocks = (unsigned)((a.n_chunk + a.wpb - 1) / a.wpb);
     if (a.wq) {
         // persistent grid: every resident wave slot once, the rest from the queue
-        const int nb_c = occ_t<SPL, NK, COL, W, LOG, BITS, BL>(a.wpb, a.lds_total);
+        const int nb_c = occ_t<SPL, NK, COL, W, LOG, BITS, BL, GS>(a.wpb, a.lds_total);
         const unsigned cap = (unsigned)(nb_c > 0 ? nb_c : 1) * (unsigned)rq_cu_count();
         if (cap < blocks) blocks = cap;
     }
-    hipLaunchKernelGGL((rq_sweep<SPL, NK, COL, W, LOG, BITS, BL>), dim3(blocks), dim3(64 * a.wpb), a.lds_total, s, a);
+    if (GS) {   // one global per-sink state slot per wave of the grid
+        const unsigned cap = (unsigned)(a.gs_slots / a.wpb);
+        if (!a.wq || cap < 1) return hipErrorInvalidValue;
+        if (cap < blocks) blocks = cap;
+    }
+    hipLaunchKernelGGL((rq_sweep<SPL, NK, COL, W, LOG, BITS, BL, GS>), dim3(blocks), dim3(64 * a.wpb), a.lds_total, s, a);
     return hipGetLastError();
 }
 
-template <int SPL, class COL, int W, bool LOG>
+template <int SPL, class COL, int W, bool LOG, bool GS = false>
 static hipError_t launch_sweep_k(const SweepArgs& a, int nK, hipStream_t s)
 {
     switch (nK) {
-    case 1: return launch_sweep_t<SPL, 1, COL, W, LOG>(a, s);
-    case 2: return launch_sweep_t<SPL, 2, COL, W, LOG>(a, s);
-    case 3: return launch_sweep_t<SPL, 3, COL, W, LOG>(a, s);
-    default: return launch_sweep_t<SPL, 4, COL, W, LOG>(a, s);
+    case 1: return launch_sweep_t<SPL, 1, COL, W, LOG, false, false, GS>(a, s);
+    case 2: return launch_sweep_t<SPL, 2, COL, W, LOG, false, false, GS>(a, s);
+    case 3: return launch_sweep_t<SPL, 3, COL, W, LOG, false, false, GS>(a, s);
+    default: return launch_sweep_t<SPL, 4, COL, W, LOG, false, false, GS>(a, s);
     }
 }
 
@@ -964,14 +996,28 @@ hipError_t rq_launch_gen(const GenArgs& a, hipStream_t s)
 hipError_t rq_launch_sweep(const SweepArgs& a, int spl, int nK, int col16, int log, int bits, hipStream_t s)
 {
     if (a.n_chunk <= 0) return hipSuccess;
-    // event log / max_events: the sequential variant, W = 8; one source per lane when
-    // they fit (the per-lane ring state of eight sources costs ~200 VGPRs and spills)
-    if (log && spl == 1)
-        return col16 ? launch_sweep_k<1, uint16_t, 8, true>(a, nK, s)
-                     : launch_sweep_k<1, int, 8, true>(a, nK, s);
+    // event log / max_events / duplicate edges / > 512 sources: the sequential variant,
+    // W = 8; one source per lane when they fit (the per-lane ring state of eight sources
+    // costs ~200 VGPRs and spills; 16 / 32 per lane spill more -- correctness instances
+    // for 513..2048 sources, global columns only)
+    if (log == 2)
+        switch (spl) {
+        case 1: return col16 ? launch_sweep_k<1, uint16_t, 8, true, true>(a, nK, s)
+                             : launch_sweep_k<1, int, 8, true, true>(a, nK, s);
+        case 8: return col16 ? launch_sweep_k<8, uint16_t, 8, true, true>(a, nK, s)
+                             : launch_sweep_k<8, int, 8, true, true>(a, nK, s);
+        case 16: return launch_sweep_k<16, int, 8, true, true>(a, nK, s);
+        default: return launch_sweep_k<32, int, 4, true, true>(a, nK, s);   // 4-deep rings: LDS
+        }
     if (log)
-        return col16 ? launch_sweep_k<8, uint16_t, 8, true>(a, nK, s)
-                     : launch_sweep_k<8, int, 8, true>(a, nK, s);
+        switch (spl) {
+        case 1: return col16 ? launch_sweep_k<1, uint16_t, 8, true>(a, nK, s)
+                             : launch_sweep_k<1, int, 8, true>(a, nK, s);
+        case 8: return col16 ? launch_sweep_k<8, uint16_t, 8, true>(a, nK, s)
+                             : launch_sweep_k<8, int, 8, true>(a, nK, s);
+        case 16: return launch_sweep_k<16, int, 8, true>(a, nK, s);
+        default: return launch_sweep_k<32, int, 4, true>(a, nK, s);
+        }
     switch (spl) {
     case 1: return launch_sweep_c<1>(a, nK, col16, bits, s);
     case 2: return launch_sweep_c<2>(a, nK, col16, bits, s);
@@ -982,19 +1028,19 @@ hipError_t rq_launch_sweep(const SweepArgs& a, int spl, int nK, int col16, int l
 
 // blocks of 64*wpb threads per CU the chosen sweep instance reaches with `lds`
 // bytes of dynamic LDS (VGPR, SGPR and LDS limits all applied by the runtime)
-template <int SPL, int NK, class COL, int W, bool LOG, bool BITS, bool BL>
+template <int SPL, int NK, class COL, int W, bool LOG, bool BITS, bool BL, bool GS>
 static int occ_t(int wpb, size_t lds)
 {
-    return rq_occupancy(rq_sweep<SPL, NK, COL, W, LOG, BITS, BL>, 64 * wpb, lds);
+    return rq_occupancy(rq_sweep<SPL, NK, COL, W, LOG, BITS, BL, GS>, 64 * wpb, lds);
 }
-template <int SPL, class COL, int W, bool LOG>
+template <int SPL, class COL, int W, bool LOG, bool GS = false>
 static int occ_k(int nK, int wpb, size_t lds)
 {
     switch (nK) {
-    case 1: return occ_t<SPL, 1, COL, W, LOG>(wpb, lds);
-    case 2: return occ_t<SPL, 2, COL, W, LOG>(wpb, lds);
-    case 3: return occ_t<SPL, 3, COL, W, LOG>(wpb, lds);
-    default: return occ_t<SPL, 4, COL, W, LOG>(wpb, lds);
+    case 1: return occ_t<SPL, 1, COL, W, LOG, false, false, GS>(wpb, lds);
+    case 2: return occ_t<SPL, 2, COL, W, LOG, false, false, GS>(wpb, lds);
+    case 3: return occ_t<SPL, 3, COL, W, LOG, false, false, GS>(wpb, lds);
+    default: return occ_t<SPL, 4, COL, W, LOG, false, false, GS>(wpb, lds);
     }
 }
 template <int SPL>
@@ -1010,9 +1056,20 @@ static int occ_c(int nK, int col16, int W, int bits, int wpb, size_t lds)
 }
 int rq_sweep_blocks_per_cu(int spl, int nK, int col16, int W, int log, int bits, int wpb, size_t lds)
 {
-    if (log && spl == 1)
-        return col16 ? occ_k<1, uint16_t, 8, true>(nK, wpb, lds) : occ_k<1, int, 8, true>(nK, wpb, lds);
-    if (log) return col16 ? occ_k<8, uint16_t, 8, true>(nK, wpb, lds) : occ_k<8, int, 8, true>(nK, wpb, lds);
+    if (log == 2)
+        switch (spl) {
+        case 1: return col16 ? occ_k<1, uint16_t, 8, true, true>(nK, wpb, lds) : occ_k<1, int, 8, true, true>(nK, wpb, lds);
+        case 8: return col16 ? occ_k<8, uint16_t, 8, true, true>(nK, wpb, lds) : occ_k<8, int, 8, true, true>(nK, wpb, lds);
+        case 16: return occ_k<16, int, 8, true, true>(nK, wpb, lds);
+        default: return occ_k<32, int, 4, true, true>(nK, wpb, lds);
+        }
+    if (log)
+        switch (spl) {
+        case 1: return col16 ? occ_k<1, uint16_t, 8, true>(nK, wpb, lds) : occ_k<1, int, 8, true>(nK, wpb, lds);
+        case 8: return col16 ? occ_k<8, uint16_t, 8, true>(nK, wpb, lds) : occ_k<8, int, 8, true>(nK, wpb, lds);
+        case 16: return occ_k<16, int, 8, true>(nK, wpb, lds);
+        default: return occ_k<32, int, 4, true>(nK, wpb, lds);
+        }
     switch (spl) {
     case 1: return occ_c<1>(nK, col16, W, bits, wpb, lds);
     case 2: return occ_c<2>(nK, col16, W, bits, wpb, lds);

@@ -86,7 +86,7 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
     const int64_t nslot = (int64_t)gridDim.x * a.wpb;
     for (int64_t rl = (int64_t)blockIdx.x * a.wpb + w; rl < a.n_chunk;) {
     const int64_t o = a.chunk0 + rl;
-    const int64_t i = a.rep0 + o;
+    const int64_t i = rq_global_replica(a.rep0 + o, a.n_rep, a.gen.rep_lo, a.gen.rep_cnt);
     const int g = (int)(i / a.n_rep);
     for (int j = lane; j < a.n_str; j += 64) invc[j] = a.inv_c[(int64_t)g * a.n_str + j];
     if (!BITS)

@@ -167,12 +167,15 @@ class Graph:
     def _run(self, ctrl="opt", q=1.0, s=None, n_rep=1, ctrl_seed=0, world_seed=0,
             randomize=False, seed_mod=0, ctrl_rate=None, Ks=(1,), max_events=None,
             event_log=False, cap_scale=1.0, chunk=0, stream=None, check=True, sweep_mode=0, replica0=0, n_local=0,
-            plan_only=False, s_pw=None, period=None):
+            plan_only=False, s_pw=None, period=None, rep_lo=0, rep_cnt=0):
         """Enqueue one batch.  ``q``: scalar or [n_grid]; ``s``: per grid point
         row(s) over the sorted followers ([n_grid, F]) or anything ``s_matrix``
         takes.  Seeds: int base (seed + replica id) or a device uint32 tensor.
         ``ctrl="sig"`` (OptPWSignificance): ``s_pw`` [F, S] or [n_grid, F, S] over the
-        sorted followers and ``period`` T."""
+        sorted followers and ``period`` T.
+        ``rep_lo`` / ``rep_cnt``: run only replicas [rep_lo, rep_lo + rep_cnt) of every grid
+        point (a balanced multi-GPU shard, rq_batch_desc.rep_lo); ``replica0`` / ``n_local``
+        then index that n_grid x rep_cnt space, and so do the outputs."""
         dev = torch.device("cuda", torch.cuda.current_device())
         ck = CTRL_BY_NAME[ctrl] if isinstance(ctrl, str) else int(ctrl)
         qv = _arr(np.atleast_1d(q), np.float64)
@@ -198,7 +201,12 @@ class Graph:
             if spw.ndim != 3 or spw.shape[:2] != (n_grid, self.n_followers) or spw.shape[2] < 1:
                 raise ValueError("s_pw must be [n_grid, n_followers, n_segments]")
         R_all = n_grid * int(n_rep)
-        R = int(n_local) if n_local else R_all - int(replica0)
+        cnt = int(rep_cnt) if rep_cnt else int(n_rep)
+        lo = int(rep_lo) if rep_cnt else 0
+        R = int(n_local) if n_local else n_grid * cnt - int(replica0)
+        # global replica ids of this call's outputs (rq_global_replica)
+        sp = np.arange(int(replica0), int(replica0) + R, dtype=np.int64)
+        gids = sp if cnt == int(n_rep) else (sp // cnt) * int(n_rep) + lo + sp % cnt
         Ks = _arr(Ks, np.int32)
         if not 1 <= Ks.size <= L.MAX_K:
             raise ValueError("1..%d K values per run" % L.MAX_K)
@@ -224,7 +232,7 @@ class Graph:
             b.world_seed0 = int(world_seed) & 0xFFFFFFFF
         b.seed_mod = int(seed_mod)
         if self.plugins and randomize:
-            self._plugin_streams(b, keep, dev, R_all, int(replica0), R, world_seed, int(seed_mod))
+            self._plugin_streams(b, keep, dev, R_all, gids, world_seed, int(seed_mod))
         if ck == L.SRC_POISSON2:
             if ctrl_rate is None:
                 raise ValueError("ctrl_rate required for a Poisson controlled source")
@@ -244,6 +252,8 @@ class Graph:
         b.sweep_mode = int(sweep_mode)
         b.replica0 = int(replica0)
         b.n_local = int(n_local)
+        b.rep_lo = lo
+        b.rep_cnt = int(rep_cnt)
         if spw is not None:
             b.n_seg = spw.shape[2]
             b.period = float(period)
@@ -256,9 +266,9 @@ class Graph:
                     "blocks_per_cu", "columns_in_lds", "lds_bytes_per_block", "chunk")
             return dict(zip(keys, (int(v) for v in info)))
         return self._run_loop(lib, b, keep, dev, R, Ks, n_grid, n_rep, ck, event_log,
-                              replica0, check, stream)
+                              gids, check, stream)
 
-    def _run_loop(self, lib, b, keep, dev, R, Ks, n_grid, n_rep, ck, event_log, replica0,
+    def _run_loop(self, lib, b, keep, dev, R, Ks, n_grid, n_rep, ck, event_log, gids,
                   check, use):
         while True:
             nbytes = C.c_size_t()
@@ -282,7 +292,8 @@ class Graph:
             L.check("rq_run_batch", lib.rq_run_batch(self._h, C.byref(b), C.byref(out),
                                                      self._ws.data_ptr(), self._ws.numel(), st))
             res = BatchResult(self, metrics, counts, status, ev_t, ev_src, Ks, n_grid, int(n_rep))
-            res.replica0 = int(replica0)
+            res.replica0 = int(gids[0]) if len(gids) else 0
+            res.global_ids = gids
             if not check:
                 return res
             use.synchronize()
@@ -293,7 +304,7 @@ class Graph:
                 # sequential variant comes from the library's own plan (rq_plan_info
                 # variant 1), not from a re-derivation of its rules here.
                 if int((status & L.ST_TIE).any().item()) and b.sweep_mode != 2 \
-                        and self._plan_variant(lib, b) % 10 != 1:
+                        and self._plan_variant(lib, b) % 10 not in (1, 4):
                     b.sweep_mode = 2
                     continue
                 return res
@@ -301,7 +312,7 @@ class Graph:
                 raise L.RQError("rq_run_batch", L.RQ_EOVERFLOW)
             b.cap_scale = b.cap_scale * 2.0
 
-    def _plugin_streams(self, b, keep, dev, R_all, replica0, R, world_seed, seed_mod):
+    def _plugin_streams(self, b, keep, dev, R_all, gids, world_seed, seed_mod):
         """Per-replica times of the registered static broadcasters of a randomized
         batch: replica i's instance gets seed u_i + 99 idx (randomize_other_sources,
         opt_model.py:795-804) and the host runs its initialize() / get_all_times();
@@ -313,7 +324,8 @@ class Graph:
             raise NotImplementedError("more than %d plugin broadcasters" % L.MAX_RD)
         counts = np.zeros((R_all, nrd), dtype=np.int64)
         chunks = []
-        for i in range(replica0, replica0 + R):
+        for i in gids:   # increasing: rd_off is a prefix over the global ids
+            i = int(i)
             k = i % seed_mod if seed_mod > 0 else i
             u = int(wseed[i]) if wseed is not None else int(world_seed) + k
             for c, (idx, cls, kw, _sid) in enumerate(self.plugins):
@@ -418,8 +430,10 @@ class BatchResult:
             a, b = int(ro[i]), int(ro[i + 1])
             return pd.DataFrame({k: host[k][a:b] for k in
                                  ("event_id", "time_delta", "src_id", "t", "sink_id")})
-        rep = np.repeat(np.arange(len(ro) - 1, dtype=np.int64) + getattr(self, "replica0", 0),
-                        np.diff(ro))
+        gids = getattr(self, "global_ids", None)
+        if gids is None:
+            gids = np.arange(len(ro) - 1, dtype=np.int64) + getattr(self, "replica0", 0)
+        rep = np.repeat(np.asarray(gids, dtype=np.int64), np.diff(ro))
         return pd.DataFrame(dict(replica=rep, **host))
 
     def events(self, i):

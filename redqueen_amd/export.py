@@ -19,8 +19,10 @@ COLUMNS = ("event_id", "time_delta", "src_id", "t", "sink_id")
 def host_columns(res):
     """(row_off, {replica, event_id, time_delta, src_id, t, sink_id} numpy) of a batch."""
     ro, cols = res.log_columns()
-    out = {"replica": np.repeat(np.arange(len(ro) - 1, dtype=np.int64) + getattr(res, "replica0", 0),
-                                np.diff(ro))}
+    gids = getattr(res, "global_ids", None)
+    if gids is None:
+        gids = np.arange(len(ro) - 1, dtype=np.int64) + getattr(res, "replica0", 0)
+    out = {"replica": np.repeat(np.asarray(gids, dtype=np.int64), np.diff(ro))}
     for k in COLUMNS:
         out[k] = cols[k].cpu().numpy()
     return ro, out

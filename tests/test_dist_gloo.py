@@ -23,6 +23,12 @@ def _rows(a, b, C=5):
     return torch.sin(i * 1.37 + torch.arange(C, dtype=torch.float64)) * (i + 1)
 
 
+def _grid_rows(n_grid, n_rep, lo, hi):
+    """Rows of the replica window [lo, hi) of every grid point, grid point major."""
+    ids = [g * n_rep + r for g in range(n_grid) for r in range(lo, hi)]
+    return torch.cat([_rows(i, i + 1) for i in ids], 0) if ids else _rows(0, 0)
+
+
 def _worker(rank, world, port, n_grid, n_rep, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -31,12 +37,15 @@ def _worker(rank, world, port, n_grid, n_rep, q):
     a, b = D.shard(R, world, rank)
     rows = D.gather_rows(_rows(a, b), R)
     means = D.grid_means(rows, n_grid, n_rep)
+    lo, hi = D.grid_shard(n_rep, world, rank)
+    grows = D.gather_grid_rows(_grid_rows(n_grid, n_rep, lo, hi), n_grid, n_rep)
+    assert (grows == rows).all()
     q.put((rank, rows.numpy(), means.numpy()))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n_grid,n_rep", [(2, 3, 5), (3, 2, 7), (2, 1, 1)])
+@pytest.mark.parametrize("world,n_grid,n_rep", [(2, 3, 5), (3, 2, 7), (2, 1, 1), (3, 4, 2)])
 def test_sharded_gather_is_rank_count_independent(world, n_grid, n_rep):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -65,3 +74,15 @@ def test_shards_cover_exactly():
                 a, b = D.shard(R, w, r)
                 cov += list(range(a, b))
             assert cov == list(range(R))
+
+
+def test_grid_shards_see_every_grid_point():
+    """grid_shard: every rank owns the same replica window of every grid point, the
+    windows tile [0, n_rep), and per-rank replica counts differ by at most n_grid."""
+    for n_grid, n_rep in ((1, 10), (64, 1000), (6, 7), (3, 2)):
+        for w in (1, 2, 3, 8):
+            wins = [D.grid_shard(n_rep, w, r) for r in range(w)]
+            assert wins[0][0] == 0 and wins[-1][1] == n_rep
+            assert all(wins[k][1] == wins[k + 1][0] for k in range(w - 1))
+            sizes = [n_grid * (hi - lo) for lo, hi in wins]
+            assert max(sizes) - min(sizes) <= n_grid

@@ -1,9 +1,9 @@
 """The real multi-process path through the engine: world-size-2
 run_sharded with BOTH ranks on the one GPU of the test box and gloo for the
 exchange (the driver's 8-GPU runs use nccl = RCCL over xGMI; only the transport
-differs).  Each rank runs its contiguous shard of a q x s x seeds grid and of a
-C3 batch; the gathered per-replica rows and the fixed-order grid means must equal
-the unsharded single-process batch bit for bit."""
+differs).  Each rank runs its replica window of every grid point of a q x s x
+seeds grid and its half of a C3 batch; the gathered per-replica rows and the
+fixed-order grid means must equal the unsharded single-process batch bit for bit."""
 import os
 import socket
 
