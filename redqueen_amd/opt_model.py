@@ -393,6 +393,14 @@ class Manager:
                                     "times": plugin_times(s, self.start_time, self.sink_ids,
                                                           self.edge_list, self.end_time)})
                       for s in others]
+        if isinstance(ctrl, (Opt, OptPWSignificance)):
+            fl = [e[1] for e in self.edge_list if e[0] == ctrl.src_id]
+            if len(set(fl)) != len(fl):
+                # the reference's per-edge follower vectors (sqrt_s_by_q / old_ranks,
+                # opt_model.py:510-517, :582) against one rank per distinct follower:
+                # its first non-own event raises
+                raise ValueError("shapes (%d,) and (%d,) not aligned: duplicated edges of the "
+                                 "controlled source %r" % (len(fl), len(set(fl)), ctrl.src_id))
         ctrl_a = ctrl_b = None
         if isinstance(ctrl, PiecewiseConst):
             ctrl_a, ctrl_b = ctrl.change_times, ctrl.rates

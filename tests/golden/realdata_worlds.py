@@ -35,7 +35,31 @@ def realdata_worlds():
                              ("RealData", {"src_id": 7, "times": [0.3, 1.0 / 3.0, 2.0 / 3.0, 3.0]})],
               edge_list=[(2, 1), (7, 1), (7, 2), (4, 2)])
     c3 = [1e-300, 0.1 + 1e-12, 0.7, 1.7]
-    return [("rd1", w1, c1, None), ("rd2", w2, c2, None), ("rd2m", w2, c2, 17), ("rd3", w3, c3, None)]
+    # multigraphs (duplicate edges, which Manager.__init__ accepts, opt_model.py:169-175):
+    # every duplicated (source, sink) edge repeats that sink's rows of each event
+    # (opt_model.py:306-307), so the pivot cells average consecutive ranks (k + 1/2, ...)
+    # and carry them by ffill; also duplicated controlled edges and equal times
+    w4 = dict(src_id=1, end_time=30.0, s=1.0, q=1.0, sink_ids=[1, 2, 3, 4],
+              other_sources=[("RealData", {"src_id": 2, "times": [0.5, 1.0, 3.0, 3.0, 7.5, 12.0,
+                                                                 20.0, 29.0]}),
+                             ("RealData", {"src_id": 3, "times": [1.0, 2.0, 7.5, 8.0, 15.0, 25.0]}),
+                             ("RealData", {"src_id": 5, "times": [4.0, 16.0, 16.0, 26.5]})],
+              edge_list=[(1, 1), (1, 2), (1, 1), (2, 1), (2, 2), (2, 1), (2, 1), (3, 3), (3, 2),
+                         (3, 3), (5, 4), (5, 1), (5, 4), (5, 4), (1, 4)])
+    c4 = [0.0, 1.0, 5.0, 7.5, 14.0, 16.0, 22.0]
+    edges5 = []
+    rs5 = np.random.RandomState(77)
+    for sid in (10, 11, 12, 13, 14):
+        for y in rs5.choice(range(1, 9), 12, replace=True):   # random multiplicities
+            edges5.append((sid, int(y)))
+    w5 = dict(src_id=10, end_time=50.0, s=1.0, q=1.0, sink_ids=list(range(1, 9)),
+              other_sources=[("RealData", {"src_id": sid,
+                                           "times": list(np.round(rs5.uniform(0, 50, 20) * 4) / 4)})
+                             for sid in (11, 12, 13, 14)],
+              edge_list=edges5)
+    c5 = list(np.round(rs5.uniform(0, 50, 15) * 4) / 4)
+    return [("rd1", w1, c1, None), ("rd2", w2, c2, None), ("rd2m", w2, c2, 17), ("rd3", w3, c3, None),
+            ("rdmg1", w4, c4, None), ("rdmg2", w5, c5, None), ("rdmg2m", w5, c5, 23)]
 
 
 class BurstyMixin:

@@ -1,0 +1,155 @@
+"""Every graph the reference accepts (Manager.__init__, opt_model.py:158-175), on the
+GPU, bit for bit against the engine-semantics oracle (oracle/rq_oracle.c):
+
+* multigraphs -- duplicate (source, sink) edges: each event repeats the sink's rows
+  (opt_model.py:306-307), RedQueen's tracked rank grows by the multiplicity
+  (:74-76) and the pivot cells average the repeated rows' ranks; the all-RealData
+  multigraph worlds equal the REFERENCE's own df (tests/test_gpu_realdata.py,
+  realdata.npz rdmg*);
+* more than 512 sources (16 and 32 sources per lane, sequential sweep);
+* 50k sinks (per-wave sink bits for K = 1, int16 ranks for K > 1, and the
+  sequential sweep with its per-sink state in global memory).
+
+A duplicated CONTROLLED edge with a RedQueen controller is refused (RQ_EINVAL /
+ValueError): the reference's sqrt_s_by_q (one entry per edge) no longer matches
+its ranks (one per distinct follower) and its first non-own event raises.
+"""
+import numpy as np
+import pytest
+
+from tests.test_gpu_engine import _cmp_replica, _ctx, _graph, _oracle, _world_with_seeds
+
+pytestmark = pytest.mark.gpu
+
+
+def _multigraph(rs, n_src=12, n_sinks=40, deg=6, n_fol=10, ctrl_dup=False):
+    """A C3-like world whose wall sources repeat some of their edges 1-3 times."""
+    sinks = list(range(1, n_sinks + 1))
+    fol = sorted(int(x) for x in rs.choice(sinks, n_fol, replace=False))
+    edges = [(1, f) for f in fol]
+    if ctrl_dup:
+        edges += [(1, fol[0]), (1, fol[3])]
+    others = []
+    for k in range(n_src):
+        sid = 100 + k
+        for y in rs.choice(sinks, deg, replace=False):
+            for _ in range(1 + (rs.randint(0, 4) if rs.rand() < 0.4 else 0)):
+                edges.append((sid, int(y)))
+        if k % 2:
+            others.append(("Hawkes", {"src_id": sid, "seed": 7 + k, "l_0": 0.6, "alpha": 1.0, "beta": 5.0}))
+        else:
+            others.append(("Poisson2", {"src_id": sid, "seed": 7 + k, "rate": 0.8}))
+    order = rs.permutation(len(edges))
+    edges = [edges[i] for i in order]   # duplicates anywhere in the list
+    return dict(src_id=1, end_time=40.0, q=2.0, s=1.0, sink_ids=sinks, other_sources=others,
+                edge_list=edges)
+
+
+@pytest.mark.parametrize("event_log", [False, True])
+def test_multigraph_redqueen_randomized(event_log):
+    torch, engine, graphs, O = _ctx()
+    so = _multigraph(np.random.RandomState(3))
+    g = _graph(engine, so)
+    Ks = (1, 2, 5)
+    R = 24
+    res = g.run("opt", q=so["q"], s=so["s"], n_rep=R, ctrl_seed=40, world_seed=40, randomize=True,
+                Ks=Ks, event_log=event_log)
+    assert int(res.status.max().item()) == 0
+    for r in range(0, R, 5):
+        u = 40 + r
+        met_o, t_o, s_o = _oracle(O, _world_with_seeds(so, u), ("opt", u), Ks)
+        _cmp_replica(res, r, met_o, t_o, s_o, Ks)
+    if event_log:   # the exported df repeats the duplicated sinks' rows
+        df = res.dataframe(0)
+        sc = O.Scenario(_world_with_seeds(so, 40), ("opt", 40))
+        t, dt, s = O.engine_run(sc)
+        cols = sc.expand(t, dt, s)
+        for c in ("event_id", "src_id", "t", "sink_id"):
+            assert np.array_equal(df[c].values, cols[c]), c
+
+
+def test_multigraph_duplicated_controlled_edges():
+    """A Poisson2 controlled source with duplicated follower edges posts the
+    duplicated rows too; RedQueen with them is refused like the reference raises."""
+    torch, engine, graphs, O = _ctx()
+    from redqueen_amd import _lib as L
+    from redqueen_amd.opt_model import SimOpts
+    so = _multigraph(np.random.RandomState(5), ctrl_dup=True)
+    g = _graph(engine, so)
+    res = g.run("poisson", ctrl_seed=9, ctrl_rate=[2.5], n_rep=1, Ks=(1, 2), event_log=True)
+    met_o, t_o, s_o = _oracle(O, so, ("poisson", 9, 2.5), (1, 2))
+    _cmp_replica(res, 0, met_o, t_o, s_o, (1, 2))
+    with pytest.raises(L.RQError) as e:
+        g.run("opt", q=1.0, s=1.0, n_rep=1, ctrl_seed=1)
+    assert e.value.code == L.RQ_EINVAL
+    m = SimOpts(**so).create_manager_with_opt(3)
+    with pytest.raises(ValueError):
+        m.run_dynamic()
+
+
+def _many_sources(n_src, n_sinks=120, deg=3, T=6.0, seed=11):
+    rs = np.random.RandomState(seed)
+    sinks = list(range(1, n_sinks + 1))
+    fol = sorted(int(x) for x in rs.choice(sinks, 30, replace=False))
+    edges = [(0, f) for f in fol]
+    others = []
+    for k in range(n_src):
+        sid = 1000 + k
+        edges += [(sid, int(y)) for y in rs.choice(sinks, deg, replace=False)]
+        if k % 3 == 0:
+            others.append(("Hawkes", {"src_id": sid, "seed": k, "l_0": 0.3, "alpha": 1.0, "beta": 4.0}))
+        else:
+            others.append(("Poisson2", {"src_id": sid, "seed": k, "rate": 0.4}))
+    return dict(src_id=0, end_time=T, q=1.0, s=1.0, sink_ids=sinks, other_sources=others,
+                edge_list=edges)
+
+
+@pytest.mark.parametrize("n_src", [600, 1500])
+def test_more_than_512_sources(n_src):
+    torch, engine, graphs, O = _ctx()
+    so = _many_sources(n_src)
+    g = _graph(engine, so)
+    plan = g.run("opt", q=1.0, s=1.0, n_rep=4, plan_only=True)
+    assert plan["variant"] in (1, 4) and plan["sources_per_lane"] == (16 if n_src <= 1024 else 32)
+    Ks = (1, 2)
+    res = g.run("opt", q=1.0, s=1.0, n_rep=4, ctrl_seed=2, world_seed=2, randomize=True, Ks=Ks,
+                event_log=True)
+    assert int(res.status.max().item()) == 0
+    for r in (0, 3):
+        met_o, t_o, s_o = _oracle(O, _world_with_seeds(so, 2 + r), ("opt", 2 + r), Ks)
+        _cmp_replica(res, r, met_o, t_o, s_o, Ks)
+
+
+def _wide(n_sinks=50000, n_src=40, deg=60, T=4.0):
+    rs = np.random.RandomState(21)
+    sinks = list(range(10, 10 + n_sinks))
+    fol = sorted(int(x) for x in rs.choice(sinks, 400, replace=False))
+    edges = [(1, f) for f in fol]
+    others = []
+    for k in range(n_src):
+        sid = 2 + k
+        ys = [int(y) for y in rs.choice(sinks, deg, replace=False)]
+        ys += [int(y) for y in rs.choice(fol, 6, replace=False) if int(y) not in ys][:3]
+        edges += [(sid, y) for y in ys]   # a simple graph (no duplicated edge)
+        others.append(("Poisson2", {"src_id": sid, "seed": 3 + k, "rate": 1.5}))
+    return dict(src_id=1, end_time=T, q=0.5, s=1.0, sink_ids=sinks, other_sources=others,
+                edge_list=edges)
+
+
+@pytest.mark.parametrize("Ks,kw,variant", [
+    ((1,), {}, 3),                                  # K = 1: per-wave LDS sink bits
+    ((1, 2), {}, 0),                                # int16 ranks, one wave per block (fused or not)
+    ((1, 2), dict(sweep_mode=2, event_log=True), 4),   # sequential, per-sink state in HBM
+])
+def test_50k_sinks(Ks, kw, variant):
+    torch, engine, graphs, O = _ctx()
+    so = _wide()
+    g = _graph(engine, so)
+    plan = g.run("opt", q=so["q"], s=so["s"], n_rep=6, Ks=Ks, plan_only=True, **kw)
+    assert plan["variant"] % 10 == variant, plan
+    res = g.run("opt", q=so["q"], s=so["s"], n_rep=6, ctrl_seed=70, world_seed=70, randomize=True,
+                Ks=Ks, **kw)
+    assert int(res.status.max().item()) == 0
+    for r in (0, 5):
+        met_o, t_o, s_o = _oracle(O, _world_with_seeds(so, 70 + r), ("opt", 70 + r), Ks)
+        _cmp_replica(res, r, met_o, t_o, s_o, Ks)
