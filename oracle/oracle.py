@@ -17,7 +17,9 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB = os.path.join(_HERE, "librq_oracle.so")
+# env RQO_SO_PATH: an alternative build of the same sources (the sanitizer build,
+# scripts/asan_cpu.sh)
+_LIB = os.environ.get("RQO_SO_PATH") or os.path.join(_HERE, "librq_oracle.so")
 
 POISSON, POISSON2, HAWKES, PWCONST, REALDATA, OPT, OPTPW = 1, 2, 3, 4, 5, 6, 7
 KIND = {"Poisson": POISSON, "Poisson2": POISSON2, "Hawkes": HAWKES,

@@ -814,7 +814,7 @@ static int engine_stream(const rqo_source* s, uint32_t salt, double start, doubl
         for (int i = 0; i < s->n_arr; i++)
             if (s->a[i] >= start && s->a[i] <= end)
                 if (dvec_push(out, s->a[i])) return -1;
-        qsort(out->v, (size_t)out->n, sizeof(double), cmp_dbl);
+        if (out->n > 1) qsort(out->v, (size_t)out->n, sizeof(double), cmp_dbl);   /* v may be NULL */
         return 0;
     }
     default:

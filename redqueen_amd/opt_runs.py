@@ -121,3 +121,194 @@ def worker_oracle(params):
     if queue is not None:
         queue.put(op)
     return op
+
+
+def extract_perf_fields(return_obj, exclude_fields=None, include_fields=None):
+    """opt_runs.extract_perf_fields (opt_runs.py:345-354), fields in
+    perf_opts.performance_fields order (the reference iterates a set)."""
+    include_fields = include_fields if include_fields is not None else set()
+    exclude_fields = exclude_fields if exclude_fields is not None else set()
+    fields = [f for f in perf_opts.performance_fields if f not in exclude_fields]
+    fields += sorted(set(include_fields) - set(fields) - set(exclude_fields))
+    return {f: return_obj[f] for f in fields}
+
+
+def _world_key(so):
+    """The world of a SimOpts without its sources' seeds (batchable replicas share it)."""
+    from .batch import _val_key
+    return (so.src_id, float(so.end_time), tuple(map(tuple, so.edge_list)), tuple(so.sink_ids),
+            repr([(n if isinstance(n, str) else n.__name__,
+                   sorted((k, _val_key(v)) for k, v in kw.items() if k != "seed"))
+                  for n, kw in so.other_sources]))
+
+
+def _randomize_seed(so):
+    """u such that so's other sources carry the randomize_other_sources(u) seeds
+    (u + 99 idx, opt_model.py:795-804), or None."""
+    idx_seeds = [(i, kw["seed"]) for i, (_, kw) in enumerate(so.other_sources) if "seed" in kw]
+    if len(idx_seeds) != len(so.other_sources):
+        return None
+    if not idx_seeds:
+        return 0
+    u = (int(idx_seeds[0][1]) - 99 * idx_seeds[0][0]) & 0xFFFFFFFF
+    ok = all((int(s) & 0xFFFFFFFF) == ((u + 99 * i) & 0xFFFFFFFF) for i, s in idx_seeds)
+    return u if ok else None
+
+
+def _opt_poisson_batches(worlds, qs, seeds, num_segments):
+    """worker_opt then worker_poisson for every (q, seed) as two GPU batches over the
+    q x seed grid; worlds[k] = sim_opts_gen(seeds[k]) (one shared network whose
+    sources carry randomize_other_sources(u_k) seeds).  Returns the op dicts in
+    (q, seed) order: [(opt_op, poisson_op)]."""
+    import torch
+    from .batch import compiled_graph
+    base = worlds[0]
+    g = compiled_graph(base)
+    N = len(seeds)
+    us = np.asarray([_randomize_seed(w) for w in worlds], dtype=np.int64)
+    sd = np.asarray(seeds, dtype=np.int64)
+    Ks = tuple(perf_opts.Ks)
+    qv = np.asarray(qs, dtype=np.float64)
+    seed_t = torch.as_tensor(np.tile(sd, len(qv)))
+    u_t = torch.as_tensor(np.tile(us, len(qv)))
+    ro = g.run("opt", q=qv, s=g.s_matrix(base.s, len(qv)), n_rep=N, ctrl_seed=seed_t,
+               world_seed=u_t, randomize=True, Ks=Ks, event_log=True)
+    posts = ro.num_events.double()
+    rp = g.run("poisson", n_rep=len(qv) * N, ctrl_seed=seed_t, world_seed=u_t, randomize=True,
+               ctrl_rate=posts / float(base.end_time), Ks=Ks)
+    ro_m, ro_c = ro.metrics.cpu().numpy(), ro.counts.cpu().numpy()
+    rp_m, rp_c = rp.metrics.cpu().numpy(), rp.counts.cpu().numpy()
+    row_off, cols = ro.log_columns()
+    host = {k: v.cpu().numpy() for k, v in cols.items()}
+    import pandas as pd
+    out = []
+    for gi, q in enumerate(qv):
+        for k, seed in enumerate(sd):
+            i = gi * N + k
+            so = worlds[k].update({"q": float(q)})
+            a, b = int(row_off[i]), int(row_off[i + 1])
+            df = pd.DataFrame({c: host[c][a:b] for c in ("event_id", "time_delta", "src_id", "t", "sink_id")})
+            op = {"type": "Opt", "seed": int(seed), "capacity": float(ro_c[i, 0]), "sim_opts": so,
+                  "q": so.q, "wall_intensities": _wall_intensities(df, so, num_segments)}
+            pp = {"type": "Poisson", "seed": int(seed), "sim_opts": so, "q": so.q}
+            for dst, m, c in ((op, ro_m[i], ro_c[i]), (pp, rp_m[i], rp_c[i])):
+                for j, kk in enumerate(Ks):
+                    dst["top_" + str(kk)] = np.float64(m[j])
+                dst["avg_rank"] = np.float64(m[len(Ks)])
+                dst["r_2"] = np.float64(m[len(Ks) + 1])
+                dst["world_events"] = int(c[1])
+                dst["num_events"] = int(c[0])
+            out.append((op, pp))
+    return out
+
+
+def run_inference_queue(N=None, T=None, num_segments=None, sim_opts_gen=None, log_q_high=None,
+                        log_q_low=None, num_procs=None, opts=None):
+    """opt_runs.run_inference_queue (opt_runs.py:560-646): for every q in
+    logspace(log_q_low, log_q_high, 10) and seed in range(N), RedQueen on
+    sim_opts_gen(seed).update({'q': q}) (worker_opt), then the follow-ups the
+    reference queues after each Opt result: Poisson at the Opt replica's capacity
+    (worker_poisson) and the Oracle at that capacity (worker_oracle).
+
+    The Opt and Poisson legs run as two GPU batches over the whole q x seed grid
+    when the generated worlds share one network and their sources carry
+    randomize_other_sources seeds (every sim_opts_gen of opt_runs.py:290-331 does),
+    else one GPU run per replica; the Oracle leg is one GPU DP search per replica.
+    ``num_procs`` is accepted for signature parity (no process pool).
+
+    The reference's 'kdd' follow-up (Karimi et al., broadcast.opt.optimizer) is not
+    vendored: there it raises in its worker and is logged as an exception record,
+    which never enters the results -- here it is logged the same way.  An Oracle
+    task that raises (worker_oracle's KeyError when q = 1 already meets the
+    capacity, utils.py:271-276) is logged and dropped as the reference's queue does.
+    Returns Options(df, raw_results, capacities) with the same fields."""
+    import pandas as pd
+    if opts is not None:   # @optioned(option_arg='opts'): explicit arguments win
+        d = opts._get_dict() if hasattr(opts, "_get_dict") else dict(opts)
+        N = d.get("N", N) if N is None else N
+        T = d.get("T", T) if T is None else T
+        num_segments = d.get("num_segments", num_segments) if num_segments is None else num_segments
+        sim_opts_gen = d.get("sim_opts_gen", sim_opts_gen) if sim_opts_gen is None else sim_opts_gen
+        log_q_high = d.get("log_q_high", log_q_high) if log_q_high is None else log_q_high
+        log_q_low = d.get("log_q_low", log_q_low) if log_q_low is None else log_q_low
+    qs = np.logspace(log_q_low, log_q_high, num=10)
+    seeds = list(range(N))
+    worlds = [sim_opts_gen(seed) for seed in seeds]
+    results, raw_results = [], []
+    capacities = {q: [] for q in qs}
+    batchable = N > 0 and len({_world_key(w) for w in worlds}) == 1 and \
+        all(_randomize_seed(w) is not None for w in worlds)
+    if batchable:
+        pairs = _opt_poisson_batches(worlds, qs, seeds, num_segments)
+    else:
+        pairs = []
+        for q in qs:
+            for seed, w in zip(seeds, worlds):
+                op = worker_opt((seed, w.update({"q": q}), num_segments, None))
+                pp = worker_poisson((seed, op["capacity"], op["sim_opts"], None))
+                pairs.append((op, pp))
+    for op, pp in pairs:
+        raw_results.append(op)
+        results.append(extract_perf_fields(op))
+        capacities[op["q"]].append((op["seed"], op["capacity"]))
+        raw_results.append(pp)
+        results.append(extract_perf_fields(pp))
+        try:
+            orc = worker_oracle((op["seed"], op["capacity"], op["world_events"], op["sim_opts"], None))
+        except Exception as e:   # the reference's worker_combined: an 'Exception' record
+            logging.error("Exception while handling: %r", {"type": "Exception", "error": e,
+                                                           "broadcaster_type": "Oracle"})
+        else:
+            raw_results.append(orc)
+            results.append(extract_perf_fields(orc))
+        logging.error("Exception while handling: %r", {
+            "type": "Exception", "broadcaster_type": "kdd",
+            "error": NameError("broadcast.opt.optimizer (Karimi et al.) is not vendored")})
+    return _Options(df=pd.DataFrame.from_records(results), raw_results=raw_results,
+                    capacities=capacities)
+
+
+# The reference's inference configurations (opt_runs.py:284-331), for
+# run_inference_queue(opts=...).
+dilation = 100.0
+simulation_opts = _Options(world_rate=1000.0 / dilation, world_alpha=1.0, world_beta=10.0,
+                           N=10, T=1.0 * dilation, num_segments=10,
+                           log_q_low=-6 + np.log10(dilation), log_q_high=5 + np.log10(dilation))
+
+
+def piecewise_sim_opt_factory(N=None, T=None, num_segments=None, world_rate=None, opts=None):
+    """opt_runs.piecewise_sim_opt_factory (opt_runs.py:294-306)."""
+    from .opt_model import SimOpts
+    d = opts._get_dict() if opts is not None else {}
+    N = d.get("N") if N is None else N
+    T = d.get("T") if T is None else T
+    num_segments = d.get("num_segments") if num_segments is None else num_segments
+    world_rate = d.get("world_rate") if world_rate is None else world_rate
+    random_state = np.random.RandomState(42)
+    world_changing_rates = random_state.uniform(low=world_rate / 2.0, high=world_rate, size=num_segments)
+    world_change_times = np.arange(num_segments) * T / num_segments
+
+    def sim_opts_gen(seed):
+        return SimOpts.std_piecewise_const(world_rates=world_changing_rates,
+                                           world_change_times=world_change_times,
+                                           world_seed=seed + 42).update({'end_time': T})
+
+    return (opts or _Options()).set_new(N=N, T=T, num_segments=num_segments, sim_opts_gen=sim_opts_gen)
+
+
+def _std_poisson_gen(seed):
+    from .opt_model import SimOpts
+    return SimOpts.std_poisson(world_rate=simulation_opts.world_rate,
+                               world_seed=seed + 42).update({'end_time': simulation_opts.T})
+
+
+def _std_hawkes_gen(seed):
+    from .opt_model import SimOpts
+    return SimOpts.std_hawkes(world_seed=seed, world_lambda_0=simulation_opts.world_rate,
+                              world_alpha=simulation_opts.world_alpha,
+                              world_beta=simulation_opts.world_beta).update({'end_time': simulation_opts.T})
+
+
+poisson_inf_opts = simulation_opts.set_new(sim_opts_gen=_std_poisson_gen)
+piecewise_inf_opts = piecewise_sim_opt_factory(opts=simulation_opts)
+hawkes_inf_opts = simulation_opts.set_new(sim_opts_gen=_std_hawkes_gen)
