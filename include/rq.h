@@ -252,8 +252,13 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out,
  *                            unique sinks
  * Workspace: rq_replay_workspace_size; the small one serves dataframes with <= 3071
  * unique sinks (the per-sink state lives in LDS), RQ_REPLAY_LARGE any width.
+ * RQ_REPLAY_CHUNKED adds room (~32 B per row + 192 KB per dataframe) for spreading ONE
+ * long dataframe over many workgroups (chunks of 4096 rows; <= 4096 unique sinks), which
+ * the call uses for up to 64 dataframes averaging >= 8192 rows (a batch of many
+ * dataframes runs one workgroup per dataframe).
  * Per dataframe: < 2^31 rows. */
 #define RQ_REPLAY_LARGE 1
+#define RQ_REPLAY_CHUNKED 2
 int rq_replay_workspace_size(int64_t n_rows, int64_t n_df, int32_t nK, int32_t flags, size_t* bytes);
 int rq_metrics_replay(const double* t, const int64_t* src, const int64_t* sink,
                       const int64_t* event_id, int64_t n_rows, int64_t src_id, double end_time,

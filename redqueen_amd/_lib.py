@@ -19,6 +19,8 @@ ST_ROWS_OVERFLOW, ST_STREAM_OVERFLOW, ST_TIE, ST_EMPTY = 1, 2, 4, 8
 RUN_EVENT_LOG = 1
 ABI_VERSION = 4
 REPLAY_LARGE = 1
+REPLAY_CHUNKED = 2
+REPLAY_CHUNK_ROWS = 4096   # RC_L: rows per workgroup of the chunked replay
 MAX_K = 4
 MAX_RD = 64
 

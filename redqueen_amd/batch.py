@@ -108,7 +108,10 @@ def run_opt_vs_poisson(sim_opts, seeds=range(10), randomize=True, Ks=(1,), max_e
     st = torch.as_tensor(seeds)
     ro = g.run("opt", q=float(sim_opts.q), s=sim_opts.s, n_rep=len(seeds), ctrl_seed=st,
                world_seed=st, randomize=randomize, Ks=Ks, max_events=max_events)
-    rate = ro.num_events.double() / float(sim_opts.end_time)
+    # capacity / end_time with IEEE division on the host (create_manager_with_poisson,
+    # opt_model.py:829): torch's tensor / scalar multiplies by the reciprocal, which is
+    # an ulp off for most capacities -- and every Poisson time with it
+    rate = torch.as_tensor(ro.num_events.cpu().numpy().astype(np.float64) / float(sim_opts.end_time))
     rp = g.run("poisson", n_rep=len(seeds), ctrl_seed=st + int(poisson_seed_offset),
                world_seed=st, randomize=randomize, ctrl_rate=rate, Ks=Ks, max_events=max_events)
     a = _frame(ro, seeds, np.full(len(seeds), float(sim_opts.q)), "Opt", Ks)

@@ -1073,6 +1073,9 @@ namespace {
 // layout adds per-df hash tables / sequential-replay state (slots [4 r0, 4 r1))
 struct RpPlan {
     size_t off_info, off_dt, off_sum, off_valid, off_cnt, off_keys, off_gkeys, off_gstate, small, large;
+    // chunked replay area (RQ_REPLAY_CHUNKED), after the large area when both are asked for
+    int64_t max_chunks;
+    size_t c_cbase, c_hkeys, c_hdense, c_gstart, c_gbase, c_carry, c_state, chunk;
 };
 RpPlan rp_plan(int64_t n_rows, int64_t n_df, int32_t nK)
 {
@@ -1089,6 +1092,20 @@ RpPlan rp_plan(int64_t n_rows, int64_t n_df, int32_t nK)
     p.off_gkeys = o; o = align_up(o + 8 * 4 * n, A);
     p.off_gstate = o; o = align_up(o + 16 * 4 * n, A);
     p.large = o;
+    // chunk area, offsets relative to its start: per df the chunk prefix and a sink hash
+    // table; per chunk (<= n_rows / RC_L + n_df) its t-group counts and RC_S carries / states
+    const size_t nd = (size_t)std::max<int64_t>(n_df, 1);
+    p.max_chunks = std::max<int64_t>(n_rows, 0) / RC_L + std::max<int64_t>(n_df, 1);
+    const size_t mc = (size_t)p.max_chunks;
+    size_t c = 0;
+    p.c_cbase = c;  c = align_up(c + 8 * (nd + 1), A);
+    p.c_hkeys = c;  c = align_up(c + 8 * nd * RC_HT, A);
+    p.c_hdense = c; c = align_up(c + 4 * nd * RC_HT, A);
+    p.c_gstart = c; c = align_up(c + 4 * mc, A);
+    p.c_gbase = c;  c = align_up(c + 8 * mc, A);
+    p.c_carry = c;  c = align_up(c + sizeof(RcCarry) * mc * RC_S, A);
+    p.c_state = c;  c = align_up(c + sizeof(RcState) * mc * RC_S, A);
+    p.chunk = c;
     return p;
 }
 
@@ -1104,8 +1121,16 @@ int rp_run(const double* t, const int64_t* src, const int64_t* sink, const int64
         if (Ks[q] < 1) return RQ_EINVAL;
     const RpPlan p = rp_plan(n_rows, n_df, nK);
     if (workspace_bytes < p.small) return RQ_EINVAL;
+    // workspace tiers (rq_replay_workspace_size): small [+ large] [+ chunk]
+    const bool both = workspace_bytes >= p.large + p.chunk;
     const bool large = workspace_bytes >= p.large;
+    const bool has_chunk = both || (!large && workspace_bytes >= p.small + p.chunk);
     char* ws = (char*)workspace;
+    char* cw = ws + (both ? p.large : p.small);
+    // one dataframe over many workgroups: few, long dataframes (a batch of many fills the
+    // chip with one workgroup each)
+    bool chunked = has_chunk && n_df <= 64 && n_rows >= 2 * (int64_t)RC_L * n_df;
+    if (const char* e = getenv("RQ_RP_CHUNK")) chunked = has_chunk && atoi(e) != 0;   // A/B only
     RpArgs a{};
     a.t = t;
     a.src = src;
@@ -1128,9 +1153,21 @@ int rp_run(const double* t, const int64_t* src, const int64_t* sink, const int64
     a.gstate = large ? (void*)(ws + p.off_gstate) : nullptr;
     a.metrics = out;
     a.counts = counts;
+    if (chunked) {
+        a.chunked = 1;
+        a.max_chunks = p.max_chunks;
+        a.cbase = (int64_t*)(cw + p.c_cbase);
+        a.ht_keys = (uint64_t*)(cw + p.c_hkeys);
+        a.ht_dense = (int*)(cw + p.c_hdense);
+        a.gstart = (int*)(cw + p.c_gstart);
+        a.gbase = (int64_t*)(cw + p.c_gbase);
+        a.carry = (RcCarry*)(cw + p.c_carry);
+        a.state = (RcState*)(cw + p.c_state);
+    }
     hipStream_t s = (hipStream_t)hip_stream;
     {
         TimedLaunch tl(K_REPLAY, s);
+        if (chunked && rq_launch_rp(a, RP_PHASE_CHUNK, s) != hipSuccess) return RQ_EHIP;
         if (rq_launch_rp(a, RP_PHASE_FAST, s) != hipSuccess) return RQ_EHIP;
         if (large && rq_launch_rp(a, RP_PHASE_GLOBAL, s) != hipSuccess) return RQ_EHIP;
         if (rq_launch_rp(a, RP_PHASE_KEYS, s) != hipSuccess) return RQ_EHIP;
@@ -1145,7 +1182,7 @@ int rq_replay_workspace_size(int64_t n_rows, int64_t n_df, int32_t nK, int32_t f
 {
     if (!bytes || n_rows < 0 || n_df < 1 || nK < 1 || nK > RQ_MAX_K) return RQ_EINVAL;
     const RpPlan p = rp_plan(n_rows, n_df, nK);
-    *bytes = (flags & RQ_REPLAY_LARGE) ? p.large : p.small;
+    *bytes = ((flags & RQ_REPLAY_LARGE) ? p.large : p.small) + ((flags & RQ_REPLAY_CHUNKED) ? p.chunk : 0);
     return RQ_OK;
 }
 

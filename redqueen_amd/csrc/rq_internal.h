@@ -174,7 +174,25 @@ struct RpInfo {
 #define RP_BIG 16        // needs the large workspace (or exceeds it)
 #define RP_EMPTYDF 32    // no rows
 #define RP_BADOFF 64     // df_off[d] .. df_off[d + 1] is not a valid row range (< 2^31 rows)
-enum { RP_PHASE_FAST = 0, RP_PHASE_GLOBAL = 1, RP_PHASE_KEYS = 2, RP_PHASE_SEQ = 3, RP_PHASE_SCAN = 4 };
+#define RP_CSKIP 128     // chunked mode: the df is not chunkable (> RC_S sinks, the INT64_MIN id):
+                         // the one-workgroup path (rq_rp_fast) takes it
+enum { RP_PHASE_FAST = 0, RP_PHASE_GLOBAL = 1, RP_PHASE_KEYS = 2, RP_PHASE_SEQ = 3, RP_PHASE_SCAN = 4,
+       RP_PHASE_CHUNK = 5 };
+// chunked replay (one dataframe over many workgroups): rows per chunk, most unique sinks
+// per dataframe, hash slots per dataframe
+#define RC_L 4096
+#define RC_S 4096
+#define RC_HT 8192
+struct RcCarry {     // one chunk's effect on one sink (rq_rc_sum)
+    int n;           // rows of the sink in the chunk
+    int after;       // rows after its last own row in the chunk (-1: no own row)
+    double last_t;   // t of its last row in the chunk
+};
+struct RcState {     // a sink's state entering a chunk (rq_rc_scan)
+    int r;           // rank of its last row (-1: no row yet, a NaN cell)
+    int pad;
+    double last_t;   // t of its last row
+};
 
 struct RpArgs {
     const double* t;
@@ -199,6 +217,17 @@ struct RpArgs {
     void* gstate;             // [4 n_rows] x 16 B
     double* metrics;          // [n_df][nK + 2]
     int64_t* counts;          // [n_df][4]
+    // chunked mode (RP_PHASE_CHUNK; null otherwise): per df chunk prefix [n_df + 1], hash
+    // tables [n_df][RC_HT], per chunk the group base, carries / entering states [chunk][RC_S]
+    int chunked;
+    int64_t max_chunks;
+    int64_t* cbase;
+    uint64_t* ht_keys;
+    int* ht_dense;
+    int* gstart;              // [chunk] t-group starts in the chunk
+    int64_t* gbase;           // [chunk] t-groups started before the chunk (within its df)
+    RcCarry* carry;
+    RcState* state;
 };
 hipError_t rq_launch_rp(const RpArgs& a, int phase, hipStream_t s);
 

@@ -41,6 +41,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "rq_device.h"
 #include "rq_internal.h"
 
@@ -51,7 +53,6 @@ using namespace rq;
 namespace {
 
 constexpr int RP_B = 1024;              // rows per batch = threads per workgroup
-constexpr int RP_LOG_B = 10;
 constexpr int RP_H = 4096;              // LDS hash slots
 constexpr int RP_LOG_H = 12;
 constexpr int RP_HMAX = RP_H - RP_B - 1;   // unique sinks the LDS table takes: a batch can
@@ -105,21 +106,8 @@ __device__ __forceinline__ int rp_gbits(int64_t n)
 
 // ---- wave scans on DPP (VALU latency; ds_bpermute shuffles cost ~100 cycles a step
 // and these chains are the batch's critical path) ----
-__device__ __forceinline__ uint32_t umax32(uint32_t a, uint32_t b) { return a > b ? a : b; }
 // inclusive 64-lane sum of 32-bit values (two's complement wrap, so int works too)
 __device__ __forceinline__ int scan_add_i32(int v) { return (int)wave_scan_add((uint32_t)v); }
-// inclusive 64-lane max of NON-NEGATIVE values (lanes outside a DPP row read 0)
-__device__ __forceinline__ int scan_max_nn(int v)
-{
-    uint32_t x = (uint32_t)v;
-    x = umax32(x, dpp0<0x111, 0xF>(x));
-    x = umax32(x, dpp0<0x112, 0xF>(x));
-    x = umax32(x, dpp0<0x114, 0xF>(x));
-    x = umax32(x, dpp0<0x118, 0xF>(x));
-    x = umax32(x, dpp0<0x142, 0xA>(x));
-    x = umax32(x, dpp0<0x143, 0xC>(x));
-    return (int)x;
-}
 // inclusive 64-lane sum of int32 values as int64 (16-bit halves scanned apart: exact)
 __device__ __forceinline__ int64_t scan_add_i64_of_i32(int v)
 {
@@ -153,15 +141,6 @@ __device__ __forceinline__ int64_t row_scan_add(int64_t v)
     }
     return v;
 }
-__device__ __forceinline__ int row_scan_max_nn(int v)
-{
-    uint32_t x = (uint32_t)v;
-    x = umax32(x, dpp0<0x111, 0xF>(x));
-    x = umax32(x, dpp0<0x112, 0xF>(x));
-    x = umax32(x, dpp0<0x114, 0xF>(x));
-    x = umax32(x, dpp0<0x118, 0xF>(x));
-    return (int)x;
-}
 
 __device__ __forceinline__ int lane_bcast(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 __device__ __forceinline__ int64_t lane_bcast(int64_t v, int l) { return bcast_i64(v, l); }
@@ -176,14 +155,6 @@ __device__ __forceinline__ void totals_add(const T* t, int w, T& pre, T& tot)
     tot = lane_bcast(x, 15);
     pre = w > 0 ? lane_bcast(x, w - 1) : (T)0;
 }
-// exclusive max-prefix of non-negative wave totals
-__device__ __forceinline__ int totals_max_nn(const int* t, int w)
-{
-    int x = lane_id() < 16 ? t[lane_id()] : 0;
-    x = row_scan_max_nn(x);
-    return w > 0 ? lane_bcast(x, w - 1) : 0;
-}
-
 template <int NK>
 struct RpAcc {
     int64_t s;      // sum of the (integral) forward-filled pivot cells
@@ -204,6 +175,7 @@ __global__ __launch_bounds__(RP_B) void rq_rp_fast(RpArgs a)
     const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
     RpInfo* inf = a.info + d;
     if (GLOBAL && !(inf->flags & RP_GLOBAL)) return;   // only the dataframes the LDS pass gave up
+    if (!GLOBAL && a.chunked && !(inf->flags & RP_CSKIP)) return;   // the chunked pass took it
     const int64_t r0 = df_begin(a, d), r1 = df_end(a, d);
     const int64_t nd = r1 - r0;
     // a malformed caller range (decreasing / negative offsets, past n_rows, >= 2^31 rows:
@@ -836,6 +808,624 @@ __global__ __launch_bounds__(64) void rq_rp_seq(RpArgs a)
 }
 
 // ============================================================================
+// Chunked replay: ONE dataframe over many workgroups (RP_PHASE_CHUNK).
+//
+// rank = (rows of the sink so far) - (position of its latest own row), so a chunk's
+// effect on a sink is a function of the sink's entering rank r alone: after an own
+// row of the sink inside the chunk, r_out = rows after it (a constant); without one,
+// r_out = max(r, 0) + n (NaN stays NaN if n = 0).  These compose associatively, so:
+//   rq_rc_plan   chunk counts per dataframe (prefix), per-df status reset
+//   rq_rc_clear  per-df sink hash tables emptied
+//   rq_rc_hash   every chunk inserts its sink ids (global atomics): S per dataframe
+//   rq_rc_dense  dense sink ids in table order
+//   rq_rc_sum    per chunk and sink: rows, rows after the last own row, last t; per chunk:
+//                t-group starts, first-of-event counts, unsorted / event-id checks
+//   rq_rc_scan   per sink, a wave scans the chunk functions: the state every chunk
+//                enters with; per dataframe the t-group base of every chunk
+//   rq_rc_apply  every chunk replays its rows exactly as rq_rp_fast does, starting from
+//                those states and from the pivot row they sum to
+//   rq_rc_keys   unique sink ids of dataframes with a pivot mean, for rq_rp_seq
+// A dataframe with more than RC_S unique sinks (or the INT64_MIN id) is flagged
+// RP_CSKIP and left to rq_rp_fast.
+// ============================================================================
+__device__ __forceinline__ int64_t rc_df_of_chunk(const RpArgs& a, int64_t c)
+{
+    int64_t lo = 0, hi = a.n_df;   // the last d with cbase[d] <= c (empty dfs share a base)
+    while (hi - lo > 1) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (a.cbase[mid] <= c) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+constexpr int RC_HBITS = 13;   // log2(RC_HT)
+static_assert((1 << RC_HBITS) == RC_HT, "RC_HT");
+static_assert(RC_L % RP_B == 0, "chunks hold whole batches");
+constexpr int RC_SKIP = RP_BADOFF | RP_EMPTYDF | RP_CSKIP;
+
+__device__ __forceinline__ int rc_dense(const uint64_t* hk, const int* hd, uint64_t k)
+{
+    uint32_t h = rp_hash(k, RC_HBITS);
+    for (int p = 0; p < RC_HT; ++p) {   // rq_rc_hash inserted every key (bounded all the same)
+        if (hk[h] == k) return hd[h];
+        h = (h + 1) & (RC_HT - 1);
+    }
+    return 0;
+}
+
+__global__ __launch_bounds__(1024) void rq_rc_plan(RpArgs a)
+{
+    __shared__ int wtot[16];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    int64_t run = 0;
+    for (int64_t d0 = 0; d0 < a.n_df; d0 += 1024) {
+        const int64_t d = d0 + tid;
+        int nc = 0;
+        if (d < a.n_df) {
+            const int64_t r0 = df_begin(a, d), r1 = df_end(a, d), nd = r1 - r0;
+            RpInfo* inf = a.info + d;
+            int fl = 0;
+            if (r0 < 0 || r1 < r0 || r1 > a.n_rows || nd >= ((int64_t)1 << 31)) fl = RP_BADOFF;
+            else if (nd == 0) fl = RP_EMPTYDF;
+            else nc = (int)((nd + RC_L - 1) / RC_L);
+            inf->n_piv = 0;
+            inf->n_own = 0;
+            inf->n_world = 0;
+            inf->S = 0;
+            inf->flags = fl;
+        }
+        const int inc = (int)wave_scan_add((uint32_t)nc);
+        if (lane == 63) wtot[w] = inc;
+        __syncthreads();
+        int64_t pre = 0, tot = 0;
+        for (int k = 0; k < 16; ++k) {
+            pre += k < w ? wtot[k] : 0;
+            tot += wtot[k];
+        }
+        if (d < a.n_df) a.cbase[d] = run + pre + inc - nc;
+        run += tot;
+        __syncthreads();
+    }
+    if (tid == 0) a.cbase[a.n_df] = run;
+}
+
+__global__ __launch_bounds__(256) void rq_rc_clear(RpArgs a)
+{
+    const int64_t n = a.n_df * RC_HT;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+        a.ht_keys[i] = RP_EMPTY_KEY;
+}
+
+// the chunk of this block: df d, rows [c0, c1); false if the block has none
+__device__ __forceinline__ bool rc_chunk(const RpArgs& a, int64_t& d, int64_t& r0, int64_t& r1, int64_t& c0,
+                                         int64_t& c1)
+{
+    const int64_t c = blockIdx.x;
+    if (c >= a.cbase[a.n_df]) return false;
+    d = rc_df_of_chunk(a, c);
+    r0 = df_begin(a, d);
+    r1 = df_end(a, d);
+    c0 = r0 + (c - a.cbase[d]) * RC_L;
+    c1 = c0 + RC_L < r1 ? c0 + RC_L : r1;
+    return true;
+}
+
+__global__ __launch_bounds__(1024) void rq_rc_hash(RpArgs a)
+{
+    int64_t d, r0, r1, c0, c1;
+    if (!rc_chunk(a, d, r0, r1, c0, c1)) return;
+    RpInfo* inf = a.info + d;
+    if (inf->flags & RC_SKIP) return;
+    unsigned long long* keys = reinterpret_cast<unsigned long long*>(a.ht_keys + d * RC_HT);
+    for (int64_t i = c0 + threadIdx.x; i < c1; i += 1024) {
+        const uint64_t k = (uint64_t)a.sink[i];
+        if (k == RP_EMPTY_KEY) {
+            atomicOr(&inf->flags, RP_CSKIP);
+            continue;
+        }
+        uint32_t h = rp_hash(k, RC_HBITS);
+        bool done = false;
+        for (int p = 0; p < RC_HT && !done; ++p) {
+            const unsigned long long cur = keys[h];   // a stale EMPTY is settled by the CAS
+            if (cur == k) {
+                done = true;
+            } else if (cur == RP_EMPTY_KEY) {
+                const unsigned long long old = atomicCAS(&keys[h], (unsigned long long)RP_EMPTY_KEY,
+                                                         (unsigned long long)k);
+                if (old == RP_EMPTY_KEY) atomicAdd(&inf->S, 1);
+                done = old == RP_EMPTY_KEY || old == k;
+            }
+            if (!done) h = (h + 1) & (RC_HT - 1);
+        }
+        if (!done) atomicOr(&inf->flags, RP_CSKIP);   // table full: > RC_HT unique sinks
+    }
+}
+
+__global__ __launch_bounds__(1024) void rq_rc_dense(RpArgs a)
+{
+    __shared__ int wtot[16];
+    const int64_t d = blockIdx.x;
+    RpInfo* inf = a.info + d;
+    if (inf->flags & RC_SKIP) return;
+    if (inf->S > RC_S) {
+        if (threadIdx.x == 0) atomicOr(&inf->flags, RP_CSKIP);
+        return;
+    }
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint64_t* keys = a.ht_keys + d * RC_HT;
+    int* dense = a.ht_dense + d * RC_HT;
+    constexpr int PER = RC_HT / 1024;
+    int occ[PER], m = 0;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        occ[u] = keys[tid * PER + u] != RP_EMPTY_KEY;
+        m += occ[u];
+    }
+    const int inc = (int)wave_scan_add((uint32_t)m);
+    if (lane == 63) wtot[w] = inc;
+    __syncthreads();
+    int pre = 0;
+    for (int k = 0; k < w; ++k) pre += wtot[k];
+    int at = pre + inc - m;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        dense[tid * PER + u] = occ[u] ? at : -1;
+        at += occ[u];
+    }
+}
+
+constexpr int RC_PER = RC_L / 1024;   // rows per thread in rq_rc_sum
+
+__global__ __launch_bounds__(1024) void rq_rc_sum(RpArgs a)
+{
+    extern __shared__ int rc_sum_smem[];   // 4 x RC_S ints
+    int* n_ = rc_sum_smem;
+    int* lown = n_ + RC_S;
+    int* lrow = lown + RC_S;
+    int* aft = lrow + RC_S;
+    __shared__ int red[4][16];
+    int64_t d, r0, r1, c0, c1;
+    if (!rc_chunk(a, d, r0, r1, c0, c1)) return;
+    RpInfo* inf = a.info + d;
+    if (inf->flags & RC_SKIP) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int S = inf->S;
+    const uint64_t* hk = a.ht_keys + d * RC_HT;
+    const int* hd = a.ht_dense + d * RC_HT;
+    for (int s = tid; s < S; s += 1024) {
+        n_[s] = 0;
+        lown[s] = -1;
+        lrow[s] = -1;
+        aft[s] = 0;
+    }
+    __syncthreads();
+    int slot[RC_PER], li[RC_PER];
+    int starts = 0, ev_own = 0, ev_world = 0, unsorted = 0, eidbad = 0;
+    const bool has_eid = a.eid != nullptr;
+#pragma unroll
+    for (int u = 0; u < RC_PER; ++u) {
+        li[u] = u * 1024 + tid;
+        const int64_t i = c0 + li[u];
+        slot[u] = -1;
+        if (i < c1) {
+            const double t = a.t[i];
+            const bool own = a.src[i] == a.src_id;
+            slot[u] = rc_dense(hk, hd, (uint64_t)a.sink[i]);
+            atomicAdd(&n_[slot[u]], 1);
+            atomicMax(&lrow[slot[u]], li[u]);
+            if (own) atomicMax(&lown[slot[u]], li[u]);
+            if (i == r0) {
+                starts += 1;
+            } else {
+                const double tp = a.t[i - 1];
+                starts += t != tp;
+                unsorted |= t < tp;
+            }
+            if (has_eid) {
+                const int64_t e = a.eid[i];
+                bool fe = true;
+                if (i > r0) {
+                    const int64_t ep = a.eid[i - 1];
+                    fe = e != ep;
+                    eidbad |= e < ep;
+                }
+                ev_own += fe && own;
+                ev_world += fe && !own;
+            }
+        }
+    }
+    // chunk totals (one atomic per quantity and block)
+    const uint32_t s0 = wave_sum_u32((uint32_t)starts), s1 = wave_sum_u32((uint32_t)ev_own),
+                   s2 = wave_sum_u32((uint32_t)ev_world);
+    const uint64_t fu = __ballot(unsorted), fe = __ballot(eidbad);
+    if (lane == 0) {
+        red[0][w] = (int)s0;
+        red[1][w] = (int)s1;
+        red[2][w] = (int)s2;
+        red[3][w] = (fu ? 1 : 0) | (fe ? 2 : 0);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int t0 = 0, t1 = 0, t2 = 0, f = 0;
+        for (int k = 0; k < 16; ++k) {
+            t0 += red[0][k];
+            t1 += red[1][k];
+            t2 += red[2][k];
+            f |= red[3][k];
+        }
+        a.gstart[blockIdx.x] = t0;
+        if (t1) atomicAdd(reinterpret_cast<unsigned long long*>(&inf->n_own), (unsigned long long)t1);
+        if (t2) atomicAdd(reinterpret_cast<unsigned long long*>(&inf->n_world), (unsigned long long)t2);
+        if (f & 1) atomicOr(&inf->flags, RP_UNSORTED);
+        if (f & 2) atomicOr(&inf->flags, RP_EIDBAD);
+    }
+    // rows after each sink's last own row
+#pragma unroll
+    for (int u = 0; u < RC_PER; ++u)
+        if (slot[u] >= 0 && lown[slot[u]] >= 0 && li[u] > lown[slot[u]]) atomicAdd(&aft[slot[u]], 1);
+    __syncthreads();
+    RcCarry* out = a.carry + (int64_t)blockIdx.x * RC_S;
+    for (int s = tid; s < S; s += 1024) {
+        RcCarry cr;
+        cr.n = n_[s];
+        cr.after = lown[s] >= 0 ? aft[s] : -1;
+        cr.last_t = cr.n > 0 ? a.t[c0 + lrow[s]] : 0.0;
+        out[s] = cr;
+    }
+}
+
+// a chunk's function on a sink's rank: CONST (an own row: r -> val) or SHIFT (r -> max(r, 0)
+// + val for val > 0, identity for val = 0); has: the chunk has rows of the sink (last t lt)
+struct RcFn {
+    int isconst, val, has;
+    double lt;
+};
+__device__ __forceinline__ RcFn rc_compose(const RcFn& later, const RcFn& earlier)
+{
+    RcFn o;
+    if (later.isconst) return later;
+    o.isconst = earlier.isconst;
+    o.val = earlier.val + later.val;
+    o.has = earlier.has | later.has;
+    o.lt = later.has ? later.lt : earlier.lt;
+    return o;
+}
+__device__ __forceinline__ RcFn rc_shfl_up(const RcFn& f, int off)
+{
+    RcFn g;
+    g.isconst = __shfl_up(f.isconst, off, 64);
+    g.val = __shfl_up(f.val, off, 64);
+    g.has = __shfl_up(f.has, off, 64);
+    g.lt = __shfl_up(f.lt, off, 64);
+    return g;
+}
+__device__ __forceinline__ RcFn rc_shfl(const RcFn& f, int l)
+{
+    RcFn g;
+    g.isconst = __shfl(f.isconst, l, 64);
+    g.val = __shfl(f.val, l, 64);
+    g.has = __shfl(f.has, l, 64);
+    g.lt = __shfl(f.lt, l, 64);
+    return g;
+}
+
+// grid (n_df, RC_S / 16) x 1024: wave w of block (d, y) scans sink 16 y + w of df d
+__global__ __launch_bounds__(1024) void rq_rc_scan(RpArgs a)
+{
+    const int64_t d = blockIdx.x;
+    RpInfo* inf = a.info + d;
+    if (inf->flags & RC_SKIP) return;
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    const int64_t cb = a.cbase[d], nch = a.cbase[d + 1] - cb;
+    if (blockIdx.y == 0 && w == 0) {   // the t-group base of every chunk
+        int64_t run = 0;
+        for (int64_t k0 = 0; k0 < nch; k0 += 64) {
+            const int64_t k = k0 + lane;
+            const int g = k < nch ? a.gstart[cb + k] : 0;
+            const int inc = (int)wave_scan_add((uint32_t)g);
+            if (k < nch) a.gbase[cb + k] = run + inc - g;
+            run += (int64_t)__shfl(inc, 63, 64);
+        }
+        if (lane == 0) inf->n_piv = run;
+    }
+    const int s = (int)blockIdx.y * 16 + w;
+    if (s >= inf->S) return;
+    RcFn P{0, 0, 0, 0.0};   // the chunks before this group, composed
+    for (int64_t k0 = 0; k0 < nch; k0 += 64) {
+        const int64_t k = k0 + lane;
+        RcFn f{0, 0, 0, 0.0};
+        if (k < nch) {
+            const RcCarry cr = a.carry[(cb + k) * RC_S + s];
+            f.isconst = cr.after >= 0;
+            f.val = f.isconst ? cr.after : cr.n;
+            f.has = cr.n > 0;
+            f.lt = cr.last_t;
+        }
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const RcFn g = rc_shfl_up(f, off);
+            if (lane >= off) f = rc_compose(f, g);
+        }
+        RcFn ex = rc_shfl_up(f, 1);
+        if (lane == 0) ex = RcFn{0, 0, 0, 0.0};
+        const RcFn e = rc_compose(ex, P);
+        if (k < nch) {
+            RcState st;
+            st.r = e.isconst ? e.val : (e.val > 0 ? e.val : -1);
+            st.pad = 0;
+            st.last_t = e.lt;
+            a.state[(cb + k) * RC_S + s] = st;
+        }
+        P = rc_compose(rc_shfl(f, 63), P);
+    }
+}
+
+template <int NK>
+__global__ __launch_bounds__(RP_B) void rq_rc_apply(RpArgs a)
+{
+    int64_t d, r0, r1, c0, c1;
+    if (!rc_chunk(a, d, r0, r1, c0, c1)) return;
+    RpInfo* inf = a.info + d;
+    if (inf->flags & (RC_SKIP | RP_UNSORTED)) return;
+    const int64_t c = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int S = inf->S;
+    const uint64_t* hk = a.ht_keys + d * RC_HT;
+    const int* hd = a.ht_dense + d * RC_HT;
+
+    extern __shared__ __align__(16) unsigned char rc_smem[];
+    unsigned char* sp = rc_smem;
+    auto carve = [&](size_t bytes) {
+        unsigned char* p = sp;
+        sp += (bytes + 15) & ~(size_t)15;
+        return p;
+    };
+    double* tb = reinterpret_cast<double*>(carve(8 * (RP_B + 2)));       // [0] prev, [1+i], [RP_B+1] next
+    int* gb = reinterpret_cast<int*>(carve(4 * RP_B));                    // t-group of row i
+    unsigned char* ob = carve(RP_B);                                      // own flag of row i
+    int* lst = reinterpret_cast<int*>(carve(4 * RP_B));                   // sink buckets: rows
+    int64_t* wsum = reinterpret_cast<int64_t*>(carve(8 * 16));            // wave totals (int64)
+    int* ws32 = reinterpret_cast<int*>(carve(4 * 16 * (NK + 6)));         // wave totals (int)
+    int* misc = reinterpret_cast<int*>(carve(4 * 16));                    // [2] dup, [8] bucket allocator
+    RpSlot* tst = reinterpret_cast<RpSlot*>(carve(sizeof(RpSlot) * RC_S));
+
+    int km1[NK];
+#pragma unroll
+    for (int q = 0; q < NK; ++q) km1[q] = a.Ks[q] - 1;
+
+    // every sink's state entering the chunk, and the pivot row it sums to
+    const RcState* stin = a.state + c * RC_S;
+    const double t_bnd = c0 > r0 ? a.t[c0 - 1] : 0.0;
+    const bool spans = c0 > r0 && a.t[c0] == t_bnd;   // the chunk continues the previous t-group
+    const int64_t G0 = a.gbase[c];
+    int64_t ps = 0;
+    int pv = 0, pc[NK];
+#pragma unroll
+    for (int q = 0; q < NK; ++q) pc[q] = 0;
+    for (int s = tid; s < S; s += RP_B) {
+        const RcState e = stin[s];
+        if (e.r >= 0) {
+            // cnt = r + 1, lastown = 1: the next row's rank is r + 1; a cell in the
+            // spanning t-group keeps its group (a second row there is a pivot mean)
+            tst[s] = RpSlot{e.r + 1, 1, (spans && e.last_t == t_bnd) ? (int)(G0 - 1) : -1, 0};
+            ps += e.r;
+            pv += 1;
+#pragma unroll
+            for (int q = 0; q < NK; ++q) pc[q] += e.r <= km1[q] ? 1 : 0;
+        } else {
+            tst[s] = RpSlot{0, 0, -1, 0};
+        }
+    }
+    if (tid < 16) misc[tid] = 0;
+    {
+        int64_t s64 = ps;   // this wave's sum (int64 butterfly)
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) s64 += __shfl_xor(s64, o, 64);
+        const int sv = scan_add_i32(pv);
+        if (lane == 63) {
+            wsum[w] = s64;
+            ws32[80 + w] = sv;
+        }
+#pragma unroll
+        for (int q = 0; q < NK; ++q) {
+            const int sq = scan_add_i32(pc[q]);
+            if (lane == 63) ws32[96 + 16 * q + w] = sq;
+        }
+    }
+    __syncthreads();
+    RpAcc<NK> carry;
+    {
+        int64_t pre64;
+        int pre;
+        totals_add(wsum, w, pre64, carry.s);
+        totals_add(ws32 + 80, w, pre, carry.v);
+#pragma unroll
+        for (int q = 0; q < NK; ++q) totals_add(ws32 + 96 + 16 * q, w, pre, carry.c[q]);
+    }
+    int64_t Gc = G0;
+    __syncthreads();   // totals read before the batch loop reuses them
+
+    bool own_c = false;
+    int slot_c = 0;
+    auto prep = [&](int64_t nb0, double t_, int64_t s_, int64_t k_, double t_after, double t_before) {
+        const bool v = nb0 + tid < c1;
+        tb[1 + tid] = v ? t_ : 0.0;
+        if (tid == 0) {
+            tb[0] = t_before;
+            tb[RP_B + 1] = t_after;
+        }
+        own_c = v && s_ == a.src_id;
+        slot_c = v ? rc_dense(hk, hd, (uint64_t)k_) : 0;
+    };
+    {
+        const int64_t i0 = c0 + tid;
+        double t0 = 0.0, ta = 0.0;
+        int64_t s0 = 0, k0 = 0;
+        if (i0 < c1) {
+            t0 = a.t[i0];
+            s0 = a.src[i0];
+            k0 = a.sink[i0];
+        }
+        if (tid == 0 && c0 + RP_B < r1) ta = a.t[c0 + RP_B];
+        prep(c0, t0, s0, k0, ta, t_bnd);
+    }
+
+    for (int64_t b0 = c0; b0 < c1; b0 += RP_B) {
+        const int64_t i = b0 + tid;
+        const bool valid = i < c1;
+        const bool has_next = b0 + RP_B < c1;
+        const int64_t in = i + RP_B;
+        double tn = 0.0, tnn = 0.0;
+        int64_t sn = 0, kn = 0;
+        if (has_next && in < c1) {
+            tn = a.t[in];
+            sn = a.src[in];
+            kn = a.sink[in];
+        }
+        if (tid == 0 && b0 + 2 * RP_B < r1) tnn = a.t[b0 + 2 * RP_B];
+
+        // ---- A: neighbours of every row; its ticket in its sink's bucket ----
+        __syncthreads();
+        const int last = (int)((c1 - b0) < RP_B ? (c1 - b0) : RP_B);
+        const double ti = tb[1 + tid];
+        const double t_prev = tb[tid], t_next = tb[tid + 2];
+        const double t_last = tb[last];
+        const bool first_row = i == r0;
+        const bool start = valid && (first_row || ti != t_prev);
+        const bool endg = valid && (i == r1 - 1 || t_next != ti);
+        const bool own = own_c;
+        RpSlot* sl = tst + slot_c;
+        const int ticket = valid ? atomicAdd(&sl->bucket, 1) : 0;
+        ob[tid] = own ? 1 : 0;
+
+        // ---- B: t-group of every row (block scan of group starts); list space ----
+        const int st_incl = scan_add_i32((int)start);
+        if (lane == 63) ws32[w] = st_incl;
+        __syncthreads();
+        int st_pre, st_tot;
+        totals_add(ws32, w, st_pre, st_tot);
+        const int64_t G = Gc + (int64_t)(st_pre + st_incl) - 1;
+        gb[tid] = (int)G;
+        const RpSlot st0 = valid ? *sl : RpSlot{0, 0, -1, 0};
+        const int m = valid ? (st0.bucket & 0xFFF) : 0;
+        if (valid && m > 1 && ticket == 0) sl->bucket = (atomicAdd(&misc[8], m) << 12) | m;
+        __syncthreads();
+
+        // ---- C: my place among my sink's rows in this batch ----
+        int boff = 0;
+        if (valid && m > 1) {
+            boff = sl->bucket >> 12;
+            lst[boff + ticket] = tid;
+        }
+        __syncthreads();
+        int j = 0, pred = -1, own_le = own ? tid : -1, own_lt = -1;
+        if (valid && m > 1) {
+            for (int k = 0; k < m; ++k) {
+                const int y = lst[boff + k];
+                if (y < tid) {
+                    ++j;
+                    pred = pred > y ? pred : y;
+                    if (ob[y]) {
+                        own_lt = own_lt > y ? own_lt : y;
+                        own_le = own_le > y ? own_le : y;
+                    }
+                }
+            }
+        }
+        int j_le = 0, j_lt = 0;
+        if (valid && m > 1 && (own_le >= 0 || own_lt >= 0)) {
+            for (int k = 0; k < m; ++k) {
+                const int y = lst[boff + k];
+                j_le += y < own_le;
+                j_lt += y < own_lt;
+            }
+        } else if (own_le >= 0) {
+            j_le = j;
+        }
+        RpAcc<NK> x;
+        x.s = 0;
+        x.v = 0;
+#pragma unroll
+        for (int q = 0; q < NK; ++q) x.c[q] = 0;
+        if (valid) {
+            const int pos = st0.cnt + j + 1;
+            const int lastown = own_le >= 0 ? st0.cnt + j_le + 1 : st0.lastown;
+            const int rank = pos - lastown;
+            int prevrank, prevg;
+            if (j > 0) {
+                prevrank = (pos - 1) - (own_lt >= 0 ? st0.cnt + j_lt + 1 : st0.lastown);
+                prevg = gb[pred];
+            } else {
+                prevrank = st0.cnt > 0 ? st0.cnt - st0.lastown : -1;
+                prevg = st0.lastgroup;
+            }
+            if (prevg == (int)G) misc[2] = 1;   // two rows of one sink at one t: a pivot mean
+            const bool pnan = prevrank < 0;
+            x.s = rank - (pnan ? 0 : prevrank);
+            x.v = pnan ? 1 : 0;
+#pragma unroll
+            for (int q = 0; q < NK; ++q)
+                x.c[q] = (rank <= km1[q] ? 1 : 0) - ((!pnan && prevrank <= km1[q]) ? 1 : 0);
+            if (j == m - 1) {
+                sl->cnt = pos;
+                sl->lastown = lastown;
+                sl->lastgroup = (int)G;
+                sl->bucket = 0;
+            }
+        }
+        if (has_next) prep(b0 + RP_B, tn, sn, kn, tnn, t_last);
+
+        // ---- D: running totals in row order; the last row of a t-group emits its pivot row ----
+        x.s = scan_add_i64_of_i32((int)x.s);
+        x.v = scan_add_i32(x.v);
+#pragma unroll
+        for (int q = 0; q < NK; ++q) x.c[q] = scan_add_i32(x.c[q]);
+        if (lane == 63) {
+            wsum[w] = x.s;
+            ws32[80 + w] = x.v;
+#pragma unroll
+            for (int q = 0; q < NK; ++q) ws32[96 + 16 * q + w] = x.c[q];
+        }
+        __syncthreads();
+        RpAcc<NK> pre, tot;
+        totals_add(wsum, w, pre.s, tot.s);
+        totals_add(ws32 + 80, w, pre.v, tot.v);
+#pragma unroll
+        for (int q = 0; q < NK; ++q) totals_add(ws32 + 96 + 16 * q, w, pre.c[q], tot.c[q]);
+        if (endg) {
+            const int64_t row = r0 + G;
+            a.rows_dt[row] = (i == r1 - 1 ? a.end : t_next) - ti;
+            a.rows_sum[row] = (double)(carry.s + pre.s + x.s);
+            a.rows_valid[row] = (uint32_t)(carry.v + pre.v + x.v);
+#pragma unroll
+            for (int q = 0; q < NK; ++q) a.rows_cnt[row * NK + q] = (uint32_t)(carry.c[q] + pre.c[q] + x.c[q]);
+        }
+        carry.s += tot.s;
+        carry.v += tot.v;
+#pragma unroll
+        for (int q = 0; q < NK; ++q) carry.c[q] += tot.c[q];
+        Gc += st_tot;
+        if (tid == 0) misc[8] = 0;   // bucket allocator (read in B, two barriers ago)
+    }
+    __syncthreads();
+    if (tid == 0 && misc[2]) atomicOr(&inf->flags, RP_FALLBACK);
+}
+
+// unique sink ids of the chunked dataframes with a pivot mean (rq_rp_keys sorts them)
+__global__ __launch_bounds__(1024) void rq_rc_keys(RpArgs a)
+{
+    const int64_t d = blockIdx.x;
+    const RpInfo* inf = a.info + d;
+    const int fl = inf->flags;
+    if (!(fl & RP_FALLBACK) || (fl & (RC_SKIP | RP_UNSORTED))) return;
+    const int64_t r0 = df_begin(a, d);
+    const uint64_t* hk = a.ht_keys + d * RC_HT;
+    const int* hd = a.ht_dense + d * RC_HT;
+    for (int h = threadIdx.x; h < RC_HT; h += 1024)
+        if (hk[h] != RP_EMPTY_KEY) a.keys[r0 + hd[h]] = (int64_t)hk[h];
+}
+
+// ============================================================================
 // rq_rp_scan: numpy-order integrals over each dataframe's pivot rows
 // (one wavefront per dataframe) and the per-dataframe outputs
 // ============================================================================
@@ -917,6 +1507,13 @@ size_t rp_fast_lds(int nK)
     return s;
 }
 
+size_t rc_apply_lds(int nK)
+{
+    auto al = [](size_t b) { return (b + 15) & ~(size_t)15; };
+    return al(8 * (RP_B + 2)) + al(4 * RP_B) + al(RP_B) + al(4 * RP_B) + al(8 * 16) + al(4 * 16 * (nK + 6)) +
+           al(4 * 16) + al(sizeof(RpSlot) * RC_S);
+}
+
 template <int NK>
 hipError_t rp_launch_t(const RpArgs& a, int phase, hipStream_t s)
 {
@@ -938,6 +1535,20 @@ hipError_t rp_launch_t(const RpArgs& a, int phase, hipStream_t s)
     case RP_PHASE_SEQ: {
         const size_t lds = npsum_lds_doubles<1>() * sizeof(double) + RP_SEQ_LDS;
         hipLaunchKernelGGL((rq_rp_seq<NK>), dim3(nd), dim3(64), lds, s, a);
+        break;
+    }
+    case RP_PHASE_CHUNK: {
+        const unsigned mc = (unsigned)a.max_chunks;
+        hipLaunchKernelGGL(rq_rc_plan, dim3(1), dim3(1024), 0, s, a);
+        const unsigned cl = (unsigned)std::min<int64_t>(1024, (a.n_df * RC_HT + 255) / 256);
+        hipLaunchKernelGGL(rq_rc_clear, dim3(cl), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(rq_rc_hash, dim3(mc), dim3(1024), 0, s, a);
+        hipLaunchKernelGGL(rq_rc_dense, dim3(nd), dim3(1024), 0, s, a);
+        hipLaunchKernelGGL(rq_rc_sum, dim3(mc), dim3(1024), 4 * RC_S * sizeof(int), s, a);
+        hipLaunchKernelGGL(rq_rc_scan, dim3(nd, RC_S / 16), dim3(1024), 0, s, a);
+        const size_t lds = rc_apply_lds(NK);
+        hipLaunchKernelGGL((rq_rc_apply<NK>), dim3(mc), dim3(RP_B), lds, s, a);
+        hipLaunchKernelGGL(rq_rc_keys, dim3(nd), dim3(1024), 0, s, a);
         break;
     }
     default: {

@@ -84,7 +84,8 @@ def grid_means(rows, n_grid, n_rep):
     by the shape and device, so the result depends only on the gathered rows --
     bit-identical on every rank and however the replicas were sharded."""
     x = rows.reshape(n_grid, n_rep, -1).to(torch.float64)
-    return x.sum(1) / n_rep
+    # divide by a tensor: torch's tensor / python-scalar multiplies by the reciprocal
+    return x.sum(1) / torch.full((), float(n_rep), dtype=torch.float64, device=x.device)
 
 
 def run_sharded(graph, n_grid, n_rep, world=None, rank=None, group=None, **run_kw):

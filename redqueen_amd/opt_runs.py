@@ -173,9 +173,11 @@ def _opt_poisson_batches(worlds, qs, seeds, num_segments):
     u_t = torch.as_tensor(np.tile(us, len(qv)))
     ro = g.run("opt", q=qv, s=g.s_matrix(base.s, len(qv)), n_rep=N, ctrl_seed=seed_t,
                world_seed=u_t, randomize=True, Ks=Ks, event_log=True)
-    posts = ro.num_events.double()
+    # capacity / end_time as create_manager_with_poisson divides (host IEEE division;
+    # torch's tensor / scalar multiplies by the reciprocal)
+    rate = ro.num_events.cpu().numpy().astype(np.float64) / float(base.end_time)
     rp = g.run("poisson", n_rep=len(qv) * N, ctrl_seed=seed_t, world_seed=u_t, randomize=True,
-               ctrl_rate=posts / float(base.end_time), Ks=Ks)
+               ctrl_rate=torch.as_tensor(rate), Ks=Ks)
     ro_m, ro_c = ro.metrics.cpu().numpy(), ro.counts.cpu().numpy()
     rp_m, rp_c = rp.metrics.cpu().numpy(), rp.counts.cpu().numpy()
     row_off, cols = ro.log_columns()

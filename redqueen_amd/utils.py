@@ -60,13 +60,15 @@ def torch_empty_u8(n, dev):
     return torch.empty(max(256, int(n)), dtype=torch.uint8, device=dev)
 
 
-def replay_columns(t, src, sink, eid=None, df_off=None, src_id=0, end_time=0.0, Ks=(1,)):
+def replay_columns(t, src, sink, eid=None, df_off=None, src_id=0, end_time=0.0, Ks=(1,), chunked=None):
     """rq_metrics_replay(_batch) on device columns (torch tensors: t f64, src / sink /
     event_id i64, df_off i64 [n_df + 1] or None for one dataframe).  Sink ids are raw:
     the pivot columns are built on the device.  Returns (metrics [n_df, nK + 2],
     counts [n_df, 4]) device tensors; counts[:, 2] < 0 flags a rejected dataframe
     (RQ_EUNSORTED).  Dataframes wider than the LDS tables are rerun with the large
-    workspace, as the engine reruns overflowing replicas."""
+    workspace, as the engine reruns overflowing replicas.  ``chunked``: None = give
+    few long dataframes the chunked (many-workgroup) replay's workspace; True / False
+    = always / never (A/B; the library then picks the path, env RQ_RP_CHUNK forces it)."""
     import torch
     from . import _lib as L
     dev = t.device
@@ -77,7 +79,11 @@ def replay_columns(t, src, sink, eid=None, df_off=None, src_id=0, end_time=0.0, 
     cnt = torch.empty((n_df, 4), dtype=torch.int64, device=dev)
     st = torch.cuda.current_stream().cuda_stream
     lib = L.lib()
-    for flags in (0, L.REPLAY_LARGE):
+    # few long dataframes: room for the chunked (many-workgroup) replay
+    if chunked is None:
+        chunked = n_df <= 64 and n >= 2 * L.REPLAY_CHUNK_ROWS * n_df
+    f0 = L.REPLAY_CHUNKED if chunked else 0
+    for flags in (f0, f0 | L.REPLAY_LARGE):
         nbytes = C.c_size_t()
         L.check("rq_replay_workspace_size",
                 lib.rq_replay_workspace_size(n, n_df, Ks.size, flags, C.byref(nbytes)))
