@@ -97,7 +97,7 @@ def replay_columns(t, src, sink, eid=None, df_off=None, src_id=0, end_time=0.0, 
         else:
             L.check("rq_metrics_replay_batch",
                     lib.rq_metrics_replay_batch(*args, df_off.data_ptr(), n_df, n, *tail))
-        if flags or not bool((cnt[:, 2] == L.RQ_EOVERFLOW).any().item()):
+        if (flags & L.REPLAY_LARGE) or not bool((cnt[:, 2] == L.RQ_EOVERFLOW).any().item()):
             break
     return out, cnt
 
