@@ -99,10 +99,33 @@ def main():
                     "GBps": per_row * nrow / (ms[3] + ms[2]) / 1e6,
                     "frac": per_row * nrow / (ms[3] + ms[2]) / 1e6 / PEAK,
                     "equal_to_sweep": bool(torch.equal(m4, r2.metrics))}
+    # the same batch through the chunked (many-workgroup) path, forced (A/B)
+    os.environ["RQ_RP_CHUNK"] = "1"
+    (m4, c4), ms, wall = timed(lambda: utils.replay_columns(
+        cols["t"], cols["src_id"], cols["sink_id"], cols["event_id"], off, so["src_id"], so["end_time"],
+        (1,), chunked=True), a.reps)
+    del os.environ["RQ_RP_CHUNK"]
+    res["replay_batch_eid_chunked"] = {"dataframes": R2, "rows": nrow, "ms_replay": ms[3], "ms_scan": ms[2],
+                                       "GBps": 32 * nrow / (ms[3] + ms[2]) / 1e6,
+                                       "equal_to_sweep": bool(torch.equal(m4, r2.metrics))}
+    # ONE dataframe (device columns): the chunked path (default for a long df) and the
+    # one-workgroup path; and through the pandas facade (host -> device copies included)
+    a0, a1 = int(ro[0]), int(ro[1])
+    one = {k: v[a0:a1].contiguous() for k, v in cols.items()}
+    for tag, ck in (("replay_one_df", None), ("replay_one_df_one_workgroup", False)):
+        if ck is False:
+            os.environ["RQ_RP_CHUNK"] = "0"
+        (m5, c5), ms, wall = timed(lambda: utils.replay_columns(
+            one["t"], one["src_id"], one["sink_id"], one["event_id"], None, so["src_id"], so["end_time"],
+            (1,), chunked=ck), a.reps)
+        os.environ.pop("RQ_RP_CHUNK", None)
+        res[tag] = {"rows": a1 - a0, "ms_replay": ms[3], "ms_scan": ms[2], "ms": ms[3] + ms[2],
+                    "wall_ms": wall * 1e3, "GBps": 32 * (a1 - a0) / (ms[3] + ms[2]) / 1e6,
+                    "equal_to_sweep": bool(torch.equal(m5[0], r2.metrics[0]))}
     df = r2.dataframe(0)
     _, ms, wall = timed(lambda: utils.replay_metrics(df, so["src_id"], so["end_time"], (1,)), a.reps)
-    res["replay_one_df"] = {"rows": len(df), "ms": ms[3] + ms[2], "wall_ms": wall * 1e3,
-                            "GBps": 32 * len(df) / (ms[3] + ms[2]) / 1e6}
+    res["replay_one_df_facade"] = {"rows": len(df), "ms": ms[3] + ms[2], "wall_ms": wall * 1e3,
+                                   "GBps": 32 * len(df) / (ms[3] + ms[2]) / 1e6}
 
     # 5. oracle DP
     rs = np.random.RandomState(0)
