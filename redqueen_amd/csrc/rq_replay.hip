@@ -52,9 +52,13 @@ using namespace rq;
 
 namespace {
 
-constexpr int RP_B = 1024;              // rows per batch = threads per workgroup
-constexpr int RP_H = 4096;              // LDS hash slots
-constexpr int RP_LOG_H = 12;
+#ifndef RQ_RP_B
+#define RQ_RP_B 1024
+#endif
+constexpr int RP_B = RQ_RP_B;           // rows per batch = threads per workgroup
+constexpr int RP_W = RP_B / 64;         // waves per workgroup
+constexpr int RP_H = 4 * RP_B;          // LDS hash slots
+constexpr int RP_LOG_H = RP_B == 1024 ? 12 : RP_B == 512 ? 11 : 10;
 constexpr int RP_HMAX = RP_H - RP_B - 1;   // unique sinks the LDS table takes: a batch can
                                            // insert RP_B more and still leave an empty slot
 constexpr uint64_t RP_EMPTY_KEY = 0x8000000000000000ull;   // INT64_MIN: gets its own slot
@@ -150,9 +154,9 @@ __device__ __forceinline__ int64_t lane_bcast(int64_t v, int l) { return bcast_i
 template <class T>
 __device__ __forceinline__ void totals_add(const T* t, int w, T& pre, T& tot)
 {
-    T x = lane_id() < 16 ? t[lane_id()] : (T)0;
+    T x = lane_id() < RP_W ? t[lane_id()] : (T)0;
     x = row_scan_add(x);
-    tot = lane_bcast(x, 15);
+    tot = lane_bcast(x, RP_W - 1);
     pre = w > 0 ? lane_bcast(x, w - 1) : (T)0;
 }
 template <int NK>
