@@ -115,6 +115,15 @@ def c5():
                            kinds=("Hawkes",), world_rate=0.5, alpha=1.0, beta=2.0)
 
 
+def g120():
+    """A > 64-source world (the general sweep's instances, like C5) small enough for the
+    reference to run thousands of replicas: 60 followers, 120 broadcasters (Poisson2
+    rate 0.5 / Hawkes l_0 0.5, alpha 1, beta 4), degree 4, T = 20 (the trim keeps the
+    broadcasters that reach a follower)."""
+    return followers_graph(num_followers=60, num_sources=120, degree=4, end_time=20.0,
+                           world_rate=0.5, alpha=1.0, beta=4.0)
+
+
 C4_S = [(1.0, 1.0), (0.5, 1.5), (1.5, 0.5), (1.0, 0.25)]
 
 

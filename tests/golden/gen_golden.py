@@ -25,6 +25,8 @@ installed and there is no network) and records, as plain data:
                    returned q and calc_q_capacity_iter per (q, seed);
                    rank_of_src_in_df tables and u_int_opt values
   dist_c3.npz      (--c3-dist N) N-replica RedQueen ensemble on the C3 bench network
+  dist_g120.npz    (--g120-dist N) N-replica RedQueen ensemble on graphs.g120 (> 64
+                   sources: the general sweep's instances)
   dist_sig.npz     (--sig-dist N) N-replica OptPWSignificance ensemble (K3 network,
                    24-segment follower significance, randomized worlds)
   realdata.npz     all-RealData worlds (create_manager_with_times): the reference's whole
@@ -622,6 +624,31 @@ def gen_c3_dist(n, start=0, procs=0):
                         seed_stride=np.asarray([C3_SEED_STRIDE]))
 
 
+G120_SEED_STRIDE = 20000   # > 99 x the broadcaster count: no shared streams
+
+
+def _g120_worker(r):
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from redqueen_amd import graphs as G
+    so = SimOpts(**G.g120())
+    u = G120_SEED_STRIDE * r
+    m = so.randomize_other_sources(u).create_manager_with_opt(seed=u)
+    m.run_dynamic()
+    df = m.state.get_dataframe()
+    met, own, world = metrics(df, so)
+    return np.concatenate([[own, world, m.state.get_num_events()], met])
+
+
+def gen_g120_dist(n, procs=0):
+    """graphs.g120 (> 64 sources: the general sweep) through the reference itself:
+    replica r runs world randomize_other_sources(20000 r), RedQueen seed 20000 r."""
+    with mp.Pool(procs or os.cpu_count()) as pool:
+        res = np.asarray(pool.map(_g120_worker, range(n), chunksize=4))
+    cols = ["posts", "world", "events"] + ["top%d" % k for k in KS] + ["avg", "r2"]
+    np.savez_compressed(os.path.join(HERE, "dist_g120.npz"), data=res, cols=np.asarray(cols),
+                        seed_stride=np.asarray([G120_SEED_STRIDE]))
+
+
 # ---------------------------------------------------------------- ensembles
 def _c2_worker(r):
     so = SimOpts(**README)
@@ -715,12 +742,17 @@ if __name__ == "__main__":
     ap.add_argument("--c3-dist", type=int, default=0, help="only dist_c3.npz with N replicas")
     ap.add_argument("--c3-start", type=int, default=0, help="append to dist_c3.npz from this replica")
     ap.add_argument("--procs", type=int, default=0)
+    ap.add_argument("--g120-dist", type=int, default=0, help="only dist_g120.npz with N replicas")
     a = ap.parse_args()
     steps = {"npsum": gen_npsum, "draws": gen_draws, "readme": gen_readme, "kats": gen_kats,
              "adv": gen_adversarial, "graphs": gen_graphs, "frac": gen_frac,
              "oracle": gen_oracle, "sweepq": gen_sweepq, "sig": gen_sig, "realdata": gen_realdata,
              "plugin": gen_plugin, "errors": gen_errors}
-    if a.c3_dist:
+    if a.g120_dist:
+        gen_g120_dist(a.g120_dist, a.procs)
+        print("done g120 dist", flush=True)
+        a.worlds = True   # nothing else
+    elif a.c3_dist:
         gen_c3_dist(a.c3_dist, a.c3_start, a.procs)
         print("done c3 dist", flush=True)
         a.worlds = True   # nothing else

@@ -257,6 +257,25 @@ def test_engine_c3_matches_reference_distribution(golden):
         assert abs(z) < 2.576, (k, r.mean(), v.mean(), z)
 
 
+def test_engine_g120_matches_reference_distribution(golden):
+    """Engine semantics on a > 64-source world (graphs.g120: the general sweep's
+    instances) vs the reference's replicas of it (dist_g120.npz)."""
+    d = golden("dist_g120.npz")
+    cols = [str(c) for c in d["cols"]]
+    ref = {c: d["data"][:, i] for i, c in enumerate(cols)}
+    so = graphs.g120()
+    out, cnt, _ = O.engine_batch(O.Scenario(so, ("opt", 0)), 4096, 900000, True, KS, 8,
+                                 seed_stride=int(d["seed_stride"][0]))
+    eng = {"posts": cnt[:, 0], "world": cnt[:, 1], "events": cnt[:, 2], "avg": out[:, len(KS)],
+           "r2": out[:, len(KS) + 1]}
+    for i, k in enumerate(KS):
+        eng["top%d" % k] = out[:, i]
+    for k, v in eng.items():
+        r = ref[k]
+        z = (v.mean() - r.mean()) / math.sqrt(v.var() / len(v) + r.var() / len(r))
+        assert abs(z) < 2.576, (k, r.mean(), v.mean(), z)
+
+
 def test_realdata_worlds_both_restatements_exact(golden):
     """All-RealData worlds (create_manager_with_times): the reference restatement
     AND the engine-semantics restatement reproduce the reference's whole df -- event
