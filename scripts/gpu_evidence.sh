@@ -33,3 +33,11 @@ echo "c5 kt ok"
 timeout -k 10 300 python3 scripts/bench_paths.py --reps 5 > "$OUT/paths.json" 2> "$OUT/paths.err" || { echo "paths failed"; tail -5 "$OUT/paths.err"; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/pathskt" -o kt -- python3 scripts/bench_paths.py --reps 3 > "$OUT/pathskt.log" 2>&1 || { echo "paths kt failed"; tail -5 "$OUT/pathskt.log"; exit 1; }
 echo "paths ok"
+# HBM bytes of the secondary paths' kernels (replay, scan, log expand): FETCH / WRITE passes
+P="--output-format csv"
+timeout -k 10 -s KILL 300 rocprofv3 --pmc FETCH_SIZE $P -d "$OUT/pathsp3" -o p3 -- python3 scripts/bench_paths.py --reps 1 > "$OUT/pathsp3.log" 2>&1 || { echo "paths fetch failed"; tail -5 "$OUT/pathsp3.log"; exit 1; }
+timeout -k 10 -s KILL 300 rocprofv3 --pmc WRITE_SIZE $P -d "$OUT/pathsp4" -o p4 -- python3 scripts/bench_paths.py --reps 1 > "$OUT/pathsp4.log" 2>&1 || { echo "paths write failed"; tail -5 "$OUT/pathsp4.log"; exit 1; }
+mkdir -p "$OUT/pathspmc" && mv "$OUT/pathsp3" "$OUT/pathsp4" "$OUT/pathspmc/"
+python3 scripts/pmc_summary.py "$OUT/pathspmc" workload=paths "command=scripts/bench_paths.py --reps 1" > "$OUT/paths_pmc_summary.txt" || { echo "paths pmc summary failed"; exit 1; }
+cp "$OUT/pathspmc/summary.json" "$OUT/paths_pmc_summary.json"
+echo "paths pmc ok"
