@@ -31,7 +31,9 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.29 TB/s measured copy
 N_CU = 256              # MI355X: 8 XCDs x 32 CUs
 # algorithmic bytes per unit (DESIGN.md "Roofline accounting")
-SWEEP_B_PER_WALL_EVENT = 8      # read one arrival time
+SWEEP_B_PER_WALL_EVENT = 8      # read one arrival time (the windowed general sweep)
+MRG_SWEEP_B_PER_WALL_EVENT = 10  # read one merged (t f64, stream u16) entry
+MERGE_B_PER_WALL_EVENT = 18     # rq_merge_streams: read the arrival (8), write the entry (10)
 SWEEP_B_PER_ROW = 24            # write t f64 + sumR f64 + nvalid u32 + cnt[K=1] u32
 SCAN_B_PER_ROW = 24             # read the same row back
 GEN_B_PER_WALL_EVENT = 8        # write one arrival time
@@ -241,7 +243,9 @@ def main():
     posts_step = posts_l / a.steps
     # the fused sweep (variant >= 10) generates its arrivals in LDS: no arrival reads
     fused = plan["variant"] >= 10
-    sweep_bytes = (0 if fused else SWEEP_B_PER_WALL_EVENT * (ev_rank - posts_step)) + \
+    merged = not fused and plan["sources_per_lane"] == 0   # rq_merge_streams feeds the sweep
+    b_wall = MRG_SWEEP_B_PER_WALL_EVENT if merged else SWEEP_B_PER_WALL_EVENT
+    sweep_bytes = (0 if fused else b_wall * (ev_rank - posts_step)) + \
         SWEEP_B_PER_ROW * rows_step
     achieved = sweep_bytes / (sweep_ms * 1e-3) / 1e9
     scan_ms = ms[2] / max(1, int(nl[2]))
@@ -249,6 +253,9 @@ def main():
     scan_gbs = SCAN_B_PER_ROW * rows_step / (scan_ms * 1e-3) / 1e9 if scan_ms > 0 else None
     gen_gbs = GEN_B_PER_WALL_EVENT * (ev_rank - posts_step) / (gen_ms * 1e-3) / 1e9 \
         if gen_ms > 0 else None
+    merge_ms = ms[4] / max(1, int(nl[4]))
+    merge_gbs = MERGE_B_PER_WALL_EVENT * (ev_rank - posts_step) / (merge_ms * 1e-3) / 1e9 \
+        if merge_ms > 0 else None
 
     traffic, traffic_src, issue = pmc_traffic(a.workload, R, plan)
     if issue and "issue_frac" in issue:
@@ -287,7 +294,8 @@ def main():
             "events_per_replica": local_ev / replicas,
             "overflow": int(status.item()),
             "tie_replicas": int(ties.item()),
-            "kernels_ms_per_launch": {"gen_streams": gen_ms, "sweep": sweep_ms, "scan": scan_ms},
+            "kernels_ms_per_launch": {"gen_streams": gen_ms, "merge_streams": merge_ms, "sweep": sweep_ms,
+                                      "scan": scan_ms},
             "sweep_plan": plan,
             "roofline": {"bound": "hbm", "kernel": "rq_sweep", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
@@ -299,9 +307,10 @@ def main():
                          "issue_frac": issue.get("issue_frac") if issue else None,
                          "note": "sweep is latency/issue-bound (serial event chain per replica); "
                                  "algorithmic bytes = 24 B/pivot row written%s" %
-                                 ("" if fused else " + 8 B/wall event read")},
+                                 ("" if fused else " + %d B/wall event read" % b_wall)},
             "scan_gbs": scan_gbs,
             "gen_gbs": gen_gbs,
+            "merge_gbs": merge_gbs,
             "cpu_baseline": cpu,
             "cpu_baseline_reference": ref_cpu_baseline(a.workload),
         }

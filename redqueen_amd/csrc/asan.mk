@@ -9,7 +9,7 @@ HSAN = -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
 FLAGS = -O2 -g --offload-arch=$(ARCH) -ffp-contract=off -fno-fast-math -fPIC -std=c++17 $(HSAN)
 OUT = ../_asan/librq.so
 BUILD = build_asan
-SRC = rq_kernels.hip rq_sweep_fw.hip rq_analysis.hip rq_replay.hip rq_api.cpp
+SRC = rq_kernels.hip rq_sweep_fw.hip rq_merge.hip rq_analysis.hip rq_replay.hip rq_api.cpp
 OBJ = $(addprefix $(BUILD)/,$(addsuffix .o,$(SRC)))
 HDR = rq_spec.h rq_tables.h rq_device.h rq_internal.h rq_gen.h rq_sweep_core.h ../../include/rq.h
 

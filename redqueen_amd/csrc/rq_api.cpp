@@ -150,6 +150,10 @@ struct Plan {
     // fused windowed sweep (n_str <= 64): arrivals generated in-kernel, window depth fw_h
     bool fw = false;
     int fw_h = 8, mstride = 1;
+    // general fast sweep on merged streams (rq_merge_streams; sweep_mode 6: the windowed
+    // per-source merge inside the sweep instead)
+    bool mrg = false;
+    size_t off_mt = 0, off_mj = 0, off_mlen = 0;
     // general sweep LDS layout
     int gwpb = 4, gwin = 16, gcol_lds = 1, gcol16 = 0;
     size_t g_col = 0, g_ptr = 0, g_odf = 0, g_cbf = 0, g_wave = 0, g_wave_stride = 0, g_rank_off = 0,
@@ -315,6 +319,10 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
         p->bl = true;
     }
     p->gs = false;
+    // the fast general sweep plays the merged (t, stream) sequence: the merge kernel reads
+    // every stream line once (one source per thread, <= RQ_MG_B sources)
+    p->mrg = !p->log && b->sweep_mode != 6 && g->n_str <= RQ_MG_B;
+    if (const char* e = getenv("RQ_MRG")) p->mrg = p->mrg && atoi(e) != 0;   // A/B only
 
     // general sweep: pick (ring depth W, waves per block) for the most waves per CU
     {
@@ -325,6 +333,8 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
         // LOG: the per-sink state in LDS, or (gs) in global memory for more sinks than fit
         for (int gs = 0; gs <= (p->log ? 1 : 0); ++gs)
         for (int col_lds = g->n_sinks <= 65535 && !(p->log && p->spl >= 16) ? 1 : 0; col_lds >= 0; --col_lds) {
+            if (const char* e = getenv("RQ_G_COLLDS"))   // tuning only: force the column placement
+                if (atoi(e) != col_lds) continue;
             const int c16 = col_lds;
             // BITS: sink bitsets [n_str][nw] replace the columns (and the per-wave ranks)
             const size_t colb = p->bits ? 4 * (size_t)g->n_str * p->mstride
@@ -348,6 +358,7 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
                 if (only_w && W != only_w) continue;
                 const size_t r_off = inv_sh ? 0 : align_up(8 * (size_t)g->n_str, 16);
                 const size_t rank_b = p->log ? (gs ? 0 : 4) : (p->bits ? 0 : 2);   // fast: int16 saturating
+            const int spl_i = p->mrg ? 0 : spl;   // the instance: 0 = merged streams
                 // BL: two bits per sink (T, V words) in place of the int16 ranks
                 const size_t w_off = p->bl ? align_up(r_off + 8 * (size_t)nwl, 16)
                                            : align_up(r_off + rank_b * (size_t)p->n_sinks_pad, 16);
@@ -360,12 +371,13 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
                 if (p->log) stride = align_up(x_off + (gs ? 0 : 12 * (size_t)p->n_sinks_pad) + 8 * 304, 16);
                 for (int wpb : {16, 12, 10, 8, 6, 5, 4, 3, 2, 1}) {
                     if (p->log && wpb > 4) continue;   // LOG instances: 256-thread blocks
-                    if (!p->log && spl >= 4 && wpb > 8) continue;   // 512-thread instances
+                    if (!p->log && !p->mrg && spl >= 4 && wpb > 8) continue;   // 512-thread instances
+                    if (p->mrg && 64 * wpb > RQ_MRG_LB) continue;
                     const size_t tot = sh + wpb * stride;
                     if (tot > kLdsMax) continue;
                     // resident waves per CU: the runtime's occupancy for this instance
                     // (VGPR/SGPR/LDS); without a device, the LDS bound capped at 16
-                    int blocks = rq_sweep_blocks_per_cu(spl, p->nK, c16, W, p->log ? 1 + gs : 0,
+                    int blocks = rq_sweep_blocks_per_cu(spl_i, p->nK, c16, W, p->log ? 1 + gs : 0,
                                                         p->bl ? 2 : p->bits, wpb, tot);
                     if (blocks <= 0) blocks = (int)std::min<size_t>(kLdsMax / tot, 16 / wpb);
                     const int waves = blocks * wpb;
@@ -395,7 +407,8 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     // fused windowed sweep: one stream per lane, rings of W arrivals generated in LDS,
     // a window of H per ring in registers; (W, H, waves per block) for the most waves per CU
     const bool pw = b->ctrl_kind == RQ_SRC_OPTPW;
-    p->fw = !p->log && !p->bl && g->n_str <= 64 && b->sweep_mode != 4 && b->sweep_mode != 5;
+    p->fw = !p->log && !p->bl && g->n_str <= 64 && b->sweep_mode != 4 && b->sweep_mode != 5 &&
+            b->sweep_mode != 6;
     if (p->fw) {
         int best = -1;
         const int c16 = p->bits ? 1 : (g->n_sinks <= 65535 ? 1 : 0);
@@ -442,6 +455,7 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
         }
         if (best < 0) p->fw = false;
     }
+    if (p->fw) p->mrg = false;
 
     const size_t A = 256;
     const int64_t C = p->chunk;
@@ -459,6 +473,10 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     const int64_t strm = p->fw ? 0 : C;   // the fused sweep keeps its arrivals in LDS
     p->off_streams = o; o = align_up(o + sizeof(double) * (size_t)strm * p->capsum, A);
     p->off_slen = o;    o = align_up(o + sizeof(int) * (size_t)strm * g->n_str, A);
+    const int64_t mrgc = p->mrg ? C : 0;   // merged sequences: t f64, stream u16, length
+    p->off_mt = o;      o = align_up(o + sizeof(double) * (size_t)mrgc * p->capsum, A);
+    p->off_mj = o;      o = align_up(o + sizeof(uint16_t) * (size_t)mrgc * p->capsum, A);
+    p->off_mlen = o;    o = align_up(o + sizeof(int) * (size_t)mrgc, A);
     p->off_rt = o;      o = align_up(o + sizeof(double) * (size_t)C * p->cap_rows, A);
     p->off_rs = o;      o = align_up(o + sizeof(double) * (size_t)C * p->cap_rows, A);
     p->off_rv = o;      o = align_up(o + sizeof(uint32_t) * (size_t)C * p->cap_rows, A);
@@ -727,12 +745,12 @@ int rq_plan_info(rq_graph_t g, const rq_batch_desc* b, int64_t* info)
     const int rc = make_plan(g, b, &p);
     if (rc) return rc;
     info[0] = (p.log ? (p.gs ? 4 : 1) : (p.bits ? 2 : (p.bl ? 3 : 0))) + (p.fw ? 10 : 0);
-    info[1] = p.spl;
+    info[1] = p.mrg ? 0 : p.spl;   // 0: merged streams (lanes own no sources)
     info[2] = p.gwin;
     info[3] = p.gwpb;
     info[4] = p.fw ? rq_fw_blocks_per_cu(p.nK, p.gcol16, p.gwin, p.bits, p.gwpb, p.g_total,
                                           b->ctrl_kind == RQ_SRC_OPTPW)
-                   : rq_sweep_blocks_per_cu(p.spl, p.nK, p.gcol16, p.gwin, p.log ? 1 + p.gs : 0,
+                   : rq_sweep_blocks_per_cu(p.mrg ? 0 : p.spl, p.nK, p.gcol16, p.gwin, p.log ? 1 + p.gs : 0,
                                             p.bl ? 2 : p.bits, p.gwpb, p.g_total);
     info[5] = p.gcol_lds;
     info[6] = (int64_t)p.g_total;
@@ -893,6 +911,32 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             TimedLaunch tl(K_GEN, s);
             if (rq_launch_gen(ga, s) != hipSuccess) return RQ_EHIP;
         }
+        if (p.mrg) {
+            MergeArgs ma{};
+            ma.n_chunk = C;
+            ma.chunk0 = c0;
+            ma.n_str = g->n_str;
+            ma.capsum = p.capsum;
+            ma.st_off = ga.st_off;
+            ma.streams = ga.streams;
+            ma.slen = ga.slen;
+            ma.end = g->end;
+            ma.out_t = (double*)(ws + p.off_mt);
+            ma.out_j = (uint16_t*)(ws + p.off_mj);
+            ma.out_len = (int*)(ws + p.off_mlen);
+            ma.status = out->status;
+#ifdef RQ_PHASE_CLOCK
+            {
+                static unsigned long long* clk = nullptr;
+                if (!clk && hipMalloc(&clk, 8 * sizeof(unsigned long long)) == hipSuccess)
+                    (void)hipMemset(clk, 0, 8 * sizeof(unsigned long long));
+                ma.clk = clk;
+                g_clk = clk;
+            }
+#endif
+            TimedLaunch tl(K_MERGE, s);
+            if (rq_launch_merge(ma, s) != hipSuccess) return RQ_EHIP;
+        }
 
         SweepArgs sa{};
         sa.n_chunk = C;
@@ -927,6 +971,11 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
         sa.capsum = p.capsum;
         sa.streams = (const double*)(ws + p.off_streams);
         sa.slen = (const int*)(ws + p.off_slen);
+        if (p.mrg) {
+            sa.mrg_t = (const double*)(ws + p.off_mt);
+            sa.mrg_j = (const uint16_t*)(ws + p.off_mj);
+            sa.mrg_len = (const int*)(ws + p.off_mlen);
+        }
         sa.start = g->start;
         sa.end = g->end;
         sa.max_events = b->max_events;
@@ -1011,7 +1060,7 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             }
             TimedLaunch tl(K_SWEEP, s);
             const hipError_t e = p.fw ? rq_launch_sweep_fw(sa, p.nK, p.gcol16, p.gwin, p.bits, s)
-                                      : rq_launch_sweep(sa, p.spl, p.nK, p.gcol16, p.log ? 1 + p.gs : 0,
+                                      : rq_launch_sweep(sa, p.mrg ? 0 : p.spl, p.nK, p.gcol16, p.log ? 1 + p.gs : 0,
                                                         p.bl ? 2 : p.bits, s);
             if (e != hipSuccess) return RQ_EHIP;
         }

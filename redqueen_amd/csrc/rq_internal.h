@@ -113,7 +113,35 @@ struct SweepArgs {
     char* gs;
     int64_t gs_stride;
     int gs_slots;
+    // general fast sweep on merged streams (rq_merge_streams): replica rl's arrivals of
+    // every source in play order, mrg_t / mrg_j [rl * capsum + k], k < mrg_len[rl]
+    const double* mrg_t;
+    const uint16_t* mrg_j;
+    const int* mrg_len;
 };
+
+// rq_merge_streams: one block per replica merges its pre-generated per-source streams
+// into the (t, stream) sequence the sweep plays -- time order, equal times in stream
+// order, a source's equal times in stream order (the windowed sweep's stage rank)
+struct MergeArgs {
+    int64_t n_chunk, chunk0;
+    int n_str;
+    int64_t capsum;
+    const int64_t* st_off;
+    const double* streams;
+    const int* slen;
+    double end;
+    double* out_t;          // [C][capsum]
+    uint16_t* out_j;        // [C][capsum]
+    int* out_len;           // [C]
+    int32_t* status;        // RQ_ST_TIE when > RQ_MG_CAP arrivals share one time
+    unsigned long long* clk;   // RQ_PHASE_CLOCK builds only: per-phase s_memtime sums [8]
+};
+// threads per block of the merged-stream sweep instances (1024: <= 128 VGPRs)
+#ifndef RQ_MRG_LB
+#define RQ_MRG_LB 1024
+#endif
+#define RQ_MG_B 512         // merge block: one source per thread (the fast general sweep: <= 512)
 
 struct ScanArgs {
     int64_t n_chunk, chunk0;
@@ -136,6 +164,8 @@ hipError_t rq_launch_gen(const GenArgs& a, hipStream_t s);
 hipError_t rq_launch_sweep(const SweepArgs& a, int spl, int nK, int col16, int log, int bits, hipStream_t s);
 hipError_t rq_launch_scan(const ScanArgs& a, int nK, hipStream_t s);
 int rq_sweep_blocks_per_cu(int spl, int nK, int col16, int W, int log, int bits, int wpb, size_t lds);
+// spl = 0 in rq_launch_sweep / rq_sweep_blocks_per_cu: the fast sweep reading merged streams
+hipError_t rq_launch_merge(const MergeArgs& a, hipStream_t s);
 hipError_t rq_launch_sweep_fw(const SweepArgs& a, int nK, int col16, int W, int bits, hipStream_t s);
 int rq_fw_blocks_per_cu(int nK, int col16, int W, int bits, int wpb, size_t lds, int pw);
 int rq_cu_count();   // CUs of the current device (256 on MI355X when the query fails)

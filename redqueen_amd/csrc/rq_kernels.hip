@@ -107,8 +107,10 @@ __global__ __launch_bounds__(256) void rq_gen_streams(GenArgs a)
 //    GS  = LOG with the per-sink state (rank, pivot-cell group) in global memory, one
 //          slot per resident wave (SweepArgs.gs): any number of sinks.
 // ============================================================================
-template <int SPL, int NK, class COL, int W, bool LOG, bool BITS, bool BL, bool GS = false>
-__global__ __launch_bounds__(LOG ? 256 : (SPL >= 4 ? 512 : 1024)) void rq_sweep(SweepArgs a)
+//    MRG = the fast sweep on merged streams (rq_merge_streams): a tile is the next 64
+//          entries of the replica's (t, stream) sequence, loaded one tile ahead.
+template <int SPL, int NK, class COL, int W, bool LOG, bool BITS, bool BL, bool GS = false, bool MRG = false>
+__global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 1024))) void rq_sweep(SweepArgs a)
 {
     extern __shared__ double lds_g[];
     char* base = reinterpret_cast<char*>(lds_g);
@@ -196,8 +198,8 @@ __global__ __launch_bounds__(LOG ? 256 : (SPL >= 4 ? 512 : 1024)) void rq_sweep(
 #pragma unroll
     for (int q = 0; q < SPL; ++q) {
         const int j = lane * SPL + q;
-        off[q] = j < a.n_str ? (int)a.st_off[j] : 0;
-        len[q] = j < a.n_str ? slen[j] : 0;
+        off[q] = j < a.n_str && !MRG ? (int)a.st_off[j] : 0;
+        len[q] = j < a.n_str && !MRG ? slen[j] : 0;
         pos[q] = 0;
         fil[q] = 0;
     }
@@ -234,9 +236,20 @@ __global__ __launch_bounds__(LOG ? 256 : (SPL >= 4 ? 512 : 1024)) void rq_sweep(
                 larg = q;
             }
         }
-    } else {
+    } else if constexpr (!MRG) {
 #pragma unroll
         for (int q = 0; q < SPL; ++q) load_win(q);
+    }
+    // MRG: the replica's merged sequence; lane l holds entry mpos + l of the next tile
+    const double* mt = MRG ? a.mrg_t + rl * a.capsum : nullptr;
+    const uint16_t* mj = MRG ? a.mrg_j + rl * a.capsum : nullptr;
+    const int mlen = MRG ? a.mrg_len[rl] : 0;
+    int mpos = 0;
+    double nxt_t = RQ_INF;
+    int nxt_j = 0;
+    if (MRG && lane < mlen) {
+        nxt_t = mt[lane];
+        nxt_j = mj[lane];
     }
     double span = -1.0;   // fast sweep: adaptive tile width in time (< 0: not estimated yet)
     double* st_t = reinterpret_cast<double*>(win);   // fast sweep: tile staging (64 t + 64 j)
@@ -334,7 +347,21 @@ __global__ __launch_bounds__(LOG ? 256 : (SPL >= 4 ? 512 : 1024)) void rq_sweep(
         double tt = RQ_INF;
         int tj = 0, n = 0;
         bool fin_w = false;
-        if constexpr (!LOG) {
+        if constexpr (MRG) {
+            if (mpos >= mlen) break;   // every arrival played
+            n = mlen - mpos < 64 ? mlen - mpos : 64;
+            tt = lane < n ? nxt_t : RQ_INF;
+            tj = lane < n ? nxt_j : 0;
+            mpos += n;
+            fin_w = mpos >= mlen;
+            // the next tile's loads stay in flight through phases B and C
+            nxt_t = RQ_INF;
+            nxt_j = 0;
+            if (mpos + lane < mlen) {
+                nxt_t = mt[mpos + lane];
+                nxt_j = mj[mpos + lane];
+            }
+        } else if constexpr (!LOG) {
             // windowed: every arrival before a cut tau, tau < the W-th pending arrival of
             // every source that has more (so the tile is complete) and tuned so the tile
             // holds <= 64; staged in source order, rank-sorted into (t, source) order --
@@ -938,15 +965,17 @@ int rq_cu_count()
     }();
     return n;
 }
-template <int SPL, int NK, class COL, int W, bool LOG, bool BITS = false, bool BL = false, bool GS = false>
+template <int SPL, int NK, class COL, int W, bool LOG, bool BITS = false, bool BL = false, bool GS = false,
+          bool MRG = false>
 static int occ_t(int wpb, size_t lds);
-template <int SPL, int NK, class COL, int W, bool LOG, bool BITS = false, bool BL = false, bool GS = false>
+template <int SPL, int NK, class COL, int W, bool LOG, bool BITS = false, bool BL = false, bool GS = false,
+          bool MRG = false>
 static hipError_t launch_sweep_t(const SweepArgs& a, hipStream_t s)
 {
     unsigned blocks = (unsigned)((a.n_chunk + a.wpb - 1) / a.wpb);
     if (a.wq) {
         // persistent grid: every resident wave slot once, the rest from the queue
-        const int nb_c = occ_t<SPL, NK, COL, W, LOG, BITS, BL, GS>(a.wpb, a.lds_total);
+        const int nb_c = occ_t<SPL, NK, COL, W, LOG, BITS, BL, GS, MRG>(a.wpb, a.lds_total);
         const unsigned cap = (unsigned)(nb_c > 0 ? nb_c : 1) * (unsigned)rq_cu_count();
         if (cap < blocks) blocks = cap;
     }
@@ -955,7 +984,8 @@ static hipError_t launch_sweep_t(const SweepArgs& a, hipStream_t s)
         if (!a.wq || cap < 1) return hipErrorInvalidValue;
         if (cap < blocks) blocks = cap;
     }
-    hipLaunchKernelGGL((rq_sweep<SPL, NK, COL, W, LOG, BITS, BL, GS>), dim3(blocks), dim3(64 * a.wpb), a.lds_total, s, a);
+    hipLaunchKernelGGL((rq_sweep<SPL, NK, COL, W, LOG, BITS, BL, GS, MRG>), dim3(blocks), dim3(64 * a.wpb), a.lds_total,
+                       s, a);
     return hipGetLastError();
 }
 
@@ -983,6 +1013,37 @@ static hipError_t launch_sweep_c(const SweepArgs& a, int nK, int col16, int bits
         return launch_sweep_t<SPL, 1, uint16_t, kGW, false, true>(a, s);
     return col16 ? launch_sweep_k<SPL, uint16_t, kGW, false>(a, nK, s)
                  : launch_sweep_k<SPL, int, kGW, false>(a, nK, s);
+}
+
+// the fast sweep on merged streams: one instance per (K variant, column type)
+template <int NK, class COL>
+static hipError_t launch_sweep_mk(const SweepArgs& a, hipStream_t s)
+{
+    return launch_sweep_t<1, NK, COL, kGW, false, false, false, false, true>(a, s);
+}
+template <class COL>
+static hipError_t launch_sweep_m(const SweepArgs& a, int nK, int bits, hipStream_t s)
+{
+    if (bits == 2) return launch_sweep_t<1, 1, COL, kGW, false, false, true, false, true>(a, s);
+    if (bits) return launch_sweep_t<1, 1, uint16_t, kGW, false, true, false, false, true>(a, s);
+    switch (nK) {
+    case 1: return launch_sweep_mk<1, COL>(a, s);
+    case 2: return launch_sweep_mk<2, COL>(a, s);
+    case 3: return launch_sweep_mk<3, COL>(a, s);
+    default: return launch_sweep_mk<4, COL>(a, s);
+    }
+}
+template <class COL>
+static int occ_m(int nK, int bits, int wpb, size_t lds)
+{
+    if (bits == 2) return occ_t<1, 1, COL, kGW, false, false, true, false, true>(wpb, lds);
+    if (bits) return occ_t<1, 1, uint16_t, kGW, false, true, false, false, true>(wpb, lds);
+    switch (nK) {
+    case 1: return occ_t<1, 1, COL, kGW, false, false, false, false, true>(wpb, lds);
+    case 2: return occ_t<1, 2, COL, kGW, false, false, false, false, true>(wpb, lds);
+    case 3: return occ_t<1, 3, COL, kGW, false, false, false, false, true>(wpb, lds);
+    default: return occ_t<1, 4, COL, kGW, false, false, false, false, true>(wpb, lds);
+    }
 }
 
 hipError_t rq_launch_gen(const GenArgs& a, hipStream_t s)
@@ -1018,6 +1079,8 @@ hipError_t rq_launch_sweep(const SweepArgs& a, int spl, int nK, int col16, int l
         case 16: return launch_sweep_k<16, int, 8, true>(a, nK, s);
         default: return launch_sweep_k<32, int, 4, true>(a, nK, s);
         }
+    if (spl == 0)   // merged streams
+        return col16 ? launch_sweep_m<uint16_t>(a, nK, bits, s) : launch_sweep_m<int>(a, nK, bits, s);
     switch (spl) {
     case 1: return launch_sweep_c<1>(a, nK, col16, bits, s);
     case 2: return launch_sweep_c<2>(a, nK, col16, bits, s);
@@ -1028,10 +1091,10 @@ hipError_t rq_launch_sweep(const SweepArgs& a, int spl, int nK, int col16, int l
 
 // blocks of 64*wpb threads per CU the chosen sweep instance reaches with `lds`
 // bytes of dynamic LDS (VGPR, SGPR and LDS limits all applied by the runtime)
-template <int SPL, int NK, class COL, int W, bool LOG, bool BITS, bool BL, bool GS>
+template <int SPL, int NK, class COL, int W, bool LOG, bool BITS, bool BL, bool GS, bool MRG>
 static int occ_t(int wpb, size_t lds)
 {
-    return rq_occupancy(rq_sweep<SPL, NK, COL, W, LOG, BITS, BL, GS>, 64 * wpb, lds);
+    return rq_occupancy(rq_sweep<SPL, NK, COL, W, LOG, BITS, BL, GS, MRG>, 64 * wpb, lds);
 }
 template <int SPL, class COL, int W, bool LOG, bool GS = false>
 static int occ_k(int nK, int wpb, size_t lds)
@@ -1070,6 +1133,7 @@ int rq_sweep_blocks_per_cu(int spl, int nK, int col16, int W, int log, int bits,
         case 16: return occ_k<16, int, 8, true>(nK, wpb, lds);
         default: return occ_k<32, int, 4, true>(nK, wpb, lds);
         }
+    if (spl == 0) return col16 ? occ_m<uint16_t>(nK, bits, wpb, lds) : occ_m<int>(nK, bits, wpb, lds);
     switch (spl) {
     case 1: return occ_c<1>(nK, col16, W, bits, wpb, lds);
     case 2: return occ_c<2>(nK, col16, W, bits, wpb, lds);

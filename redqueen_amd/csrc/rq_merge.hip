@@ -1,0 +1,303 @@
+// rq_merge.hip -- the general fast sweep's arrival merge as its own kernel.
+//
+// Manager.run_dynamic (opt_model.py:241-314) plays the other sources' events in
+// (time, source) order; with > 64 sources the arrivals are pre-generated per source
+// (rq_gen_streams), and a sweep wave that merges 500 streams itself touches each
+// source's stream 8 bytes at a time -- the lines are evicted between touches (round 2:
+// ~10x the algorithmic read bytes).  Here one block per replica merges them once:
+//
+//   thread j owns source j (<= RQ_MG_B sources) and reads its stream in aligned
+//   64-byte chunks (one chunk in use, the next in flight), so every line is read once;
+//   rounds: every arrival before a cut tau (tau adapts so a round holds ~MG_TARGET)
+//   goes to an LDS buffer with its time sub-bucket (M equal slices of [t_lo, tau),
+//   a monotone map of t) and its slot in that bucket (LDS atomics), a block scan of the
+//   bucket counts places the buckets, and each arrival's rank inside its bucket --
+//   (t, source, buffer index) order, a bucket holds ~1 arrival -- gives its place;
+//   the round is written out contiguously: mrg_t f64 / mrg_j u16 [replica][capsum].
+//
+// A source's arrivals enter the buffer in stream order (a lane's buffer indices grow),
+// so equal times keep stream order within a source and source order across sources:
+// the order the windowed sweep's stage rank gives (rq_device.h stage_rank).
+// More than MG_CAP arrivals at ONE time (only replayed data can do that) cannot be
+// ordered in a round: the block emits them MG_CAP at a time and flags RQ_ST_TIE, which
+// sends the batch to the exact sequential sweep (engine.Graph.run(check=True)).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rq_device.h"
+#include "rq_internal.h"
+
+#pragma clang fp contract(off)
+
+using namespace rq;
+
+namespace {
+
+constexpr int MG_B = RQ_MG_B;
+constexpr int MG_W = MG_B / 64;
+constexpr int MG_CAP = 2048;        // arrivals per round (LDS buffer)
+constexpr int MG_M = 2048;          // time sub-buckets per round
+constexpr int MG_TARGET = 1536;     // arrivals a round aims at
+#ifndef RQ_MG_PF
+#define RQ_MG_PF 1                  // stream chunks in flight ahead of the one in use
+#endif
+constexpr int MG_SB = 11;           // bits of a slot / buffer index (< MG_CAP)
+
+static_assert(MG_CAP <= (1 << MG_SB) && MG_M <= (1 << MG_SB), "packed fields");
+static_assert(MG_M == 4 * MG_B, "the bucket scan gives each thread 4 buckets");
+
+__device__ __forceinline__ double sel8(const double (&c)[8], int k)
+{
+    const double a0 = (k & 1) ? c[1] : c[0], a1 = (k & 1) ? c[3] : c[2];
+    const double a2 = (k & 1) ? c[5] : c[4], a3 = (k & 1) ? c[7] : c[6];
+    const double b0 = (k & 2) ? a1 : a0, b1 = (k & 2) ? a3 : a2;
+    return (k & 4) ? b1 : b0;
+}
+
+__device__ __forceinline__ void load8(double (&c)[8], const double* p)
+{
+    const double4* q = reinterpret_cast<const double4*>(p);   // 64-byte aligned chunk
+    const double4 x = q[0], y = q[1];
+    c[0] = x.x; c[1] = x.y; c[2] = x.z; c[3] = x.w;
+    c[4] = y.x; c[5] = y.y; c[6] = y.z; c[7] = y.w;
+}
+
+// sub-bucket of t in [t_lo, tau): non-decreasing in t (a NaN scale -- tau one ulp
+// above t_lo = 0 -- sends every arrival of the round to the last bucket)
+__device__ __forceinline__ int sub_of(double t, double t_lo, double scale)
+{
+    const double x = (t - t_lo) * scale;
+    return x < (double)(MG_M - 1) ? (int)x : MG_M - 1;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
+{
+    __shared__ double bt[MG_CAP];          // round buffer (arrival order)
+    __shared__ uint32_t bs[MG_CAP];        // (sub-bucket << MG_SB) | slot
+    __shared__ uint16_t bj[MG_CAP];
+    __shared__ double st[MG_CAP];          // bucket order
+    __shared__ uint32_t sk[MG_CAP];        // (stream << MG_SB) | buffer index
+    __shared__ uint32_t cnt[MG_M];
+    __shared__ uint32_t bbase[MG_M + 1];
+    __shared__ double wmin[MG_W];
+    __shared__ uint32_t wsum[MG_W];
+    __shared__ uint32_t nb;
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int64_t rl = blockIdx.x;
+    const int j = tid;
+    int L = 0;
+    const double* src = a.streams;
+    if (j < a.n_str) {
+        L = a.slen[rl * a.n_str + j];
+        src = a.streams + rl * a.capsum + a.st_off[j];
+    }
+    // the aligned chunk holding position p, and the next RQ_MG_PF ones (in flight)
+    double c[8], nx[8];
+#if RQ_MG_PF > 1
+    double nx2[8];
+#endif
+    int p = 0;
+    auto reload = [&](int p0) __attribute__((always_inline)) {
+        const int c0 = p0 & ~7;
+        if (c0 < L) load8(c, src + c0);
+        if (c0 + 8 < L) load8(nx, src + c0 + 8);
+#if RQ_MG_PF > 1
+        if (c0 + 16 < L) load8(nx2, src + c0 + 16);
+#endif
+    };
+    reload(0);
+    double head = L > 0 ? c[0] : RQ_INF;
+    auto consume = [&]() __attribute__((always_inline)) {
+        ++p;
+        if ((p & 7) == 0) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) c[k] = nx[k];
+#if RQ_MG_PF > 1
+#pragma unroll
+            for (int k = 0; k < 8; ++k) nx[k] = nx2[k];
+            if (p + 16 < L) load8(nx2, src + p + 16);
+#else
+            if (p + 8 < L) load8(nx, src + p + 8);
+#endif
+        }
+        head = p < L ? sel8(c, p & 7) : RQ_INF;
+    };
+
+    for (int k = tid; k < MG_M; k += MG_B) cnt[k] = 0;
+    if (tid == 0) nb = 0;
+    {
+        const double m = wave_min_f64(head);
+        const uint32_t s = wave_sum_u32((uint32_t)L);
+        if (lane == 0) {
+            wmin[w] = m;
+            wsum[w] = s;
+        }
+    }
+    __syncthreads();
+    double t_lo = wmin[0];
+    uint32_t total = 0;
+#pragma unroll
+    for (int k = 0; k < MG_W; ++k) {
+        t_lo = wmin[k] < t_lo ? wmin[k] : t_lo;
+        total += wsum[k];
+    }
+    double span = (a.end - t_lo) * ((double)MG_TARGET / (double)(total > 1 ? total : 1));
+    int64_t outpos = 0;
+    double* out_t = a.out_t + rl * a.capsum;
+    uint16_t* out_j = a.out_j + rl * a.capsum;
+    int status = 0;
+    __syncthreads();   // wmin / wsum read before the first round rewrites them
+#ifdef RQ_PHASE_CLOCK
+    // diagnostic builds: block-0-thread view of where a round's time goes
+    unsigned long long ck[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tc0 = 0, tc1 = 0;
+#define RQ_MG_TICK(k)                                                    \
+    do {                                                                 \
+        tc1 = __builtin_amdgcn_s_memtime();                              \
+        ck[k] += tc1 - tc0;                                              \
+        tc0 = tc1;                                                       \
+    } while (0)
+#else
+#define RQ_MG_TICK(k) do { } while (0)
+#endif
+
+    while (t_lo <= a.end) {
+#ifdef RQ_PHASE_CLOCK
+        tc0 = __builtin_amdgcn_s_memtime();
+        ck[4] += 1;
+#endif
+        double tau = t_lo + span;
+        if (!(tau > t_lo)) tau = next_up(t_lo);
+        const double scale = (double)MG_M / (tau - t_lo);
+        const int p0 = p;
+        // ---- every arrival before tau into the buffer (a lane stops at a full buffer) ----
+        bool more = true;
+        for (;;) {
+            const bool act = more && head < tau;
+            const uint64_t m = __ballot(act);
+            if (!m) break;
+            const int fl = __ffsll((unsigned long long)m) - 1;
+            uint32_t b0 = 0;
+            if (lane == fl) b0 = atomicAdd(&nb, (uint32_t)__popcll(m));
+            b0 = (uint32_t)__builtin_amdgcn_readlane((int)b0, fl);
+            if (act) {
+                const uint32_t idx = b0 + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                if (idx < (uint32_t)MG_CAP) {
+                    const int sb = sub_of(head, t_lo, scale);
+                    const uint32_t slot = atomicAdd(&cnt[sb], 1u);
+                    bt[idx] = head;
+                    bj[idx] = (uint16_t)j;
+                    bs[idx] = ((uint32_t)sb << MG_SB) | slot;
+                    consume();
+                } else {
+                    more = false;
+                }
+            }
+        }
+        {
+            const double m = wave_min_f64(head);
+            if (lane == 0) wmin[w] = m;
+        }
+        RQ_MG_TICK(0);
+        __syncthreads();
+        RQ_MG_TICK(1);
+        const uint32_t nr_all = nb;
+        uint32_t nr = nr_all;
+        if (nr_all > (uint32_t)MG_CAP) {
+            if (tau != next_up(t_lo)) {
+                // too many for one round: undo it and halve the cut
+                p = p0;
+                reload(p0);
+                head = p < L ? sel8(c, p & 7) : RQ_INF;
+                for (int k = tid; k < MG_M; k += MG_B) cnt[k] = 0;
+                __syncthreads();
+                if (tid == 0) nb = 0;
+                span = (tau - t_lo) * 0.5;
+                __syncthreads();
+#ifdef RQ_PHASE_CLOCK
+                ck[5] += 1;
+#endif
+                continue;
+            }
+            // more than MG_CAP arrivals at t_lo itself: take the first MG_CAP (any subset
+            // of equal times is a time prefix) and flag the replica
+            nr = MG_CAP;
+            status |= RQ_ST_TIE;
+        }
+        double t_next = wmin[0];
+#pragma unroll
+        for (int k = 1; k < MG_W; ++k) t_next = wmin[k] < t_next ? wmin[k] : t_next;
+        // ---- bucket bases: exclusive scan of cnt (4 buckets per thread) ----
+        uint32_t v0 = cnt[4 * tid], v1 = cnt[4 * tid + 1], v2 = cnt[4 * tid + 2], v3 = cnt[4 * tid + 3];
+        const uint32_t tsum = v0 + v1 + v2 + v3;
+        const uint32_t incl = wave_scan_add(tsum);
+        if (lane == 63) wsum[w] = incl;
+        __syncthreads();
+        if (tid == 0) nb = 0;   // every thread read nb before this barrier
+        uint32_t wo = 0;
+#pragma unroll
+        for (int k = 0; k < MG_W; ++k) wo += k < w ? wsum[k] : 0u;
+        {
+            const uint32_t b = wo + incl - tsum;
+            bbase[4 * tid] = b;
+            bbase[4 * tid + 1] = b + v0;
+            bbase[4 * tid + 2] = b + v0 + v1;
+            bbase[4 * tid + 3] = b + v0 + v1 + v2;
+            cnt[4 * tid] = cnt[4 * tid + 1] = cnt[4 * tid + 2] = cnt[4 * tid + 3] = 0;
+            if (tid == 0) bbase[MG_M] = nr;
+        }
+        __syncthreads();
+        RQ_MG_TICK(2);
+        // ---- into bucket order ----
+        for (int i = tid; i < (int)nr; i += MG_B) {
+            const uint32_t x = bs[i];
+            const uint32_t pos = bbase[x >> MG_SB] + (x & ((1u << MG_SB) - 1u));
+            st[pos] = bt[i];
+            sk[pos] = ((uint32_t)bj[i] << MG_SB) | (uint32_t)i;
+        }
+        __syncthreads();
+        RQ_MG_TICK(3);
+        // ---- rank inside the bucket, written out in play order ----
+        for (int i = tid; i < (int)nr; i += MG_B) {
+            const double x = st[i];
+            const uint32_t kx = sk[i];
+            const int sb = sub_of(x, t_lo, scale);
+            const int g0 = (int)bbase[sb], g1 = (int)bbase[sb + 1];
+            int r = 0;
+            for (int k = g0; k < g1; ++k) {
+                const double y = st[k];
+                r += (y < x || (y == x && sk[k] < kx)) ? 1 : 0;
+            }
+            out_t[outpos + g0 + r] = x;
+            out_j[outpos + g0 + r] = (uint16_t)(kx >> MG_SB);
+        }
+        RQ_MG_TICK(6);
+        outpos += nr;
+        // next cut: aim at MG_TARGET arrivals, grow at most 4x per round
+        const double wdt = tau - t_lo;
+        const double f = (double)MG_TARGET / (double)(nr > 64 ? nr : 64);
+        span = wdt * (f < 4.0 ? f : 4.0);
+        t_lo = t_next;   // the heads after the walk (an equal-time round: t_lo again)
+    }
+#ifdef RQ_PHASE_CLOCK
+    // phases: 0 walk, 1 barrier after the walk, 2 bucket scan, 3 scatter, 6 rank + write;
+    // 4 rounds, 5 retried rounds
+    if (a.clk && w == 0 && lane == 0)
+        for (int k = 0; k < 8; ++k) atomicAdd(&a.clk[k], ck[k]);
+#endif
+#undef RQ_MG_TICK
+    if (tid == 0) {
+        a.out_len[rl] = (int)outpos;
+        if (status) atomicOr(&a.status[a.chunk0 + rl], status);
+    }
+}
+
+hipError_t rq_launch_merge(const MergeArgs& a, hipStream_t s)
+{
+    if (a.n_chunk <= 0) return hipSuccess;
+    if (a.n_str > MG_B) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(rq_merge_streams, dim3((unsigned)a.n_chunk), dim3(MG_B), 0, s, a);
+    return hipGetLastError();
+}

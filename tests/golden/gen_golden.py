@@ -619,9 +619,11 @@ def gen_c3_dist(n, start=0, procs=0):
         old = np.load(path)["data"]
         assert old.shape[0] == start, (old.shape, start)
         res = np.concatenate([old, res])
-    np.savez_compressed(os.path.join(HERE, "dist_c3.npz"), data=res,
+    tmp = path + ".tmp.npz"   # written whole, then renamed: a reader never sees half a file
+    np.savez_compressed(tmp, data=res,
                         cols=np.asarray(["posts", "world", "events", "top1", "avg"]),
                         seed_stride=np.asarray([C3_SEED_STRIDE]))
+    os.replace(tmp, path)
 
 
 G120_SEED_STRIDE = 20000   # > 99 x the broadcaster count: no shared streams

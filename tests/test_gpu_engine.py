@@ -42,7 +42,7 @@ def _oracle(O, so, ctrl, Ks, max_events=None):
     return met, t, s
 
 
-MODES = ["fast", "scatter", "log", "legacy", "fastlog", "legacylog"]
+MODES = ["fast", "scatter", "log", "legacy", "fastlog", "legacylog", "window", "windowlog"]
 
 
 def _mode_kw(mode):
@@ -51,14 +51,19 @@ def _mode_kw(mode):
     (sweep_mode=2), events compared too; legacy: pre-generated streams + serial
     wave-min merge (sweep_mode=4); fastlog: the fused sweep writing the event log
     itself (event_log=True, auto mode), events compared too; legacylog: the general
-    (pre-generated streams) fast sweep writing the event log (sweep_mode=4)."""
+    (pre-generated streams) fast sweep writing the event log (sweep_mode=4).
+    legacy / legacylog play the streams merged by rq_merge_streams; window /
+    windowlog (sweep_mode=6) the same general sweep merging the streams itself
+    (per-source register windows)."""
+    if mode == "windowlog":
+        return dict(event_log=True, sweep_mode=6)
     if mode == "log":
         return dict(event_log=True, sweep_mode=2)
     if mode == "fastlog":
         return dict(event_log=True, sweep_mode=0)
     if mode == "legacylog":
         return dict(event_log=True, sweep_mode=4)
-    return dict(event_log=False, sweep_mode={"scatter": 3, "legacy": 4}.get(mode, 0))
+    return dict(event_log=False, sweep_mode={"scatter": 3, "legacy": 4, "window": 6}.get(mode, 0))
 
 
 def _cmp_replica(res, i, met_o, t_o, s_o, Ks):
