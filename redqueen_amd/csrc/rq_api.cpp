@@ -46,7 +46,15 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // stream around every kernel, summed by rq_timing_read.  Off by default.
 enum { K_GEN = 0, K_SWEEP = 1, K_SCAN = 2, K_REPLAY = 3, K_MERGE = 4, K_N = 5 };
 bool g_timing = false;
-unsigned long long* g_clk = nullptr;   // RQ_PHASE_CLOCK builds: the sweep's phase clocks
+unsigned long long* g_clk = nullptr;   // RQ_PHASE_CLOCK builds: the sweep's / merge's phase clocks
+#ifdef RQ_PHASE_CLOCK
+unsigned long long* phase_clk()
+{
+    if (!g_clk && hipMalloc(&g_clk, 8 * sizeof(unsigned long long)) == hipSuccess)
+        (void)hipMemset(g_clk, 0, 8 * sizeof(unsigned long long));
+    return g_clk;
+}
+#endif
 
 std::vector<std::pair<hipEvent_t, hipEvent_t>> g_ev[K_N];
 
@@ -926,13 +934,7 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             ma.out_len = (int*)(ws + p.off_mlen);
             ma.status = out->status;
 #ifdef RQ_PHASE_CLOCK
-            {
-                static unsigned long long* clk = nullptr;
-                if (!clk && hipMalloc(&clk, 8 * sizeof(unsigned long long)) == hipSuccess)
-                    (void)hipMemset(clk, 0, 8 * sizeof(unsigned long long));
-                ma.clk = clk;
-                g_clk = clk;
-            }
+            ma.clk = phase_clk();
 #endif
             TimedLaunch tl(K_MERGE, s);
             if (rq_launch_merge(ma, s) != hipSuccess) return RQ_EHIP;
@@ -1039,13 +1041,7 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             sa.fw_hfill = p.fw_h;
             if (const char* e = getenv("RQ_FW_HFILL")) sa.fw_hfill = std::max(1, std::min(p.gwin, atoi(e)));   // tuning only
 #ifdef RQ_PHASE_CLOCK
-            {
-                static unsigned long long* clk = nullptr;
-                if (!clk && hipMalloc(&clk, 8 * sizeof(unsigned long long)) == hipSuccess)
-                    (void)hipMemset(clk, 0, 8 * sizeof(unsigned long long));
-                sa.clk = clk;
-                g_clk = clk;
-            }
+            sa.clk = phase_clk();
 #endif
             sa.lds_total = p.g_total;
             sa.lds_stage_off = p.g_stage_off;

@@ -115,7 +115,7 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
     extern __shared__ double lds_g[];
     char* base = reinterpret_cast<char*>(lds_g);
     const int lane = lane_id();
-    const int w = threadIdx.x >> 6;
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // wave-uniform: SGPR addressing
     int* cptr = reinterpret_cast<int*>(base + a.lds_ptr);
     int* odf = reinterpret_cast<int*>(base + a.lds_odf);
     int* cbf = reinterpret_cast<int*>(base + a.lds_cbf);

@@ -7,7 +7,8 @@
 // ~10x the algorithmic read bytes).  Here one block per replica merges them once:
 //
 //   thread j owns source j (<= RQ_MG_B sources) and reads its stream in aligned
-//   64-byte chunks (one chunk in use, the next in flight), so every line is read once;
+//   64-byte chunks (two in registers, the next load issued between rounds), so every
+//   line is read once;
 //   rounds: every arrival before a cut tau (tau adapts so a round holds ~MG_TARGET)
 //   goes to an LDS buffer with its time sub-bucket (M equal slices of [t_lo, tau),
 //   a monotone map of t) and its slot in that bucket (LDS atomics), a block scan of the
@@ -38,28 +39,36 @@ constexpr int MG_W = MG_B / 64;
 constexpr int MG_CAP = 2048;        // arrivals per round (LDS buffer)
 constexpr int MG_M = 2048;          // time sub-buckets per round
 constexpr int MG_TARGET = 1536;     // arrivals a round aims at
-#ifndef RQ_MG_PF
-#define RQ_MG_PF 1                  // stream chunks in flight ahead of the one in use
-#endif
 constexpr int MG_SB = 11;           // bits of a slot / buffer index (< MG_CAP)
 
 static_assert(MG_CAP <= (1 << MG_SB) && MG_M <= (1 << MG_SB), "packed fields");
 static_assert(MG_M == 4 * MG_B, "the bucket scan gives each thread 4 buckets");
 
-__device__ __forceinline__ double sel8(const double (&c)[8], int k)
+// eight consecutive arrivals of one stream (a 64-byte aligned chunk)
+struct Chunk {
+    double4 a, b;
+};
+
+__device__ __forceinline__ double sel8(Chunk c, int k)
 {
-    const double a0 = (k & 1) ? c[1] : c[0], a1 = (k & 1) ? c[3] : c[2];
-    const double a2 = (k & 1) ? c[5] : c[4], a3 = (k & 1) ? c[7] : c[6];
+    const double a0 = (k & 1) ? c.a.y : c.a.x, a1 = (k & 1) ? c.a.w : c.a.z;
+    const double a2 = (k & 1) ? c.b.y : c.b.x, a3 = (k & 1) ? c.b.w : c.b.z;
     const double b0 = (k & 2) ? a1 : a0, b1 = (k & 2) ? a3 : a2;
     return (k & 4) ? b1 : b0;
 }
 
-__device__ __forceinline__ void load8(double (&c)[8], const double* p)
+__device__ __forceinline__ Chunk load_chunk(const double* p)
 {
-    const double4* q = reinterpret_cast<const double4*>(p);   // 64-byte aligned chunk
-    const double4 x = q[0], y = q[1];
-    c[0] = x.x; c[1] = x.y; c[2] = x.z; c[3] = x.w;
-    c[4] = y.x; c[5] = y.y; c[6] = y.z; c[7] = y.w;
+    const double4* q = reinterpret_cast<const double4*>(p);
+    return Chunk{q[0], q[1]};
+}
+
+// arrival k (0..15) of the two chunks; both halves selected as values (a select of the
+// chunks themselves would put them in scratch memory)
+__device__ __forceinline__ double sel16(Chunk c, Chunk nx, int k)
+{
+    const double x0 = sel8(c, k & 7), x1 = sel8(nx, k & 7);
+    return (k & 8) ? x1 : x0;
 }
 
 // sub-bucket of t in [t_lo, tau): non-decreasing in t (a NaN scale -- tau one ulp
@@ -94,37 +103,27 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
         L = a.slen[rl * a.n_str + j];
         src = a.streams + rl * a.capsum + a.st_off[j];
     }
-    // the aligned chunk holding position p, and the next RQ_MG_PF ones (in flight)
-    double c[8], nx[8];
-#if RQ_MG_PF > 1
-    double nx2[8];
-#endif
-    int p = 0;
-    auto reload = [&](int p0) __attribute__((always_inline)) {
-        const int c0 = p0 & ~7;
-        if (c0 < L) load8(c, src + c0);
-        if (c0 + 8 < L) load8(nx, src + c0 + 8);
-#if RQ_MG_PF > 1
-        if (c0 + 16 < L) load8(nx2, src + c0 + 16);
-#endif
-    };
-    reload(0);
-    double head = L > 0 ? c[0] : RQ_INF;
-    auto consume = [&]() __attribute__((always_inline)) {
-        ++p;
-        if ((p & 7) == 0) {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) c[k] = nx[k];
-#if RQ_MG_PF > 1
-#pragma unroll
-            for (int k = 0; k < 8; ++k) nx[k] = nx2[k];
-            if (p + 16 < L) load8(nx2, src + p + 16);
-#else
-            if (p + 8 < L) load8(nx, src + p + 8);
-#endif
-        }
-        head = p < L ? sel8(c, p & 7) : RQ_INF;
-    };
+    // the stream's aligned chunks [p8, p8 + 8) in c and [p8 + 8, p8 + 16) in nx, with
+    // p8 <= p < p8 + 16: a round's walk reads registers only; after the walk a lane that
+    // moved into nx shifts it down and issues the load of the next chunk, which has the
+    // rest of the round to arrive (a lane that runs through both chunks inside one walk
+    // -- a burst -- loads synchronously)
+    // (loads are unconditional, clamped to the stream's last chunk -- or to the buffer's
+    // start for an empty stream -- so they land straight in c / nx and are waited for
+    // only where the values are used)
+    Chunk c, nx;
+    int p = 0, p8 = 0;
+    const int lastc = L > 0 ? (L - 1) & ~7 : 0;
+#define RQ_MG_CHUNK(q) load_chunk(src + ((q) < lastc ? (q) : lastc))
+#define RQ_MG_RELOAD(p0)                 \
+    do {                                 \
+        p8 = (p0) & ~7;                  \
+        c = RQ_MG_CHUNK(p8);             \
+        nx = RQ_MG_CHUNK(p8 + 8);        \
+    } while (0)
+#define RQ_MG_HEAD() (p < L ? sel16(c, nx, p - p8) : RQ_INF)
+    RQ_MG_RELOAD(0);
+    double head = L > 0 ? c.a.x : RQ_INF;
 
     for (int k = tid; k < MG_M; k += MG_B) cnt[k] = 0;
     if (tid == 0) nb = 0;
@@ -190,7 +189,9 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
                     bt[idx] = head;
                     bj[idx] = (uint16_t)j;
                     bs[idx] = ((uint32_t)sb << MG_SB) | slot;
-                    consume();
+                    ++p;
+                    if (p - p8 == 16 && p < L) RQ_MG_RELOAD(p);   // a burst: both chunks consumed
+                    head = RQ_MG_HEAD();
                 } else {
                     more = false;
                 }
@@ -199,6 +200,11 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
         {
             const double m = wave_min_f64(head);
             if (lane == 0) wmin[w] = m;
+        }
+        if (p - p8 >= 8) {   // into nx: its successor's load overlaps the rest of the round
+            c = nx;
+            p8 += 8;
+            nx = RQ_MG_CHUNK(p8 + 8);
         }
         RQ_MG_TICK(0);
         __syncthreads();
@@ -209,8 +215,8 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
             if (tau != next_up(t_lo)) {
                 // too many for one round: undo it and halve the cut
                 p = p0;
-                reload(p0);
-                head = p < L ? sel8(c, p & 7) : RQ_INF;
+                RQ_MG_RELOAD(p0);
+                head = RQ_MG_HEAD();
                 for (int k = tid; k < MG_M; k += MG_B) cnt[k] = 0;
                 __syncthreads();
                 if (tid == 0) nb = 0;
@@ -288,6 +294,9 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
         for (int k = 0; k < 8; ++k) atomicAdd(&a.clk[k], ck[k]);
 #endif
 #undef RQ_MG_TICK
+#undef RQ_MG_HEAD
+#undef RQ_MG_RELOAD
+#undef RQ_MG_CHUNK
     if (tid == 0) {
         a.out_len[rl] = (int)outpos;
         if (status) atomicOr(&a.status[a.chunk0 + rl], status);
