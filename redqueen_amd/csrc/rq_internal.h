@@ -141,6 +141,10 @@ struct MergeArgs {
 #ifndef RQ_MRG_LB
 #define RQ_MRG_LB 1024
 #endif
+// wall events per branch-free batch of the merged-stream K = 1 sink-bit sweep
+#ifndef RQ_MRG_BLB
+#define RQ_MRG_BLB 4
+#endif
 #define RQ_MG_B 512         // merge block: one source per thread (the fast general sweep: <= 512)
 
 struct ScanArgs {

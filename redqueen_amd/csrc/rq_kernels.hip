@@ -696,19 +696,21 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
                         ++q;
                         continue;
                     }
-                    // events q .. q+m-1: no break after q, at most 8
+                    // events q .. q+m-1: no break after q, at most BLB (8; the merged-stream
+                    // instances 4 -- RQ_MRG_BLB -- so the batch fits their 128 VGPRs)
+                    constexpr int BLB = MRG ? RQ_MRG_BLB : 8;
                     const uint64_t rest = (brk >> q) & ~1ull;
                     int m = rest ? __builtin_ctzll(rest) : 64 - q;
-                    m = m < 8 ? m : 8;
+                    m = m < BLB ? m : BLB;
                     // straight-line batch: every slot loads and issues its atomics (slots
                     // past m and lanes past the event's sinks: index 0, no-op masks), so the
                     // compiler keeps the 16 loads and then the atomics in flight together
                     auto batch = [&](auto vf) __attribute__((always_inline)) {
                         constexpr bool VF = decltype(vf)::value;   // V all ones: leave it
-                        int ca[8], cb[8];
-                        bool aa[8], ab[8];
+                        int ca[BLB], cb[BLB];
+                        bool aa[BLB], ab[BLB];
 #pragma unroll
-                        for (int k = 0; k < 8; ++k) {
+                        for (int k = 0; k < BLB; ++k) {
                             const int f0 = bcast_i(e0, q + k < 64 ? q + k : 63);
                             const int f1 = k < m ? bcast_i(e1, q + k) : f0;
                             aa[k] = f0 + lane < f1;
@@ -716,9 +718,9 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
                             ca[k] = colat(aa[k] ? f0 + lane : 0);
                             cb[k] = colat(ab[k] ? f0 + 64 + lane : 0);
                         }
-                        uint32_t ta[8], tb[8], va[8], vb[8];
+                        uint32_t ta[BLB], tb[BLB], va[BLB], vb[BLB];
 #pragma unroll
-                        for (int k = 0; k < 8; ++k) {
+                        for (int k = 0; k < BLB; ++k) {
                             const uint32_t ba = aa[k] ? 1u << (ca[k] & 31) : 0u;
                             const uint32_t bb = ab[k] ? 1u << (cb[k] & 31) : 0u;
                             const int wa = aa[k] ? ca[k] >> 5 : nopw;
@@ -731,7 +733,7 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
                             }
                         }
 #pragma unroll
-                        for (int k = 0; k < 8; ++k) {
+                        for (int k = 0; k < BLB; ++k) {
                             if (k < m) {
                                 const int qk = q + k;
                                 ag.cnt[0] -= popc(__ballot(ta[k] != 0u)) + popc(__ballot(tb[k] != 0u));
