@@ -160,8 +160,11 @@ typedef struct rq_batch_desc {
                                     log themselves; 1 fast whenever max_events allows; 2 force the sequential sweep;
                                     3 as 0 but never a K=1 sink-bit variant (per-sink ranks);
                                     4 / 5 as 0 / 1 on the legacy kernels (arrival streams
-                                    pre-generated into HBM by rq_gen_streams, serial wave-min
-                                    merge) -- kept for A/B parity checks of the fused sweep  */
+                                    pre-generated into HBM by rq_gen_streams and merged into one
+                                    (t, source) sequence per replica by rq_merge_streams) --
+                                    kept for A/B parity checks of the fused sweep;
+                                    6 as 4, the general sweep merging the per-source streams
+                                    itself (register windows; the round-2 kernel)            */
                                  /* sweep; both are bit-identical, auto picks the faster one    */
     /* RQ_SRC_OPTPW (create_manager_with_significance, opt_model.py:850-884): the follower
        significance s_pw[g][f][k] over n_seg equal segments of time_period, rows in the

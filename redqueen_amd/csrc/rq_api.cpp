@@ -1198,6 +1198,9 @@ int rp_run(const double* t, const int64_t* src, const int64_t* sink, const int64
     a.gstate = large ? (void*)(ws + p.off_gstate) : nullptr;
     a.metrics = out;
     a.counts = counts;
+    // the small-table tier (two workgroups per CU) first, for one K; A/B knob RQ_RP_SMALL
+    a.first_tier = nK == 1 ? 0 : 1;
+    if (const char* e = getenv("RQ_RP_SMALL")) a.first_tier = (nK == 1 && atoi(e) != 0) ? 0 : 1;   // A/B only
     if (chunked) {
         a.chunked = 1;
         a.max_chunks = p.max_chunks;
@@ -1213,6 +1216,7 @@ int rp_run(const double* t, const int64_t* src, const int64_t* sink, const int64
     {
         TimedLaunch tl(K_REPLAY, s);
         if (chunked && rq_launch_rp(a, RP_PHASE_CHUNK, s) != hipSuccess) return RQ_EHIP;
+        if (a.first_tier == 0 && rq_launch_rp(a, RP_PHASE_SMALL, s) != hipSuccess) return RQ_EHIP;
         if (rq_launch_rp(a, RP_PHASE_FAST, s) != hipSuccess) return RQ_EHIP;
         if (large && rq_launch_rp(a, RP_PHASE_GLOBAL, s) != hipSuccess) return RQ_EHIP;
         if (rq_launch_rp(a, RP_PHASE_KEYS, s) != hipSuccess) return RQ_EHIP;

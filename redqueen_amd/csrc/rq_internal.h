@@ -208,10 +208,11 @@ struct RpInfo {
 #define RP_BIG 16        // needs the large workspace (or exceeds it)
 #define RP_EMPTYDF 32    // no rows
 #define RP_BADOFF 64     // df_off[d] .. df_off[d + 1] is not a valid row range (< 2^31 rows)
+#define RP_MID 256       // more unique sinks than the small LDS table: the full-table pass takes it
 #define RP_CSKIP 128     // chunked mode: the df is not chunkable (> RC_S sinks, the INT64_MIN id):
                          // the one-workgroup path (rq_rp_fast) takes it
 enum { RP_PHASE_FAST = 0, RP_PHASE_GLOBAL = 1, RP_PHASE_KEYS = 2, RP_PHASE_SEQ = 3, RP_PHASE_SCAN = 4,
-       RP_PHASE_CHUNK = 5 };
+       RP_PHASE_CHUNK = 5, RP_PHASE_SMALL = 6 };
 // chunked replay (one dataframe over many workgroups): rows per chunk, most unique sinks
 // per dataframe, hash slots per dataframe
 #define RC_L 4096
@@ -254,6 +255,7 @@ struct RpArgs {
     // chunked mode (RP_PHASE_CHUNK; null otherwise): per df chunk prefix [n_df + 1], hash
     // tables [n_df][RC_HT], per chunk the group base, carries / entering states [chunk][RC_S]
     int chunked;
+    int first_tier;         // 0: the small-table pass runs first (RP_PHASE_SMALL), 1: the full-table pass
     int64_t max_chunks;
     int64_t* cbase;
     uint64_t* ht_keys;

@@ -61,6 +61,13 @@ constexpr int RP_H = 4 * RP_B;          // LDS hash slots
 constexpr int RP_LOG_H = RP_B == 1024 ? 12 : RP_B == 512 ? 11 : 10;
 constexpr int RP_HMAX = RP_H - RP_B - 1;   // unique sinks the LDS table takes: a batch can
                                            // insert RP_B more and still leave an empty slot
+// the small tier: a half-size LDS table (<= RP_B - 1 unique sinks) and <= 64 VGPRs, so two
+// workgroups share a CU and one's barriers overlap the other's work; wider dataframes
+// (or nK > RP_SMALL_NK) go on to the full table, then the global one
+constexpr int RP_HS = 2 * RP_B;
+constexpr int RP_LOG_HS = RP_LOG_H - 1;
+constexpr int RP_HMAX_S = RP_HS - RP_B - 1;
+constexpr int RP_SMALL_NK = 1;
 constexpr uint64_t RP_EMPTY_KEY = 0x8000000000000000ull;   // INT64_MIN: gets its own slot
 
 struct alignas(16) RpSlot {
@@ -171,21 +178,25 @@ struct RpAcc {
 // ============================================================================
 // rq_rp_fast: one workgroup per dataframe
 // ============================================================================
-template <int NK, bool GLOBAL>
-__global__ __launch_bounds__(RP_B) void rq_rp_fast(RpArgs a)
+// TIER 0: small LDS table (first pass), 1: full LDS table (the dataframes tier 0 gave up:
+// RP_MID), 2: global table (those tier 1 gave up: RP_GLOBAL)
+template <int NK, int TIER>
+__device__ __forceinline__ void rp_fast_body(RpArgs a)
 {
+    constexpr bool GLOBAL = TIER == 2;
     const int64_t d = blockIdx.x;
     const int tid = threadIdx.x;
     const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
     RpInfo* inf = a.info + d;
     if (GLOBAL && !(inf->flags & RP_GLOBAL)) return;   // only the dataframes the LDS pass gave up
-    if (!GLOBAL && a.chunked && !(inf->flags & RP_CSKIP)) return;   // the chunked pass took it
+    if (TIER == 1 && a.first_tier == 0 && !(inf->flags & RP_MID)) return;   // ... the small pass gave up
+    if (TIER == a.first_tier && a.chunked && !(inf->flags & RP_CSKIP)) return;   // the chunked pass took it
     const int64_t r0 = df_begin(a, d), r1 = df_end(a, d);
     const int64_t nd = r1 - r0;
     // a malformed caller range (decreasing / negative offsets, past n_rows, >= 2^31 rows:
     // the row positions below are int) touches no workspace; rq_rp_scan reports RQ_EINVAL
     if (r0 < 0 || r1 < r0 || r1 > a.n_rows || nd >= ((int64_t)1 << 31)) {
-        if (!GLOBAL && tid == 0) {
+        if (TIER == a.first_tier && tid == 0) {
             inf->flags = RP_BADOFF;
             inf->n_piv = 0;
             inf->n_own = 0;
@@ -221,16 +232,17 @@ __global__ __launch_bounds__(RP_B) void rq_rp_fast(RpArgs a)
         tkeys = reinterpret_cast<unsigned long long*>(a.gkeys) + 4 * r0;
         tst = reinterpret_cast<RpSlot*>(a.gstate) + 4 * r0;
     } else {
-        tbits = RP_LOG_H;
-        tcap = RP_H;
-        tkeys = reinterpret_cast<unsigned long long*>(carve(8 * (RP_H + 1)));
-        tst = reinterpret_cast<RpSlot*>(carve(sizeof(RpSlot) * (RP_H + 1)));
+        constexpr int H = TIER == 0 ? RP_HS : RP_H;
+        tbits = TIER == 0 ? RP_LOG_HS : RP_LOG_H;
+        tcap = H;
+        tkeys = reinterpret_cast<unsigned long long*>(carve(8 * (H + 1)));
+        tst = reinterpret_cast<RpSlot*>(carve(sizeof(RpSlot) * (H + 1)));
     }
     tmask = (uint32_t)(tcap - 1);
     // misc: [0] unique sinks, [1] sentinel-key seen, [2] dup, [3] unsorted, [4] eid bad,
     //       [5] own events, [6] world events, [7] key dump cursor, [8] bucket allocator
     if (tid < 16) misc[tid] = 0;
-    if (!GLOBAL && tid == 0) inf->flags = 0;   // this call's status (the LDS pass runs first)
+    if (TIER == a.first_tier && tid == 0) inf->flags = 0;   // this call's status (the first pass)
     for (int64_t h = tid; h <= tcap; h += RP_B) {
         tkeys[h] = RP_EMPTY_KEY;
         tst[h] = RpSlot{0, 0, -1, 0};
@@ -346,7 +358,7 @@ __global__ __launch_bounds__(RP_B) void rq_rp_fast(RpArgs a)
             ev_own = fe && own;
             ev_world = fe && !own;
         }
-        if (!GLOBAL && misc[0] > RP_HMAX) aborted = true;   // uniform: read after the barrier
+        if (!GLOBAL && misc[0] > (TIER == 0 ? RP_HMAX_S : RP_HMAX)) aborted = true;   // uniform: read after the barrier
 
         // ---- B: t-group of every row (block scan of group starts) + event counts;
         //      buckets of more than one row get list space ----
@@ -481,7 +493,7 @@ __global__ __launch_bounds__(RP_B) void rq_rp_fast(RpArgs a)
 
     __syncthreads();
     if (aborted) {
-        if (tid == 0) atomicOr(&inf->flags, RP_GLOBAL);
+        if (tid == 0) atomicOr(&inf->flags, TIER == 0 ? RP_MID : RP_GLOBAL);
         return;
     }
     const int S = misc[0];
@@ -511,6 +523,17 @@ __global__ __launch_bounds__(RP_B) void rq_rp_fast(RpArgs a)
             }
         }
     }
+}
+
+template <int NK, bool GLOBAL>
+__global__ __launch_bounds__(RP_B) void rq_rp_fast(RpArgs a)
+{
+    rp_fast_body<NK, GLOBAL ? 2 : 1>(a);
+}
+template <int NK>
+__global__ __launch_bounds__(RP_B) __attribute__((amdgpu_waves_per_eu(8, 8))) void rq_rp_fast_s(RpArgs a)
+{
+    rp_fast_body<NK, 0>(a);
 }
 
 // ============================================================================
@@ -1501,13 +1524,14 @@ __global__ __launch_bounds__(256) void rq_rp_scan(RpArgs a)
 // launch wrappers
 // ============================================================================
 namespace {
-template <bool GLOBAL>
+template <int TIER>
 size_t rp_fast_lds(int nK)
 {
     auto al = [](size_t b) { return (b + 15) & ~(size_t)15; };
     size_t s = al(8 * (RP_B + 2)) + al(8 * (RP_B + 1)) + al(4 * RP_B) + al(RP_B) + al(4 * RP_B) +
                al(8 * 16) + al(4 * 16 * (nK + 6)) + al(4 * 16);
-    if (!GLOBAL) s += al(8 * (RP_H + 1)) + al(sizeof(RpSlot) * (RP_H + 1));
+    const size_t h = TIER == 0 ? RP_HS : RP_H;
+    if (TIER < 2) s += al(8 * (h + 1)) + al(sizeof(RpSlot) * (h + 1));
     return s;
 }
 
@@ -1523,13 +1547,19 @@ hipError_t rp_launch_t(const RpArgs& a, int phase, hipStream_t s)
 {
     const unsigned nd = (unsigned)a.n_df;
     switch (phase) {
+    case RP_PHASE_SMALL:
+        if constexpr (NK <= RP_SMALL_NK) {
+            const size_t lds = rp_fast_lds<0>(NK);
+            hipLaunchKernelGGL((rq_rp_fast_s<NK>), dim3(nd), dim3(RP_B), lds, s, a);
+        }
+        break;
     case RP_PHASE_FAST: {
-        const size_t lds = rp_fast_lds<false>(NK);
+        const size_t lds = rp_fast_lds<1>(NK);
         hipLaunchKernelGGL((rq_rp_fast<NK, false>), dim3(nd), dim3(RP_B), lds, s, a);
         break;
     }
     case RP_PHASE_GLOBAL: {
-        const size_t lds = rp_fast_lds<true>(NK);
+        const size_t lds = rp_fast_lds<2>(NK);
         hipLaunchKernelGGL((rq_rp_fast<NK, true>), dim3(nd), dim3(RP_B), lds, s, a);
         break;
     }

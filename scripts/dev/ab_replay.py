@@ -29,12 +29,13 @@ def timed(fn, reps):
 
 so = graphs.c3()
 g = engine.Graph(so["src_id"], so["other_sources"], so["sink_ids"], so["edge_list"], so["end_time"])
-r2 = g.run("opt", q=so["q"], s=so["s"], n_rep=256, ctrl_seed=0, world_seed=0, randomize=True, event_log=True)
+NDF = int(os.environ.get("RQ_AB_NDF", "256"))   # dataframes in the batch
+r2 = g.run("opt", q=so["q"], s=so["s"], n_rep=NDF, ctrl_seed=0, world_seed=0, randomize=True, event_log=True)
 ro, cols = r2.log_columns()
 off = torch.from_numpy(ro).cuda()
 nrow = int(ro[-1])
 res = {"so": os.environ.get("RQ_SO_PATH", "librq.so")}
-for tag, ck in (("batch", False), ("batch_chunked", True)):
+for tag, ck in (("batch", False),) + ((("batch_chunked", True),) if NDF <= 256 else ()):
     if ck:
         os.environ["RQ_RP_CHUNK"] = "1"
     (m, c), ms = timed(lambda: utils.replay_columns(cols["t"], cols["src_id"], cols["sink_id"], cols["event_id"],
