@@ -242,7 +242,7 @@ def main():
     rows_step = rows_l / a.steps
     posts_step = posts_l / a.steps
     # the fused sweep (variant >= 10) generates its arrivals in LDS: no arrival reads
-    fused = plan["variant"] >= 10
+    fused = 10 <= plan["variant"] < 20   # 20+: the fused sweep on merged streams (reads them)
     merged = not fused and plan["sources_per_lane"] == 0   # rq_merge_streams feeds the sweep
     b_wall = MRG_SWEEP_B_PER_WALL_EVENT if merged else SWEEP_B_PER_WALL_EVENT
     sweep_bytes = (0 if fused else b_wall * (ev_rank - posts_step)) + \

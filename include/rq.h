@@ -164,7 +164,9 @@ typedef struct rq_batch_desc {
                                     (t, source) sequence per replica by rq_merge_streams) --
                                     kept for A/B parity checks of the fused sweep;
                                     6 as 4, the general sweep merging the per-source streams
-                                    itself (register windows; the round-2 kernel)            */
+                                    itself (register windows; the round-2 kernel);
+                                    7 as 0, the fused sweep generating its arrivals in-kernel
+                                    (LDS rings) instead of playing merged streams            */
                                  /* sweep; both are bit-identical, auto picks the faster one    */
     /* RQ_SRC_OPTPW (create_manager_with_significance, opt_model.py:850-884): the follower
        significance s_pw[g][f][k] over n_seg equal segments of time_period, rows in the

@@ -162,6 +162,9 @@ struct Plan {
     // per-source merge inside the sweep instead)
     bool mrg = false;
     size_t off_mt = 0, off_mj = 0, off_mlen = 0;
+    // the fused sweep's phases B / C on merged streams (rq_gen_streams + rq_merge_streams
+    // instead of in-kernel generation; sweep_mode 7: the in-kernel generating sweep)
+    bool fwm = false;
     // general sweep LDS layout
     int gwpb = 4, gwin = 16, gcol_lds = 1, gcol16 = 0;
     size_t g_col = 0, g_ptr = 0, g_odf = 0, g_cbf = 0, g_wave = 0, g_wave_stride = 0, g_rank_off = 0,
@@ -417,6 +420,8 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     const bool pw = b->ctrl_kind == RQ_SRC_OPTPW;
     p->fw = !p->log && !p->bl && g->n_str <= 64 && b->sweep_mode != 4 && b->sweep_mode != 5 &&
             b->sweep_mode != 6;
+    p->fwm = p->fw && !pw && b->sweep_mode != 7;
+    if (const char* e = getenv("RQ_FWM")) p->fwm = p->fwm && atoi(e) != 0;   // A/B only
     if (p->fw) {
         int best = -1;
         const int c16 = p->bits ? 1 : (g->n_sinks <= 65535 ? 1 : 0);
@@ -442,12 +447,13 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
             const size_t r_off = align_up(8 * (size_t)g->n_str, 16);
             // per wave: BITS -> (F, T) word pairs [nw]; else int16 sink ranks
             const size_t w_off = align_up(r_off + (p->bits ? 8 * (size_t)((g->nw + 1) & ~1) : 2 * (size_t)p->n_sinks_pad), 16);
-            const size_t s_off = align_up(w_off + 8 * (size_t)g->n_str * (W + 1), 16);
+            // merged streams: no arrival rings
+            const size_t s_off = align_up(w_off + (p->fwm ? 0 : 8 * (size_t)g->n_str * (W + 1)), 16);
             const size_t stride = align_up(s_off + 64 * 12, 16);
             for (int wpb : {16, 12, 10, 8, 6, 5, 4, 3, 2, 1}) {
                 const size_t tot = sh + wpb * stride;
                 if (tot > kLdsMax) continue;
-                int blocks = rq_fw_blocks_per_cu(p->nK, c16, W, p->bits, wpb, tot, pw);
+                int blocks = rq_fw_blocks_per_cu(p->nK, c16, p->fwm ? 0 : W, p->bits, wpb, tot, pw);
                 if (blocks <= 0) blocks = (int)std::min<size_t>(kLdsMax / tot, 16 / wpb);
                 const int waves = blocks * wpb;
                 const int score = waves * 4 + (W == 16 ? 2 : W == 32 ? 1 : 0);
@@ -463,7 +469,8 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
         }
         if (best < 0) p->fw = false;
     }
-    if (p->fw) p->mrg = false;
+    if (!p->fw) p->fwm = false;
+    if (p->fw) p->mrg = p->fwm;   // the merge kernel feeds the fused sweep too
 
     const size_t A = 256;
     const int64_t C = p->chunk;
@@ -478,7 +485,7 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     p->off_pwmax = o;   o = o + sizeof(double) * (nseg ? (size_t)b->n_grid * g->n_str : 0);
     p->tables_bytes = o;
     o = align_up(o, A);
-    const int64_t strm = p->fw ? 0 : C;   // the fused sweep keeps its arrivals in LDS
+    const int64_t strm = p->fw && !p->fwm ? 0 : C;   // the generating fused sweep keeps its arrivals in LDS
     p->off_streams = o; o = align_up(o + sizeof(double) * (size_t)strm * p->capsum, A);
     p->off_slen = o;    o = align_up(o + sizeof(int) * (size_t)strm * g->n_str, A);
     const int64_t mrgc = p->mrg ? C : 0;   // merged sequences: t f64, stream u16, length
@@ -752,11 +759,11 @@ int rq_plan_info(rq_graph_t g, const rq_batch_desc* b, int64_t* info)
     Plan p;
     const int rc = make_plan(g, b, &p);
     if (rc) return rc;
-    info[0] = (p.log ? (p.gs ? 4 : 1) : (p.bits ? 2 : (p.bl ? 3 : 0))) + (p.fw ? 10 : 0);
+    info[0] = (p.log ? (p.gs ? 4 : 1) : (p.bits ? 2 : (p.bl ? 3 : 0))) + (p.fwm ? 20 : p.fw ? 10 : 0);
     info[1] = p.mrg ? 0 : p.spl;   // 0: merged streams (lanes own no sources)
     info[2] = p.gwin;
     info[3] = p.gwpb;
-    info[4] = p.fw ? rq_fw_blocks_per_cu(p.nK, p.gcol16, p.gwin, p.bits, p.gwpb, p.g_total,
+    info[4] = p.fw ? rq_fw_blocks_per_cu(p.nK, p.gcol16, p.fwm ? 0 : p.gwin, p.bits, p.gwpb, p.g_total,
                                           b->ctrl_kind == RQ_SRC_OPTPW)
                    : rq_sweep_blocks_per_cu(p.mrg ? 0 : p.spl, p.nK, p.gcol16, p.gwin, p.log ? 1 + p.gs : 0,
                                             p.bl ? 2 : p.bits, p.gwpb, p.g_total);
@@ -915,7 +922,7 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             ga.rd_times = b->rd_times;
             ga.rd_off = b->rd_off;
         }
-        if (!p.fw) {
+        if (!p.fw || p.fwm) {
             TimedLaunch tl(K_GEN, s);
             if (rq_launch_gen(ga, s) != hipSuccess) return RQ_EHIP;
         }
@@ -1055,7 +1062,7 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
                 sa.wq = (int*)(ws + p.off_wq);
             }
             TimedLaunch tl(K_SWEEP, s);
-            const hipError_t e = p.fw ? rq_launch_sweep_fw(sa, p.nK, p.gcol16, p.gwin, p.bits, s)
+            const hipError_t e = p.fw ? rq_launch_sweep_fw(sa, p.nK, p.gcol16, p.fwm ? 0 : p.gwin, p.bits, s)
                                       : rq_launch_sweep(sa, p.mrg ? 0 : p.spl, p.nK, p.gcol16, p.log ? 1 + p.gs : 0,
                                                         p.bl ? 2 : p.bits, s);
             if (e != hipSuccess) return RQ_EHIP;

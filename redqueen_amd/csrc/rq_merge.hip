@@ -6,7 +6,8 @@
 // source's stream 8 bytes at a time -- the lines are evicted between touches (round 2:
 // ~10x the algorithmic read bytes).  Here one block per replica merges them once:
 //
-//   thread j owns source j (<= RQ_MG_B sources) and reads its stream in aligned
+//   thread j owns source j (<= RQ_MG_B sources; a one-wave block for <= 64) and reads
+//   its stream in aligned
 //   64-byte chunks (two in registers, the next load issued between rounds), so every
 //   line is read once;
 //   rounds: every arrival before a cut tau (tau adapts so a round holds ~MG_TARGET)
@@ -34,15 +35,17 @@ using namespace rq;
 
 namespace {
 
-constexpr int MG_B = RQ_MG_B;
-constexpr int MG_W = MG_B / 64;
-constexpr int MG_CAP = 2048;        // arrivals per round (LDS buffer)
-constexpr int MG_M = 2048;          // time sub-buckets per round
-constexpr int MG_TARGET = 1536;     // arrivals a round aims at
+// block sizes: RQ_MG_B (512) threads for 65-512 sources, one wave for <= 64 (the fused
+// sweep's worlds); per block size B: rounds of <= 4B arrivals over 4B sub-buckets
 constexpr int MG_SB = 11;           // bits of a slot / buffer index (< MG_CAP)
-
-static_assert(MG_CAP <= (1 << MG_SB) && MG_M <= (1 << MG_SB), "packed fields");
-static_assert(MG_M == 4 * MG_B, "the bucket scan gives each thread 4 buckets");
+template <int B>
+struct MgCfg {
+    static constexpr int W = B / 64;
+    static constexpr int CAP = 4 * B;       // arrivals per round (LDS buffer)
+    static constexpr int M = 4 * B;         // time sub-buckets per round (4 per thread in the scan)
+    static constexpr int TARGET = 3 * B;    // arrivals a round aims at
+    static_assert(CAP <= (1 << MG_SB) && M <= (1 << MG_SB), "packed fields");
+};
 
 // eight consecutive arrivals of one stream (a 64-byte aligned chunk)
 struct Chunk {
@@ -73,16 +76,20 @@ __device__ __forceinline__ double sel16(Chunk c, Chunk nx, int k)
 
 // sub-bucket of t in [t_lo, tau): non-decreasing in t (a NaN scale -- tau one ulp
 // above t_lo = 0 -- sends every arrival of the round to the last bucket)
+template <int M>
 __device__ __forceinline__ int sub_of(double t, double t_lo, double scale)
 {
     const double x = (t - t_lo) * scale;
-    return x < (double)(MG_M - 1) ? (int)x : MG_M - 1;
+    return x < (double)(M - 1) ? (int)x : M - 1;
 }
 
 }  // namespace
 
+template <int MG_B>
 __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
 {
+    constexpr int MG_W = MgCfg<MG_B>::W, MG_CAP = MgCfg<MG_B>::CAP, MG_M = MgCfg<MG_B>::M;
+    constexpr int MG_TARGET = MgCfg<MG_B>::TARGET;
     __shared__ double bt[MG_CAP];          // round buffer (arrival order)
     __shared__ uint32_t bs[MG_CAP];        // (sub-bucket << MG_SB) | slot
     __shared__ uint16_t bj[MG_CAP];
@@ -184,7 +191,7 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
             if (act) {
                 const uint32_t idx = b0 + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
                 if (idx < (uint32_t)MG_CAP) {
-                    const int sb = sub_of(head, t_lo, scale);
+                    const int sb = sub_of<MG_M>(head, t_lo, scale);
                     const uint32_t slot = atomicAdd(&cnt[sb], 1u);
                     bt[idx] = head;
                     bj[idx] = (uint16_t)j;
@@ -269,7 +276,7 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
         for (int i = tid; i < (int)nr; i += MG_B) {
             const double x = st[i];
             const uint32_t kx = sk[i];
-            const int sb = sub_of(x, t_lo, scale);
+            const int sb = sub_of<MG_M>(x, t_lo, scale);
             const int g0 = (int)bbase[sb], g1 = (int)bbase[sb + 1];
             int r = 0;
             for (int k = g0; k < g1; ++k) {
@@ -306,7 +313,10 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
 hipError_t rq_launch_merge(const MergeArgs& a, hipStream_t s)
 {
     if (a.n_chunk <= 0) return hipSuccess;
-    if (a.n_str > MG_B) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(rq_merge_streams, dim3((unsigned)a.n_chunk), dim3(MG_B), 0, s, a);
+    if (a.n_str > RQ_MG_B) return hipErrorInvalidValue;
+    if (a.n_str <= 64)
+        hipLaunchKernelGGL(rq_merge_streams<64>, dim3((unsigned)a.n_chunk), dim3(64), 0, s, a);
+    else
+        hipLaunchKernelGGL(rq_merge_streams<RQ_MG_B>, dim3((unsigned)a.n_chunk), dim3(RQ_MG_B), 0, s, a);
     return hipGetLastError();
 }

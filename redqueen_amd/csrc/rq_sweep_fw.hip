@@ -34,7 +34,10 @@ using namespace rq;
 //     events: per sink-bitset word, segmented prefix ORs (segments start at the
 //     posts) give each event's top-1 set, plain prefix ORs its valid set.
 // ============================================================================
-template <int NK, class COL, int W, int H, bool BITS, bool PW = false>
+// MRG: the arrivals come pre-generated (rq_gen_streams) and merged into the replica's
+// (t, stream) sequence (rq_merge_streams): a tile is its next 64 entries, loaded one tile
+// ahead, and phase A (refill passes, window cut, rank sort) disappears
+template <int NK, class COL, int W, int H, bool BITS, bool PW = false, bool MRG = false>
 __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
 {
     static_assert((W & (W - 1)) == 0 && H <= W, "ring");
@@ -108,9 +111,20 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
     } while (0)
 #endif
     SrcGen gen;
-    if (lane < a.n_str) gen.init(a.gen, lane, i, etab);
+    if (lane < a.n_str && !MRG) gen.init(a.gen, lane, i, etab);
     else gen.none();
     int pos = 0, fil = 0;   // arrivals consumed / generated by this lane's source
+    // MRG: the replica's merged sequence; lane l holds entry mpos + l of the next tile
+    const double* mt = MRG ? a.mrg_t + rl * a.capsum : nullptr;
+    const uint16_t* mj = MRG ? a.mrg_j + rl * a.capsum : nullptr;
+    const int mlen = MRG ? a.mrg_len[rl] : 0;
+    int mpos = 0;
+    double nxt_t = RQ_INF;
+    int nxt_j = 0;
+    if (MRG && lane < mlen) {
+        nxt_t = mt[lane];
+        nxt_j = mj[lane];
+    }
 
     const bool opt = a.ctrl_kind == RQ_SRC_OPT || a.ctrl_kind == RQ_SRC_OPTPW;
     // OptPWSignificance only in the PW instances: the thinning loop's registers stay out
@@ -160,6 +174,27 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
         }
     };
     for (;;) {
+        int n = 0;
+        bool act, fin;
+        double tt;
+        int tj;
+        if constexpr (MRG) {
+            if (mpos >= mlen) break;   // every arrival played
+            n = mlen - mpos < 64 ? mlen - mpos : 64;
+            act = lane < n;
+            tt = act ? nxt_t : RQ_INF;
+            tj = act ? nxt_j : 0;
+            mpos += n;
+            fin = mpos >= mlen;
+            // the next tile's loads stay in flight through phases B and C
+            nxt_t = RQ_INF;
+            nxt_j = 0;
+            if (mpos + lane < mlen) {
+                nxt_t = mt[mpos + lane];
+                nxt_j = mj[mpos + lane];
+            }
+            RQ_CLK(2);
+        } else {
         // ---- A1: opportunistic passes while >= thr rings are below W; if some unfinished
         //      ring shows < hmin arrivals, passes until every ring shows >= hfill ----
         {
@@ -188,7 +223,7 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
         const double tmax = wave_min_f64(more ? vb : RQ_INF);
 
         // ---- A2: the cut (exclusive): complete below tmax, <= 64 arrivals ----
-        int c = 0, n = 0;
+        int c = 0;
         bool trunc = !(tmax > tfirst);   // a ring's window is all at tfirst: equal-time prefix
         if (!trunc) {
             double cut = tmax;
@@ -239,7 +274,7 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
             }
         if (lane >= n) st_t[lane] = RQ_INF;   // the rank loop reads whole blocks of 8
         wave_lds_sync();
-        const bool act = lane < n;
+        act = lane < n;
         const double ti = act ? st_t[lane] : RQ_INF;
         const int ji = act ? st_j[lane] : 0;
         // rank = #staged arrivals before this one in (t, stream) order (stage_rank:
@@ -251,10 +286,12 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
             st_j[rnk] = ji;
         }
         wave_lds_sync();
-        const double tt = act ? st_t[lane] : RQ_INF;
-        const int tj = act ? st_j[lane] : 0;
+        tt = act ? st_t[lane] : RQ_INF;
+        tj = act ? st_j[lane] : 0;
         pos += c;
-        const bool fin = !__ballot(!gen.done || pos < fil);
+        fin = !__ballot(!gen.done || pos < fil);
+        RQ_CLK(2);   // A3 stage + rank sort
+        }   // !MRG
 
         int e0 = 0, e1 = 0, od = 0;
         if (act) {
@@ -262,7 +299,6 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
             e1 = cptr[tj + 1];
             od = odf[tj];
         }
-        RQ_CLK(2);   // A3 stage + rank sort
         // ---- B: RedQueen controller over the tile ----
         uint64_t ownm = 0;
         double ot = RQ_INF;
@@ -481,34 +517,40 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
 // ============================================================================
 // fused windowed sweep: (W, H) in {(16, 8), (8, 4)}; OptPWSignificance (PW) instances
 // exist for uint16 columns and W = 16 only (make_plan keeps other PW runs off this path)
-template <int NK, class COL, int W, bool BITS, bool PW = false>
+template <int NK, class COL, int W, bool BITS, bool PW = false, bool MRG = false>
 static int occ_fw_t(int wpb, size_t lds);
-template <int NK, class COL, int W, bool BITS, bool PW = false>
+template <int NK, class COL, int W, bool BITS, bool PW = false, bool MRG = false>
 static hipError_t launch_fw_t(const SweepArgs& a, hipStream_t s)
 {
     unsigned blocks = (unsigned)((a.n_chunk + a.wpb - 1) / a.wpb);
     if (a.wq) {
         // persistent grid: every resident wave slot once, the rest from the queue
-        const int nb = occ_fw_t<NK, COL, W, BITS, PW>(a.wpb, a.lds_total);
+        const int nb = occ_fw_t<NK, COL, W, BITS, PW, MRG>(a.wpb, a.lds_total);
         const unsigned cap = (unsigned)(nb > 0 ? nb : 1) * (unsigned)rq_cu_count();
         if (cap < blocks) blocks = cap;
     }
-    hipLaunchKernelGGL((rq_sweep_fw<NK, COL, W, (W > 16 ? 8 : W / 2), BITS, PW>), dim3(blocks), dim3(64 * a.wpb), a.lds_total, s, a);
+    hipLaunchKernelGGL((rq_sweep_fw<NK, COL, W, (W > 16 ? 8 : W / 2), BITS, PW, MRG>), dim3(blocks), dim3(64 * a.wpb),
+                       a.lds_total, s, a);
     return hipGetLastError();
 }
-template <class COL, int W, bool PW = false>
+template <class COL, int W, bool PW = false, bool MRG = false>
 static hipError_t launch_fw_k(const SweepArgs& a, int nK, hipStream_t s)
 {
     switch (nK) {
-    case 1: return launch_fw_t<1, COL, W, false, PW>(a, s);
-    case 2: return launch_fw_t<2, COL, W, false, PW>(a, s);
-    case 3: return launch_fw_t<3, COL, W, false, PW>(a, s);
-    default: return launch_fw_t<4, COL, W, false, PW>(a, s);
+    case 1: return launch_fw_t<1, COL, W, false, PW, MRG>(a, s);
+    case 2: return launch_fw_t<2, COL, W, false, PW, MRG>(a, s);
+    case 3: return launch_fw_t<3, COL, W, false, PW, MRG>(a, s);
+    default: return launch_fw_t<4, COL, W, false, PW, MRG>(a, s);
     }
 }
 hipError_t rq_launch_sweep_fw(const SweepArgs& a, int nK, int col16, int W, int bits, hipStream_t s)
 {
     if (a.n_chunk <= 0) return hipSuccess;
+    if (W == 0) {   // merged streams (RedQueen / Poisson / replayed controllers)
+        if (a.pw_c) return hipErrorInvalidValue;
+        if (bits) return launch_fw_t<1, uint16_t, 16, true, false, true>(a, s);
+        return col16 ? launch_fw_k<uint16_t, 16, false, true>(a, nK, s) : launch_fw_k<int, 16, false, true>(a, nK, s);
+    }
     if (a.pw_c) {
         if (!col16 || W != 16) return hipErrorInvalidValue;
         return bits ? launch_fw_t<1, uint16_t, 16, true, true>(a, s) : launch_fw_k<uint16_t, 16, true>(a, nK, s);
@@ -519,23 +561,29 @@ hipError_t rq_launch_sweep_fw(const SweepArgs& a, int nK, int col16, int W, int 
     if (W == 16) return col16 ? launch_fw_k<uint16_t, 16>(a, nK, s) : launch_fw_k<int, 16>(a, nK, s);
     return col16 ? launch_fw_k<uint16_t, 8>(a, nK, s) : launch_fw_k<int, 8>(a, nK, s);
 }
-template <int NK, class COL, int W, bool BITS, bool PW>
+template <int NK, class COL, int W, bool BITS, bool PW, bool MRG>
 static int occ_fw_t(int wpb, size_t lds)
 {
-    return rq_occupancy(rq_sweep_fw<NK, COL, W, (W > 16 ? 8 : W / 2), BITS, PW>, 64 * wpb, lds);
+    return rq_occupancy(rq_sweep_fw<NK, COL, W, (W > 16 ? 8 : W / 2), BITS, PW, MRG>, 64 * wpb, lds);
 }
-template <class COL, int W, bool PW = false>
+template <class COL, int W, bool PW = false, bool MRG = false>
 static int occ_fw_k(int nK, int wpb, size_t lds)
 {
     switch (nK) {
-    case 1: return occ_fw_t<1, COL, W, false, PW>(wpb, lds);
-    case 2: return occ_fw_t<2, COL, W, false, PW>(wpb, lds);
-    case 3: return occ_fw_t<3, COL, W, false, PW>(wpb, lds);
-    default: return occ_fw_t<4, COL, W, false, PW>(wpb, lds);
+    case 1: return occ_fw_t<1, COL, W, false, PW, MRG>(wpb, lds);
+    case 2: return occ_fw_t<2, COL, W, false, PW, MRG>(wpb, lds);
+    case 3: return occ_fw_t<3, COL, W, false, PW, MRG>(wpb, lds);
+    default: return occ_fw_t<4, COL, W, false, PW, MRG>(wpb, lds);
     }
 }
+// W = 0: the merged-stream instances
 int rq_fw_blocks_per_cu(int nK, int col16, int W, int bits, int wpb, size_t lds, int pw)
 {
+    if (W == 0) {
+        if (pw) return -1;
+        if (bits) return occ_fw_t<1, uint16_t, 16, true, false, true>(wpb, lds);
+        return col16 ? occ_fw_k<uint16_t, 16, false, true>(nK, wpb, lds) : occ_fw_k<int, 16, false, true>(nK, wpb, lds);
+    }
     if (pw) {
         if (!col16 || W != 16) return -1;
         return bits ? occ_fw_t<1, uint16_t, 16, true, true>(wpb, lds) : occ_fw_k<uint16_t, 16, true>(nK, wpb, lds);

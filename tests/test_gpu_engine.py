@@ -42,7 +42,7 @@ def _oracle(O, so, ctrl, Ks, max_events=None):
     return met, t, s
 
 
-MODES = ["fast", "scatter", "log", "legacy", "fastlog", "legacylog", "window", "windowlog"]
+MODES = ["fast", "scatter", "log", "legacy", "fastlog", "legacylog", "window", "windowlog", "gen", "genlog"]
 
 
 def _mode_kw(mode):
@@ -54,16 +54,20 @@ def _mode_kw(mode):
     (pre-generated streams) fast sweep writing the event log (sweep_mode=4).
     legacy / legacylog play the streams merged by rq_merge_streams; window /
     windowlog (sweep_mode=6) the same general sweep merging the streams itself
-    (per-source register windows)."""
+    (per-source register windows).  fast / fastlog / scatter run the fused sweep on
+    merged streams (the default); gen / genlog (sweep_mode=7) the fused sweep generating
+    its arrivals in-kernel."""
     if mode == "windowlog":
         return dict(event_log=True, sweep_mode=6)
+    if mode == "genlog":
+        return dict(event_log=True, sweep_mode=7)
     if mode == "log":
         return dict(event_log=True, sweep_mode=2)
     if mode == "fastlog":
         return dict(event_log=True, sweep_mode=0)
     if mode == "legacylog":
         return dict(event_log=True, sweep_mode=4)
-    return dict(event_log=False, sweep_mode={"scatter": 3, "legacy": 4, "window": 6}.get(mode, 0))
+    return dict(event_log=False, sweep_mode={"scatter": 3, "legacy": 4, "window": 6, "gen": 7}.get(mode, 0))
 
 
 def _cmp_replica(res, i, met_o, t_o, s_o, Ks):
@@ -191,7 +195,11 @@ def test_large_batch_no_overflow_and_determinism():
               randomize=True, Ks=(1,), sweep_mode=3)
     e = g.run("opt", q=so["q"], s=so["s"], n_rep=2048, ctrl_seed=0, world_seed=0,
               randomize=True, Ks=(1,), sweep_mode=4)
-    assert g.run("opt", q=so["q"], s=so["s"], n_rep=2048, Ks=(1,), plan_only=True)["variant"] == 12
+    f = g.run("opt", q=so["q"], s=so["s"], n_rep=2048, ctrl_seed=0, world_seed=0,
+              randomize=True, Ks=(1,), sweep_mode=7)
+    assert g.run("opt", q=so["q"], s=so["s"], n_rep=2048, Ks=(1,), plan_only=True)["variant"] == 22
+    assert g.run("opt", q=so["q"], s=so["s"], n_rep=2048, Ks=(1,), sweep_mode=7, plan_only=True)["variant"] == 12
+    assert torch.equal(a.metrics, f.metrics) and torch.equal(a.counts, f.counts)
     assert torch.equal(a.metrics, b.metrics) and torch.equal(a.counts, b.counts)
     # the fused bitset sweep, the sequential event-log variant, the rank-scatter sweep
     # and the legacy pre-generated-stream sweep are the same machine

@@ -23,12 +23,14 @@ POLICIES = [
 ]
 
 
-def _run(g, so, env, R):
+def _run(g, so, env, R, mode=7):
+    # sweep_mode 7: the fused sweep generating its arrivals in-kernel (the knobs' subject);
+    # the default (mode 0) plays merged pre-generated streams and must agree with it
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
         return g.run("opt", q=so["q"], s=so["s"], n_rep=R, ctrl_seed=300, world_seed=300,
-                     randomize=True, Ks=(1,), event_log=True, sweep_mode=0)
+                     randomize=True, Ks=(1,), event_log=True, sweep_mode=mode)
     finally:
         for k, v in old.items():
             if v is None:
@@ -47,8 +49,8 @@ def test_refill_policies_same_bits():
     g = engine.Graph(so["src_id"], so["other_sources"], so["sink_ids"], so["edge_list"], so["end_time"])
     R = 96
     base = None
-    for env in POLICIES:
-        res = _run(g, so, env, R)
+    for env in POLICIES + [None]:
+        res = _run(g, so, env or {}, R, 7 if env is not None else 0)
         assert int(res.status.max().item()) == 0, env
         got = (res.metrics.cpu().numpy(), res.counts.cpu().numpy(),
                [res.events(i) for i in range(0, R, 5)])
