@@ -180,14 +180,21 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
         const int p0 = p;
         // ---- every arrival before tau into the buffer (a lane stops at a full buffer) ----
         bool more = true;
+        uint32_t nb1 = 0;   // one-wave blocks: the buffer cursor
         for (;;) {
             const bool act = more && head < tau;
             const uint64_t m = __ballot(act);
             if (!m) break;
-            const int fl = __ffsll((unsigned long long)m) - 1;
-            uint32_t b0 = 0;
-            if (lane == fl) b0 = atomicAdd(&nb, (uint32_t)__popcll(m));
-            b0 = (uint32_t)__builtin_amdgcn_readlane((int)b0, fl);
+            uint32_t b0;
+            if constexpr (MG_W == 1) {   // one wave: the buffer cursor is a register
+                b0 = nb1;
+                nb1 += (uint32_t)__popcll(m);
+            } else {
+                const int fl = __ffsll((unsigned long long)m) - 1;
+                b0 = 0;
+                if (lane == fl) b0 = atomicAdd(&nb, (uint32_t)__popcll(m));
+                b0 = (uint32_t)__builtin_amdgcn_readlane((int)b0, fl);
+            }
             if (act) {
                 const uint32_t idx = b0 + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
                 if (idx < (uint32_t)MG_CAP) {
@@ -212,6 +219,9 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
             c = nx;
             p8 += 8;
             nx = RQ_MG_CHUNK(p8 + 8);
+        }
+        if constexpr (MG_W == 1) {
+            if (lane == 0) nb = nb1;
         }
         RQ_MG_TICK(0);
         __syncthreads();
