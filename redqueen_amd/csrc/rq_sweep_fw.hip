@@ -37,8 +37,8 @@ using namespace rq;
 // MRG: the arrivals come pre-generated (rq_gen_streams) and merged into the replica's
 // (t, stream) sequence (rq_merge_streams): a tile is its next 64 entries, loaded one tile
 // ahead, and phase A (refill passes, window cut, rank sort) disappears
-template <int NK, class COL, int W, int H, bool BITS, bool PW = false, bool MRG = false>
-__global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
+template <int NK, class COL, int W, int H, bool BITS, bool PW, bool MRG>
+__device__ __forceinline__ void sweep_fw_body(SweepArgs a)
 {
     static_assert((W & (W - 1)) == 0 && H <= W, "ring");
     extern __shared__ double lds_g[];
@@ -512,6 +512,22 @@ __global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
     }   // replica loop
 }
 
+template <int NK, class COL, int W, int H, bool BITS, bool PW = false, bool MRG = false>
+__global__ __launch_bounds__(1024) void rq_sweep_fw(SweepArgs a)
+{
+    sweep_fw_body<NK, COL, W, H, BITS, PW, MRG>(a);
+}
+// the merged-stream instances: no generator state, so a tighter VGPR budget buys waves
+// (RQ_FWM_WPE waves per SIMD; the planner picks the block size that fills them)
+#ifndef RQ_FWM_WPE
+#define RQ_FWM_WPE 4
+#endif
+template <int NK, class COL, bool BITS>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(RQ_FWM_WPE))) void rq_sweep_fwm(SweepArgs a)
+{
+    sweep_fw_body<NK, COL, 16, 8, BITS, false, true>(a);
+}
+
 // ============================================================================
 // launch wrappers
 // ============================================================================
@@ -529,8 +545,11 @@ static hipError_t launch_fw_t(const SweepArgs& a, hipStream_t s)
         const unsigned cap = (unsigned)(nb > 0 ? nb : 1) * (unsigned)rq_cu_count();
         if (cap < blocks) blocks = cap;
     }
-    hipLaunchKernelGGL((rq_sweep_fw<NK, COL, W, (W > 16 ? 8 : W / 2), BITS, PW, MRG>), dim3(blocks), dim3(64 * a.wpb),
-                       a.lds_total, s, a);
+    if constexpr (MRG)
+        hipLaunchKernelGGL((rq_sweep_fwm<NK, COL, BITS>), dim3(blocks), dim3(64 * a.wpb), a.lds_total, s, a);
+    else
+        hipLaunchKernelGGL((rq_sweep_fw<NK, COL, W, (W > 16 ? 8 : W / 2), BITS, PW, MRG>), dim3(blocks), dim3(64 * a.wpb),
+                           a.lds_total, s, a);
     return hipGetLastError();
 }
 template <class COL, int W, bool PW = false, bool MRG = false>
@@ -564,7 +583,8 @@ hipError_t rq_launch_sweep_fw(const SweepArgs& a, int nK, int col16, int W, int 
 template <int NK, class COL, int W, bool BITS, bool PW, bool MRG>
 static int occ_fw_t(int wpb, size_t lds)
 {
-    return rq_occupancy(rq_sweep_fw<NK, COL, W, (W > 16 ? 8 : W / 2), BITS, PW, MRG>, 64 * wpb, lds);
+    if constexpr (MRG) return rq_occupancy(rq_sweep_fwm<NK, COL, BITS>, 64 * wpb, lds);
+    else return rq_occupancy(rq_sweep_fw<NK, COL, W, (W > 16 ? 8 : W / 2), BITS, PW, MRG>, 64 * wpb, lds);
 }
 template <class COL, int W, bool PW = false, bool MRG = false>
 static int occ_fw_k(int nK, int wpb, size_t lds)
