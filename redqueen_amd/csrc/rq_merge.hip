@@ -181,6 +181,51 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
         // ---- every arrival before tau into the buffer (a lane stops at a full buffer) ----
         bool more = true;
         uint32_t nb1 = 0;   // one-wave blocks: the buffer cursor
+#ifndef RQ_MG_VEC
+#define RQ_MG_VEC 1
+#endif
+        if (RQ_MG_VEC) {
+            // the cached ones, every lane at once: a lane's arrivals before tau are the run
+            // [k0, k0 + cl) of its 16 cached (the stream is sorted), one wave prefix sum
+            // places them, and the 16 register slots are unrolled (static indices)
+            const double cv[16] = {c.a.x, c.a.y, c.a.z, c.a.w, c.b.x, c.b.y, c.b.z, c.b.w,
+                                   nx.a.x, nx.a.y, nx.a.z, nx.a.w, nx.b.x, nx.b.y, nx.b.z, nx.b.w};
+            const int k0 = p - p8;
+            int cl = 0;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) cl += (k >= k0 && p8 + k < L && cv[k] < tau) ? 1 : 0;
+            const uint32_t incl = wave_scan_add((uint32_t)cl);
+            const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+            uint32_t b0;
+            if constexpr (MG_W == 1) {
+                b0 = nb1;
+                nb1 += tot;
+            } else {
+                b0 = 0;
+                if (lane == 0 && tot) b0 = atomicAdd(&nb, tot);
+                b0 = (uint32_t)__builtin_amdgcn_readlane((int)b0, 0);
+            }
+            const int base = (int)(b0 + incl) - cl;
+            const int room = MG_CAP - base;
+            const int take = cl < room ? cl : (room > 0 ? room : 0);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const int e = k - k0;
+                if (e >= 0 && e < take) {
+                    const int idx = base + e;
+                    const int sb = sub_of<MG_M>(cv[k], t_lo, scale);
+                    const uint32_t slot = atomicAdd(&cnt[sb], 1u);
+                    bt[idx] = cv[k];
+                    bj[idx] = (uint16_t)j;
+                    bs[idx] = ((uint32_t)sb << MG_SB) | slot;
+                }
+            }
+            p += take;
+            if (take < cl) more = false;   // the buffer is full
+            if (p - p8 == 16 && p < L) RQ_MG_RELOAD(p);   // a burst: both chunks consumed
+            head = RQ_MG_HEAD();
+        }
+        // the rest of a burst (a lane ran through both chunks), one arrival per step
         for (;;) {
             const bool act = more && head < tau;
             const uint64_t m = __ballot(act);
