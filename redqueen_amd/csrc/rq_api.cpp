@@ -941,7 +941,7 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             ma.out_len = (int*)(ws + p.off_mlen);
             ma.status = out->status;
 #ifdef RQ_PHASE_CLOCK
-            ma.clk = phase_clk();
+            if (getenv("RQ_CLK_MERGE")) ma.clk = phase_clk();   // else the sweep's phases only
 #endif
             TimedLaunch tl(K_MERGE, s);
             if (rq_launch_merge(ma, s) != hipSuccess) return RQ_EHIP;

@@ -11,6 +11,7 @@ so = graphs.c5() if WL == "c5" else graphs.c3()
 g = engine.Graph(so["src_id"], so["other_sources"], so["sink_ids"], so["edge_list"], so["end_time"])
 lib = L.lib()
 lib.rq_phase_clock.argtypes = [C.POINTER(C.c_ulonglong)]
+os.environ["RQ_CLK_MERGE"] = "1"
 R = 1024 if WL == "c5" else 10000
 for k in range(2):
     g.run("opt", q=so["q"], s=so["s"], n_rep=R, ctrl_seed=0, world_seed=0, randomize=True, check=False)
