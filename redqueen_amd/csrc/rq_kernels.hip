@@ -660,6 +660,13 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
                 // each returns the T / V bits as of its own event's turn -- and counted
                 // after; one latency chain per batch instead of one per event
                 int wsl = 0, wsh = 0, osl = 0, osh = 0;
+                // MRG (delta mode): per event only its kills / new valid sinks go to its lane;
+                // own posts and own-stream arrivals leave the absolute counts after them
+                // (anchors); sumR / sumF come from segmented scans after the tile
+                constexpr bool DM = MRG;
+                int dcnt = 0, dval = 0, acnt = 0, aval = 0;
+                const int cnt0 = ag.cnt[0], val0 = ag.nvalid;
+                const int64_t S0 = ag.sumR, F0 = ag.sumF;
                 // per tile: events that cannot join a batch -- an own-stream arrival, no
                 // sinks or more than 128 -- and the batch breaks (those, an own post
                 // before the event, the end of the tile)
@@ -674,14 +681,21 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
                 while (q < n) {
                     if ((ownm >> q) & 1ull) {
                         agl.own(ag, lane);
-                        osl = wlane(osl, (int)(uint32_t)ag.sumR, q);
-                        osh = wlane(osh, (int)(ag.sumR >> 32), q);
-                        oval = wlane(oval, ag.nvalid, q);
-                        ocnt[0] = wlane(ocnt[0], ag.cnt[0], q);
+                        if (DM) {
+                            acnt = wlane(acnt, ag.cnt[0], q);
+                            aval = wlane(aval, ag.nvalid, q);
+                        } else {
+                            osl = wlane(osl, (int)(uint32_t)ag.sumR, q);
+                            osh = wlane(osh, (int)(ag.sumR >> 32), q);
+                            oval = wlane(oval, ag.nvalid, q);
+                            ocnt[0] = wlane(ocnt[0], ag.cnt[0], q);
+                        }
                     }
                     if ((specm >> q) & 1ull) {
                         // an own-stream arrival, or no / more than 128 sinks: one event alone
-                        if (!opt && bcast_i(tj, q) == a.ctrl_idx) {
+                        const int c_b = ag.cnt[0], v_b = ag.nvalid;
+                        const bool sown = !opt && bcast_i(tj, q) == a.ctrl_idx;
+                        if (sown) {
                             agl.own(ag, lane);
                         } else if (a.dbg != 2) {
                             const int f0 = bcast_i(e0, q), f1 = bcast_i(e1, q);
@@ -689,10 +703,20 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
                             const int cb = f0 + 64 + lane < f1 ? colat(f0 + 64 + lane) : 0;
                             agl.wall_pf(ag, colat, ca, cb, f0, f1, bcast_i(od, q), lane);
                         }
-                        wsl = wlane(wsl, (int)(uint32_t)ag.sumR, q);
-                        wsh = wlane(wsh, (int)(ag.sumR >> 32), q);
-                        wval = wlane(wval, ag.nvalid, q);
-                        wcnt[0] = wlane(wcnt[0], ag.cnt[0], q);
+                        if (DM) {
+                            if (sown) {
+                                acnt = wlane(acnt, ag.cnt[0], q);
+                                aval = wlane(aval, ag.nvalid, q);
+                            } else {
+                                dcnt = wlane(dcnt, c_b - ag.cnt[0], q);
+                                dval = wlane(dval, ag.nvalid - v_b, q);
+                            }
+                        } else {
+                            wsl = wlane(wsl, (int)(uint32_t)ag.sumR, q);
+                            wsh = wlane(wsh, (int)(ag.sumR >> 32), q);
+                            wval = wlane(wval, ag.nvalid, q);
+                            wcnt[0] = wlane(wcnt[0], ag.cnt[0], q);
+                        }
                         ++q;
                         continue;
                     }
@@ -736,14 +760,21 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
                         for (int k = 0; k < BLB; ++k) {
                             if (k < m) {
                                 const int qk = q + k;
-                                ag.cnt[0] -= popc(__ballot(ta[k] != 0u)) + popc(__ballot(tb[k] != 0u));
-                                if (!VF) ag.nvalid += popc(__ballot(va[k] != 0u)) + popc(__ballot(vb[k] != 0u));
-                                ag.sumR += bcast_i(degl, qk);
-                                ag.sumF += bcast_i(od, qk);
-                                wsl = wlane(wsl, (int)(uint32_t)ag.sumR, qk);
-                                wsh = wlane(wsh, (int)(ag.sumR >> 32), qk);
-                                wval = wlane(wval, ag.nvalid, qk);
-                                wcnt[0] = wlane(wcnt[0], ag.cnt[0], qk);
+                                const int dk = popc(__ballot(ta[k] != 0u)) + popc(__ballot(tb[k] != 0u));
+                                const int dv = VF ? 0 : popc(__ballot(va[k] != 0u)) + popc(__ballot(vb[k] != 0u));
+                                ag.cnt[0] -= dk;
+                                ag.nvalid += dv;
+                                if (DM) {
+                                    dcnt = wlane(dcnt, dk, qk);
+                                    if (!VF) dval = wlane(dval, dv, qk);
+                                } else {
+                                    ag.sumR += bcast_i(degl, qk);
+                                    ag.sumF += bcast_i(od, qk);
+                                    wsl = wlane(wsl, (int)(uint32_t)ag.sumR, qk);
+                                    wsh = wlane(wsh, (int)(ag.sumR >> 32), qk);
+                                    wval = wlane(wval, ag.nvalid, qk);
+                                    wcnt[0] = wlane(wcnt[0], ag.cnt[0], qk);
+                                }
                             }
                         }
                     };
@@ -753,8 +784,49 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
                         batch(std::false_type{});
                     q += m;
                 }
-                wsum = (int64_t)(((uint64_t)(uint32_t)wsh << 32) | (uint32_t)wsl);
-                osum = (int64_t)(((uint64_t)(uint32_t)osh << 32) | (uint32_t)osl);
+                if constexpr (DM) {
+                    // rank sums: a wall event adds its degree (sumR) and its follower edges
+                    // (sumF); a post or own-stream arrival drops sumF from sumR (AggL)
+                    const bool rst = own_b || strm_own;
+                    const uint64_t rm = __ballot(rst);
+                    const bool hasr = (rm & (~0ull >> (63 - lane))) != 0;   // reset at or before #lane
+                    const bool wl = act && !strm_own;
+                    const int deg = wl ? e1 - e0 : 0;
+                    const int odv = wl ? od : 0;
+                    SegFlags sf;
+                    sf.init(rst);
+                    const int pdeg = (int)wave_scan_add((uint32_t)deg);
+                    const int64_t sfq = (int64_t)(int)sf.scan_add((uint32_t)odv) + (hasr ? 0 : F0);
+                    int64_t dec = 0;
+                    // counts: the last anchor at or before #lane, minus / plus the deltas since
+                    const uint32_t P = wave_scan_add((uint32_t)dcnt), PV = wave_scan_add((uint32_t)dval);
+                    int bc = cnt0, bv = val0;
+                    uint32_t oc = 0u, ov = 0u;
+                    for (uint64_t bm = rm; bm; bm &= bm - 1) {
+                        const int r = __ffsll((unsigned long long)bm) - 1;
+                        const int64_t D = r == 0 ? F0 : bcast_i64(sfq, r - 1);
+                        if (lane >= r) {
+                            dec += D;
+                            bc = bcast_i(acnt, r);
+                            bv = bcast_i(aval, r);
+                            oc = (uint32_t)bcast_i((int)P, r) - (uint32_t)bcast_i(dcnt, r);
+                            ov = (uint32_t)bcast_i((int)PV, r) - (uint32_t)bcast_i(dval, r);
+                        }
+                    }
+                    wsum = S0 + pdeg - dec;
+                    osum = S0 + (pdeg - deg) - dec;
+                    wcnt[0] = bc - (int)(P - oc);
+                    wval = bv + (int)(PV - ov);
+                    ocnt[0] = acnt;
+                    oval = aval;
+                    if (n > 0) {
+                        ag.sumR = bcast_i64(wsum, n - 1);
+                        ag.sumF = bcast_i64(sfq, n - 1);
+                    }
+                } else {
+                    wsum = (int64_t)(((uint64_t)(uint32_t)wsh << 32) | (uint32_t)wsl);
+                    osum = (int64_t)(((uint64_t)(uint32_t)osh << 32) | (uint32_t)osl);
+                }
               } else {
                 // the first 128 sink columns of events q + 1 .. q + PF are in flight while
               // event q runs (global columns: an L2 round trip outlasts one event's work)
