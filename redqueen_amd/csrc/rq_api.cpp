@@ -377,9 +377,9 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
                 size_t stride = p->log ? align_up(w_off + 8 * (size_t)g->n_str * W, 16)
                                        : align_up(w_off + 64 * 12, 16);
                 // LOG: per-sink gtag/gcnt/gsum (gs: in global memory) + a wave_npsum<1>
-                // scratch (304 doubles)
+                // scratch (RQ_NPSUM1_LDS doubles)
                 const size_t x_off = stride;
-                if (p->log) stride = align_up(x_off + (gs ? 0 : 12 * (size_t)p->n_sinks_pad) + 8 * 304, 16);
+                if (p->log) stride = align_up(x_off + (gs ? 0 : 12 * (size_t)p->n_sinks_pad) + 8 * (size_t)RQ_NPSUM1_LDS, 16);
                 for (int wpb : {16, 12, 10, 8, 6, 5, 4, 3, 2, 1}) {
                     if (p->log && wpb > 4) continue;   // LOG instances: 256-thread blocks
                     if (!p->log && !p->mrg && spl >= 4 && wpb > 8) continue;   // 512-thread instances

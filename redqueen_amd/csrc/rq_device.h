@@ -396,9 +396,110 @@ __device__ __forceinline__ uint64_t order_key(double t)
 template <int NV>
 __host__ __device__ constexpr int npsum_lds_doubles()
 {
-    // leaf values [NV][128] + leaf (off,len) [128][2 ints = 1 double] + value stack [24][NV+1]
-    // (rows 16-23 of the value stack hold the two int recursion stacks [2][16])
-    return NV * 128 + 128 + 24 * (NV + 1);
+    // leaf values [NV][128] + leaf (off,len) [128][2 ints = 1 double] + the tree's levels
+    // [8][128] uint16 + their node counts [8] ints
+    return NV * 128 + 128 + 256 + 4;
+}
+
+// numpy's pairwise tree over m <= 8192 elements (pairwise_sum: a node of len > 128
+// elements splits at n2 = len / 2 rounded down to a multiple of 8), planned by one wave
+// level by level -- no serial walk.  With len = 8k + r (r < 8), n2 = 8 floor(k/2): the
+// children are 8 floor(k/2) and 8 ceil(k/2) + r elements, so only the LAST node of a
+// level carries the remainder r = m % 8 and a level is its nodes' unit counts k (two
+// nodes per lane: j = lane, lane + 64).  A leaf passes through to the next level
+// unchanged, so the last level is the leaves left to right.  Leaves hold >= 64 elements
+// unless m <= 128, hence <= 65 leaves and depth <= 7 (8192 = 1024 units, 6 halvings to
+// 16 units, one more for the remainder).
+// leaf[2L] / leaf[2L+1]: leaf L's offset / length; lev[d * 128 + j]: node j of level d's
+// first child index at level d + 1 | (split << 8); cnt[d]: nodes at level d; tmp: 128
+// ints of scratch.  Returns the leaf count; depth = the last level's index.
+__device__ __forceinline__ int npsum_plan(int m, int* leaf, uint16_t* lev, int* cnt, int* tmp, int& depth)
+{
+    const int lane = lane_id();
+    const int r = m & 7;
+    const uint64_t lt = (1ull << lane) - 1;
+    int n = 1, d = 0;
+    int kA = lane == 0 ? (m >> 3) : 0, kB = 0;
+    for (;;) {
+        const bool vA = lane < n, vB = lane + 64 < n;
+        const int lenA = 8 * kA + (lane == n - 1 ? r : 0);
+        const int lenB = 8 * kB + (lane + 64 == n - 1 ? r : 0);
+        const bool sA = vA && lenA > 128, sB = vB && lenB > 128;
+        const uint64_t bA = __ballot(sA), bB = __ballot(sB);
+        if ((bA | bB) == 0 || d == 7) {
+            // leaves: exclusive prefix sum of the lengths (lane order, then lane + 64)
+            const uint32_t iA = wave_scan_add(vA ? (uint32_t)lenA : 0u);
+            const uint32_t iB = wave_scan_add(vB ? (uint32_t)lenB : 0u);
+            const int totA = __builtin_amdgcn_readlane((int)iA, 63);
+            if (vA) {
+                leaf[2 * lane] = (int)iA - lenA;
+                leaf[2 * lane + 1] = lenA;
+            }
+            if (vB) {
+                leaf[2 * (lane + 64)] = totA + (int)iB - lenB;
+                leaf[2 * (lane + 64) + 1] = lenB;
+            }
+            wave_lds_sync();
+            depth = d;
+            return n;
+        }
+        const int pA = popc(bA);
+        const int cA = lane + popc(bA & lt);
+        const int cB = lane + 64 + pA + popc(bB & lt);
+        if (vA) {
+            lev[d * 128 + lane] = (uint16_t)(cA | (sA ? 256 : 0));
+            tmp[cA] = sA ? (kA >> 1) : kA;
+            if (sA) tmp[cA + 1] = (kA + 1) >> 1;
+        }
+        if (vB) {
+            lev[d * 128 + lane + 64] = (uint16_t)(cB | (sB ? 256 : 0));
+            tmp[cB] = sB ? (kB >> 1) : kB;
+            if (sB) tmp[cB + 1] = (kB + 1) >> 1;
+        }
+        if (lane == 0) cnt[d] = n;
+        n += pA + popc(bB);
+        ++d;
+        wave_lds_sync();
+        kA = lane < n ? tmp[lane] : 0;
+        kB = lane + 64 < n ? tmp[lane + 64] : 0;
+        wave_lds_sync();   // every lane's reads of tmp before the next level's writes
+    }
+}
+
+// fold the leaf values leafv[s * 128 + L] up the planned tree in place, level by level
+// (node j's children sit at indices >= j, and every read of a level precedes its
+// writes): a split node is left + right in numpy's order, a pass-through node keeps its
+// child's value bit for bit (-0.0 included).  The root's values end in cv (every lane).
+template <int NV>
+__device__ __forceinline__ void npsum_fold(int depth, const uint16_t* lev, const int* cnt, double* leafv,
+                                           double cv[NV])
+{
+    const int lane = lane_id();
+    for (int d = depth - 1; d >= 0; --d) {
+        const int n = cnt[d];
+        double vA[NV], vB[NV];
+        const bool okA = lane < n, okB = lane + 64 < n;
+        const int eA = okA ? lev[d * 128 + lane] : 0;
+        const int eB = okB ? lev[d * 128 + lane + 64] : 0;
+        const int cA = eA & 255, cB = eB & 255;
+#pragma unroll
+        for (int s = 0; s < NV; ++s) {
+            vA[s] = leafv[s * 128 + cA];
+            vB[s] = leafv[s * 128 + cB];
+            if (eA & 256) vA[s] = vA[s] + leafv[s * 128 + cA + 1];
+            if (eB & 256) vB[s] = vB[s] + leafv[s * 128 + cB + 1];
+        }
+        wave_lds_sync();
+#pragma unroll
+        for (int s = 0; s < NV; ++s) {
+            if (okA) leafv[s * 128 + lane] = vA[s];
+            if (okB) leafv[s * 128 + lane + 64] = vB[s];
+        }
+        wave_lds_sync();
+    }
+#pragma unroll
+    for (int s = 0; s < NV; ++s) cv[s] = leafv[s * 128];
+    wave_lds_sync();   // before the next chunk's plan reuses leafv as scratch
 }
 
 template <int NV, class VAL>
@@ -408,7 +509,8 @@ __device__ void wave_npsum(int64_t n, VAL&& val, double* lds, double out[NV])
     const int grp = lane >> 3, jj = lane & 7;
     double* leafv = lds;                                   // [NV][128]
     int* leaf = reinterpret_cast<int*>(lds + NV * 128);    // [128][2]
-    double* stk = lds + NV * 128 + 128;                    // [24][NV+1]
+    uint16_t* levt = reinterpret_cast<uint16_t*>(lds + NV * 128 + 128);   // [8][128]
+    int* lcnt = reinterpret_cast<int*>(lds + NV * 128 + 128 + 256);         // [8]
 
     double res[NV];
 #pragma unroll
@@ -416,40 +518,9 @@ __device__ void wave_npsum(int64_t n, VAL&& val, double* lds, double out[NV])
 
     for (int64_t c0 = 0; c0 < n; c0 += 8192) {
         const int m = (int)((n - c0) < 8192 ? (n - c0) : 8192);
-        // ---- enumerate the leaves of pairwise(m), left to right (uniform) ----
-        // the uniform recursion stacks live in LDS (slack of stk past depth 16), not in
-        // dynamically indexed VGPR arrays: the scan kernel's occupancy is VGPR-bound
-        int* so = reinterpret_cast<int*>(stk + 16 * (NV + 1));
-        int* sn = so + 16;
-        int nleaf = 0;
-        {
-            int sp = 0;
-            so[0] = 0;
-            sn[0] = m;
-            sp = 1;
-            while (sp > 0) {
-                --sp;
-                const int o = so[sp], len = sn[sp];
-                if (len <= 128) {
-                    if (lane == 0) {
-                        leaf[2 * nleaf] = o;
-                        leaf[2 * nleaf + 1] = len;
-                    }
-                    ++nleaf;
-                } else {
-                    int n2 = len / 2;
-                    n2 -= n2 % 8;
-                    so[sp] = o + n2;
-                    sn[sp] = len - n2;   // right pushed first
-                    so[sp + 1] = o;
-                    sn[sp + 1] = n2;     // left on top
-                    sp += 2;
-                }
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // ---- the leaves of pairwise(m), left to right, and the tree above them ----
+        int depth = 0;
+        const int nleaf = npsum_plan(m, leaf, levt, lcnt, reinterpret_cast<int*>(leafv), depth);
         // ---- leaf values: 8 leaves per round, lane jj = accumulator jj ----
         for (int L0 = 0; L0 < nleaf; L0 += 8) {
             const int L = L0 + grp;
@@ -495,52 +566,9 @@ __device__ void wave_npsum(int64_t n, VAL&& val, double* lds, double out[NV])
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // ---- post-order walk of the tree; leaves consumed left to right ----
+        // ---- the tree above the leaves, level by level ----
         double cv[NV];
-        {
-            int* st = so;   // the enumeration's stacks are free again
-            int sp = 0, li = 0;
-            sn[0] = m;
-            st[0] = 0;
-            sp = 1;
-            bool have = false;
-            while (sp > 0) {
-                const int top = sp - 1;
-                const int len = sn[top];
-                if (len <= 128) {
-#pragma unroll
-                    for (int s = 0; s < NV; ++s) cv[s] = leafv[s * 128 + li];
-                    ++li;
-                    --sp;
-                    have = true;
-                } else if (st[top] == 0) {
-                    int n2 = len / 2;
-                    n2 -= n2 % 8;
-                    st[top] = 1;
-                    sn[sp] = n2;
-                    st[sp] = 0;
-                    ++sp;
-                    have = false;
-                } else if (st[top] == 1) {
-                    // left value arrived in cv: park it, descend right
-#pragma unroll
-                    for (int s = 0; s < NV; ++s) stk[top * (NV + 1) + s] = cv[s];
-                    int n2 = len / 2;
-                    n2 -= n2 % 8;
-                    st[top] = 2;
-                    sn[sp] = len - n2;
-                    st[sp] = 0;
-                    ++sp;
-                    have = false;
-                } else {
-#pragma unroll
-                    for (int s = 0; s < NV; ++s) cv[s] = stk[top * (NV + 1) + s] + cv[s];
-                    --sp;
-                    have = true;
-                }
-                (void)have;
-            }
-        }
+        npsum_fold<NV>(depth, levt, lcnt, leafv, cv);
 #pragma unroll
         for (int s = 0; s < NV; ++s) res[s] = res[s] + cv[s];
         __builtin_amdgcn_wave_barrier();
@@ -584,44 +612,16 @@ __device__ void wave_npsum_rows(int64_t n, double end, LD&& ld, TLD&& tld, VF&& 
     const int grp = lane >> 3, jj = lane & 7;
     double* leafv = lds;
     int* leaf = reinterpret_cast<int*>(lds + NV * 128);
-    double* stk = lds + NV * 128 + 128;
+    uint16_t* levt = reinterpret_cast<uint16_t*>(lds + NV * 128 + 128);   // [8][128]
+    int* lcnt = reinterpret_cast<int*>(lds + NV * 128 + 128 + 256);         // [8]
     double res[NV];
 #pragma unroll
     for (int s = 0; s < NV; ++s) res[s] = 0.0;
 
     for (int64_t c0 = 0; c0 < n; c0 += 8192) {
         const int m = (int)((n - c0) < 8192 ? (n - c0) : 8192);
-        int* so = reinterpret_cast<int*>(stk + 16 * (NV + 1));
-        int* sn = so + 16;
-        int nleaf = 0;
-        {
-            int sp = 0;
-            so[0] = 0;
-            sn[0] = m;
-            sp = 1;
-            while (sp > 0) {
-                --sp;
-                const int o = so[sp], len = sn[sp];
-                if (len <= 128) {
-                    if (lane == 0) {
-                        leaf[2 * nleaf] = o;
-                        leaf[2 * nleaf + 1] = len;
-                    }
-                    ++nleaf;
-                } else {
-                    int n2 = len / 2;
-                    n2 -= n2 % 8;
-                    so[sp] = o + n2;
-                    sn[sp] = len - n2;
-                    so[sp + 1] = o;
-                    sn[sp + 1] = n2;
-                    sp += 2;
-                }
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        int depth = 0;
+        const int nleaf = npsum_plan(m, leaf, levt, lcnt, reinterpret_cast<int*>(leafv), depth);
         for (int L0 = 0; L0 < nleaf; L0 += 8) {
             const int L = L0 + grp;
             const bool act = L < nleaf;
@@ -692,43 +692,7 @@ __device__ void wave_npsum_rows(int64_t n, double end, LD&& ld, TLD&& tld, VF&& 
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         double cv[NV];
-        {
-            int* st = so;
-            int sp = 0, li = 0;
-            sn[0] = m;
-            st[0] = 0;
-            sp = 1;
-            while (sp > 0) {
-                const int top = sp - 1;
-                const int len = sn[top];
-                if (len <= 128) {
-#pragma unroll
-                    for (int s = 0; s < NV; ++s) cv[s] = leafv[s * 128 + li];
-                    ++li;
-                    --sp;
-                } else if (st[top] == 0) {
-                    int n2 = len / 2;
-                    n2 -= n2 % 8;
-                    st[top] = 1;
-                    sn[sp] = n2;
-                    st[sp] = 0;
-                    ++sp;
-                } else if (st[top] == 1) {
-#pragma unroll
-                    for (int s = 0; s < NV; ++s) stk[top * (NV + 1) + s] = cv[s];
-                    int n2 = len / 2;
-                    n2 -= n2 % 8;
-                    st[top] = 2;
-                    sn[sp] = len - n2;
-                    st[sp] = 0;
-                    ++sp;
-                } else {
-#pragma unroll
-                    for (int s = 0; s < NV; ++s) cv[s] = stk[top * (NV + 1) + s] + cv[s];
-                    --sp;
-                }
-            }
-        }
+        npsum_fold<NV>(depth, levt, lcnt, leafv, cv);
 #pragma unroll
         for (int s = 0; s < NV; ++s) res[s] = res[s] + cv[s];
         __builtin_amdgcn_wave_barrier();

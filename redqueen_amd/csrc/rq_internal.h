@@ -139,6 +139,7 @@ struct MergeArgs {
 };
 // threads per block of the merged-stream sweep instances (1024: <= 128 VGPRs)
 #ifndef RQ_MRG_LB
+#define RQ_NPSUM1_LDS 516   // doubles of wave_npsum<1> scratch (== rq::npsum_lds_doubles<1>())
 #define RQ_MRG_LB 1024
 #endif
 // wall events per branch-free batch of the merged-stream K = 1 sink-bit sweep

@@ -13,6 +13,7 @@
 #include "rq_internal.h"
 
 namespace rq {
+static_assert(npsum_lds_doubles<1>() == RQ_NPSUM1_LDS, "wave_npsum<1> scratch size (rq_api.cpp plans it)");
 
 template <int NK>
 struct Agg {
