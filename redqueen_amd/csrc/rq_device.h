@@ -604,7 +604,7 @@ __device__ __forceinline__ double dpp_shr7_f64(double x)
     return rq_bits_dbl(((uint64_t)hi << 32) | lo);
 }
 
-template <int NV, bool TNEXT, class Row, class LD, class TLD, class VF>
+template <int NV, bool TNEXT, class Row, int TU = 8, class LD, class TLD, class VF>
 __device__ void wave_npsum_rows(int64_t n, double end, LD&& ld, TLD&& tld, VF&& vf, double* lds,
                                 double out[NV])
 {
@@ -632,7 +632,6 @@ __device__ void wave_npsum_rows(int64_t n, double end, LD&& ld, TLD&& tld, VF&& 
             for (int s = 0; s < NV; ++s) r[s] = 0.0;
             const int lim = len - (len % 8);
             // a trip: up to TU rows per lane (8 TU per group), all loads in flight at once
-            constexpr int TU = 8;
             for (int i = 0; i < lim; i += 8 * TU) {
                 const int nu = (lim - i) >> 3 < TU ? (lim - i) >> 3 : TU;   // group-uniform
                 const int64_t e0 = c0 + off + i + jj;

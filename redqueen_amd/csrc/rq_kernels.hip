@@ -1011,7 +1011,9 @@ __global__ __launch_bounds__(256, WPE) void rq_scan(ScanArgs a)
                 v[NK + 1] = (m * m) * dt;
             };
             double res[NV];
-            wave_npsum_rows<NV, true, Row>(n, end, ld, tld, vf, lds, res);
+            // fewer waves / SIMD: the registers for a whole leaf (<= 16 rows per lane) in
+            // one trip (2), or for the 10-11 rows of C3's 80-88-row leaves (3)
+            wave_npsum_rows<NV, true, Row, (WPE <= 2 ? 16 : WPE == 3 ? 12 : 8)>(n, end, ld, tld, vf, lds, res);
             if (lane_id() == 0) {
 #pragma unroll
                 for (int s = 0; s < NV; ++s) out[s] = res[s];
@@ -1231,14 +1233,20 @@ template <int NK>
 static hipError_t launch_scan_t(const ScanArgs& a, hipStream_t s)
 {
     const size_t lds = 4 * npsum_lds_doubles<NK + 2>() * sizeof(double);
-    // waves per SIMD the build targets (VGPR budget): A/B knob RQ_SCAN_WPE
-    static const int wpe = getenv("RQ_SCAN_WPE") ? atoi(getenv("RQ_SCAN_WPE")) : 4;
+    // waves per SIMD the build targets (VGPR budget): A/B knob RQ_SCAN_WPE.  2 (a whole
+    // leaf per trip, 176 VGPRs at K = 1) measured 0.296 ms on the C3 step's scan against
+    // 0.313 / 0.332 / 0.645 / 0.805 ms at 3 / 4 / 6 / 8 (same box, profiles/r03_scan_ab.txt)
+    static const int wpe = getenv("RQ_SCAN_WPE") ? atoi(getenv("RQ_SCAN_WPE")) : 2;
     if (wpe >= 8)
         hipLaunchKernelGGL((rq_scan<NK, 8>), dim3(scan_blocks<NK, 8>(a, lds)), dim3(256), lds, s, a);
     else if (wpe >= 6)
         hipLaunchKernelGGL((rq_scan<NK, 6>), dim3(scan_blocks<NK, 6>(a, lds)), dim3(256), lds, s, a);
-    else
+    else if (wpe >= 4)
         hipLaunchKernelGGL((rq_scan<NK, 4>), dim3(scan_blocks<NK, 4>(a, lds)), dim3(256), lds, s, a);
+    else if (wpe == 3)
+        hipLaunchKernelGGL((rq_scan<NK, 3>), dim3(scan_blocks<NK, 3>(a, lds)), dim3(256), lds, s, a);
+    else
+        hipLaunchKernelGGL((rq_scan<NK, 2>), dim3(scan_blocks<NK, 2>(a, lds)), dim3(256), lds, s, a);
     return hipGetLastError();
 }
 
