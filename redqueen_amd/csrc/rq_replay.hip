@@ -1513,7 +1513,9 @@ __global__ __launch_bounds__(256) void rq_rp_scan(RpArgs a)
         v[NK + 1] = (m * m) * r.dt;
     };
     double res[NV];
-    wave_npsum_rows<NV, false, Row>(n, 0.0, ld, tld, vf, lds, res);
+    // one wave per df (<= 4 per CU for batches of a few hundred): a whole leaf per trip
+    // (16 rows per lane) halves the chain of load latencies a long df's scan waits on
+    wave_npsum_rows<NV, false, Row, 16>(n, 0.0, ld, tld, vf, lds, res);
     if (lane == 0) {
 #pragma unroll
         for (int s = 0; s < NV; ++s) out[s] = res[s];
