@@ -41,6 +41,10 @@ GEN_B_PER_WALL_EVENT = 8        # write one arrival time
 
 def workload(name):
     from redqueen_amd import graphs
+    if name == "c4":
+        return graphs.readme(), ("C4: README graph (3 sources, 3 sinks), T=100, RedQueen x 64 q "
+                                 "(logspace(-4, 7)) x 4 s ((1,1), (0.5,1.5), (1.5,0.5), (1,0.25)), "
+                                 "grid-window sharded, per-grid-point means")
     if name == "c3":
         return graphs.c3(), ("C3 syn1k: 1000 followers, 50 sources (25 Poisson2 rate 1 + 25 Hawkes "
                              "l0=1 a=1 b=10), degree 5, T=100, q=1e6, s=1, RedQueen, "
@@ -53,14 +57,20 @@ def workload(name):
     raise SystemExit("unknown workload " + name)
 
 
-def cpu_baseline(so, n_threads, sample, Ks=(1,)):
-    """Oracle (C port of the reference algorithm + Appendix-B metrics) on host cores."""
+def cpu_baseline(so, n_threads, sample, Ks=(1,), grid=None):
+    """Oracle (C port of the reference algorithm + Appendix-B metrics) on host cores.
+    grid: [(q, s)] -- the sample is spread evenly over these grid points (C4)."""
     from oracle import oracle as O
-    sc = O.Scenario(so, ("opt", 0))
+    pts = [dict(so)] if not grid else [dict(so, q=float(q), s=np.asarray(s, dtype=float))
+                                        for q, s in grid]
+    per = max(1, sample // len(pts))
     t0 = time.perf_counter()
-    out, cnt, tot = O.engine_batch(sc, sample, 0, True, Ks, n_threads)
+    tot = 0
+    for k, d in enumerate(pts):
+        out, cnt, t = O.engine_batch(O.Scenario(d, ("opt", 0)), per, k * per, True, Ks, n_threads)
+        tot += t
     el = time.perf_counter() - t0
-    return sample / el, tot / el, el
+    return per * len(pts) / el, tot / el, el
 
 
 def pmc_summary_paths(workload):
@@ -113,7 +123,8 @@ def pmc_traffic(workload, R, plan):
             continue
         for k, v in d.items():
             if k.startswith("rq_sweep") and "hbm_write_bytes" in v and "hbm_read_bytes" in v:
-                issue = {q: v[q] for q in ("frac_active_inst", "frac_wait_any", "frac_wait_inst") if q in v}
+                issue = {q: v[q] for q in ("frac_active_inst", "frac_wait_any", "frac_wait_inst",
+                                           "wave_slot_occupancy") if q in v}
                 c = v.get("counters", {})
                 # VALU issue ceiling: one wave64 VALU instruction per 2 cycles per SIMD
                 # (MI355X_MICROARCH.md), 4 SIMDs per CU, over the launch's cycles on one
@@ -124,6 +135,44 @@ def pmc_traffic(workload, R, plan):
                     issue["issue_frac"] = c["SQ_INSTS_VALU"] / (N_CU * 4 * cyc / 2.0)
                 return v["hbm_read_bytes"] + v["hbm_write_bytes"], os.path.relpath(path, ROOT), issue
     return None, None, None
+
+
+def make_step(wl, g, so, R, world, rank, dev, Ks, group=None):
+    """The bench step of a workload, on this rank: (step(k) -> (this rank's BatchResult,
+    ensemble means), replicas per step over all ranks, plan kwargs).
+    c2 / c3 / c5: R replicas per GPU with their own seeds, one all-gather of the
+    per-replica metric rows (RCCL over xGMI), the ensemble means.
+    c4: the 64 q x 4 s grid with R replicas per grid point per GPU -- rank k runs the
+    k-th replica window of EVERY grid point (dist.run_sharded), one all-gather, then
+    per-grid-point means in fixed replica order (dist.grid_means)."""
+    from redqueen_amd import dist as D
+    if wl == "c4":
+        from redqueen_amd import graphs
+        grid = graphs.c4_grid()
+        qs = np.asarray([q for q, _ in grid])
+        sm = np.asarray([list(s) for _, s in grid])
+        n_rep = R * world
+        lo, hi = D.grid_shard(n_rep, world, rank)
+        kw = dict(q=qs, s=sm, randomize=True, Ks=Ks, seed_mod=n_rep)
+
+        def step(k):
+            base = k * n_rep
+            m, c, res = D.run_sharded(g, len(grid), n_rep, world, rank, group, ctrl="opt",
+                                      ctrl_seed=base, world_seed=base, check=False, **kw)
+            return res, D.grid_means(m, len(grid), n_rep)
+        return step, len(grid) * n_rep, dict(kw, n_rep=n_rep, rep_lo=lo, rep_cnt=hi - lo)
+
+    def step(k):
+        base = (k * world + rank) * R
+        res = g.run("opt", q=so["q"], s=so["s"], n_rep=R, ctrl_seed=base, world_seed=base,
+                    randomize=True, Ks=Ks, check=False)
+        m = res.metrics
+        if world > 1:
+            allm = D.gather_rows(m, world * R, world, rank, group)   # RCCL over xGMI: the only exchange
+            m = allm
+        # ensemble means (redqueen_amd.dist.grid_means): identical on every rank
+        return res, D.grid_means(m, 1, m.shape[0])[0]
+    return step, R * world, dict(q=so["q"], s=so["s"], n_rep=R, randomize=True, Ks=Ks)
 
 
 def main():
@@ -154,29 +203,17 @@ def main():
     so, desc = workload(a.workload)
     g = engine.Graph(so["src_id"], so["other_sources"], so["sink_ids"], so["edge_list"],
                      so["end_time"])
-    R = a.replicas or (4096 if a.workload == "c5" else 10000)
+    # replicas per GPU per step (c4: per grid point per GPU)
+    R = a.replicas or {"c5": 8192, "c4": 1000}.get(a.workload, 10000)
     Ks = (1,)
-    plan = g.run("opt", q=so["q"], s=so["s"], n_rep=R, randomize=True, Ks=Ks, plan_only=True)
-
-    def step(k):
-        base = (k * world + rank) * R
-        res = g.run("opt", q=so["q"], s=so["s"], n_rep=R, ctrl_seed=base, world_seed=base,
-                    randomize=True, Ks=Ks, check=False)
-        m = res.metrics
-        if world > 1:
-            allm = torch.empty((world * R, m.shape[1]), dtype=m.dtype, device=dev)
-            dist.all_gather_into_tensor(allm, m)       # RCCL over xGMI: the only exchange
-            m = allm
-        # ensemble means (redqueen_amd.dist.grid_means): identical on every rank
-        means = D.grid_means(m, 1, m.shape[0])[0]
-        return res, means
+    step, rep_step, pkw = make_step(a.workload, g, so, R, world, rank, dev, Ks)
+    plan = g.run("opt", plan_only=True, **pkw)
 
     # capacity check once at full size (overflow -> the engine reruns with doubled
     # capacities; every launch of the run has the timed launches' shape, so a rocprofv3
     # average over the whole command matches the per-launch HIP-event time), then
     # warmup so the timed region starts with every buffer allocated
-    ok = g.run("opt", q=so["q"], s=so["s"], n_rep=R, ctrl_seed=0, world_seed=0,
-               randomize=True, Ks=Ks, check=True)
+    ok = g.run("opt", ctrl_seed=0, world_seed=0, check=True, **pkw)
     del ok
     mask = L.ST_ROWS_OVERFLOW | L.ST_STREAM_OVERFLOW
 
@@ -185,6 +222,8 @@ def main():
         # count of the replicas the fast sweep flagged RQ_ST_TIE (equal event times:
         # check=True would rerun them on the exact sequential sweep; never taken by
         # the continuous-time bench worlds, and reported so that it shows if it is)
+        if res is None:   # a rank without replicas (more ranks than replicas per point)
+            return
         acc[0] += res.counts.sum(0)
         torch.maximum(acc[1], (res.status & mask).max(), out=acc[1])
         acc[2] += ((res.status & L.ST_TIE) != 0).sum()
@@ -231,16 +270,19 @@ def main():
     if world > 1:   # reporting only, after the timed region
         dist.all_reduce(tot)
     local_ev = int(tot[2].item())   # events of all ranks
-    replicas = R * world * a.steps
+    replicas = rep_step * a.steps
     value = replicas / el
     ev_rate = local_ev / el
 
     # roofline of the dominant kernel (the sweep), per launch, this rank
     n_sweep = max(1, int(nl[1]))
     sweep_ms = ms[1] / n_sweep
-    ev_rank = local_ev / world / a.steps
-    rows_step = rows_l / a.steps
-    posts_step = posts_l / a.steps
+    # per LAUNCH: a step runs one launch of each kernel per replica chunk (the engine's
+    # pipelined chunks, rq_run_batch), so the step's bytes are split over its launches
+    lps = n_sweep / a.steps
+    ev_rank = local_ev / world / a.steps / lps
+    rows_step = rows_l / a.steps / lps
+    posts_step = posts_l / a.steps / lps
     # the fused sweep (variant >= 10) generates its arrivals in LDS: no arrival reads
     fused = 10 <= plan["variant"] < 20   # 20+: the fused sweep on merged streams (reads them)
     merged = not fused and plan["sources_per_lane"] == 0   # rq_merge_streams feeds the sweep
@@ -266,8 +308,12 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
         nt = min(16, os.cpu_count() or 1)
-        sample = a.cpu_sample or (2 if a.workload == "c5" else 128) * nt
-        crate, cev, cel = cpu_baseline(so, nt, sample, Ks)
+        sample = a.cpu_sample or {"c5": 2, "c4": 512}.get(a.workload, 128) * nt
+        cgrid = None
+        if a.workload == "c4":   # 16 grid points spread over the q x s grid
+            from redqueen_amd import graphs
+            cgrid = graphs.c4_grid()[::16]
+        crate, cev, cel = cpu_baseline(so, nt, sample, Ks, cgrid)
         cpu = {"value": crate, "unit": "replicas/s", "cores": nt, "kind": "port",
                "sample": "%d %s replicas through the C oracle (engine semantics + Appendix-B "
                          "metrics), %d pthreads, %.1f s, %.0f events/s" %
@@ -288,14 +334,17 @@ def main():
             "dtype": "f64",
             "data": "synthetic (Philox-seeded arrival streams on the reference's %s network)" %
                     a.workload.upper(),
-            "config": {"workload": desc, "replicas_per_gpu": R, "global_batch": R * world,
-                       "parallelism": "replica-sharded dp%d" % world, "Ks": list(Ks)},
+            "config": {"workload": desc, "replicas_per_gpu": rep_step // world, "global_batch": rep_step,
+                       "parallelism": ("grid-window sharded dp%d (each rank: every grid point's "
+                                       "replica window)" if a.workload == "c4" else
+                                       "replica-sharded dp%d") % world, "Ks": list(Ks)},
             "events_per_sec": ev_rate,
             "events_per_replica": local_ev / replicas,
             "overflow": int(status.item()),
             "tie_replicas": int(ties.item()),
             "kernels_ms_per_launch": {"gen_streams": gen_ms, "merge_streams": merge_ms, "sweep": sweep_ms,
                                       "scan": scan_ms},
+            "launches_per_step": lps,
             "sweep_plan": plan,
             "roofline": {"bound": "hbm", "kernel": "rq_sweep", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
@@ -305,6 +354,7 @@ def main():
                          # issue_frac = VALU instructions / the VALU issue ceiling (same PMC run)
                          "issue": issue,
                          "issue_frac": issue.get("issue_frac") if issue else None,
+                         "wave_slot_occupancy": issue.get("wave_slot_occupancy") if issue else None,
                          "note": "sweep is latency/issue-bound (serial event chain per replica); "
                                  "algorithmic bytes = 24 B/pivot row written%s" %
                                  ("" if fused else " + %d B/wall event read" % b_wall)},

@@ -148,5 +148,6 @@ def run_significance(sim_opts, significance, time_period, seeds=range(10), rando
         src = res.ev_src.cpu().numpy()
         ids = g.stream_src_ids
         for i in range(src.shape[0]):
-            _sig_reach_check(g, sim_opts.edge_list, spw, 1.0, ids[src[i, :n[i]]], bad=bad)
+            _sig_reach_check(g, sim_opts.edge_list, spw, 1.0, ids[src[i, :n[i]]], bad=bad,
+                             max_events=max_events)
     return _frame(res, np.tile(seeds, len(qv)), np.repeat(qv, R), "OptPW", Ks)

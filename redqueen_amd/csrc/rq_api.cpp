@@ -76,6 +76,34 @@ struct TimedLaunch {
     }
 };
 
+// Side streams of the pipelined chunk loop (rq_run_batch): per host thread, created on
+// first use on the caller's current device, with the fork / join events.  Work on them
+// is always bracketed by a wait on the caller's stream (fork) and a wait of the caller's
+// stream on them (join), so the call stays stream-ordered for the caller.
+struct SidePipe {
+    int dev = -1;
+    hipStream_t s[2] = {nullptr, nullptr};
+    hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};
+    int get(int n, hipStream_t* out)
+    {
+        int d = 0;
+        if (hipGetDevice(&d) != hipSuccess) return RQ_EHIP;
+        if (dev != d) {   // first use (or another device): fresh streams and events
+            for (int k = 0; k < 2; ++k) s[k] = nullptr, join[k] = nullptr;
+            fork = nullptr;
+            dev = d;
+        }
+        if (!fork && hipEventCreateWithFlags(&fork, hipEventDisableTiming) != hipSuccess) return RQ_EHIP;
+        for (int k = 0; k < n && k < 2; ++k) {
+            if (!s[k] && hipStreamCreateWithFlags(&s[k], hipStreamNonBlocking) != hipSuccess) return RQ_EHIP;
+            if (!join[k] && hipEventCreateWithFlags(&join[k], hipEventDisableTiming) != hipSuccess) return RQ_EHIP;
+            out[k] = s[k];
+        }
+        return RQ_OK;
+    }
+};
+thread_local SidePipe t_pipe;
+
 }  // namespace
 
 namespace {
@@ -170,6 +198,15 @@ struct Plan {
     size_t g_col = 0, g_ptr = 0, g_odf = 0, g_cbf = 0, g_wave = 0, g_wave_stride = 0, g_rank_off = 0,
            g_win_off = 0, g_x_off = 0, g_total = 0, g_stage_off = 0;
     size_t tables_bytes = 0;
+    // resident sweep waves per CU of the chosen instance (the persistent grid's slots)
+    int wpc = 0;
+    // pipelined chunks (merged-stream sweeps): nbuf buffer sets, chunk k on stream k % nbuf
+    // with set k % nbuf, so chunk k+1's generation / merge and chunk k-1's scan fill the
+    // wave slots chunk k's sweep tail leaves (rq_run_batch); off_set0 + set * set_stride
+    // is a set's base, the per-chunk offsets below are relative to it
+    int nbuf = 1;
+    bool order = false;   // longest-first replica order for the sweep (rq_order_replicas)
+    size_t off_set0 = 0, set_stride = 0, off_ord = 0;
     size_t off_pwc = 0, off_pwmax = 0;
     size_t off_invc = 0, off_streams = 0, off_slen = 0, off_rt = 0, off_rs = 0, off_rv = 0,
            off_rc = 0, off_sall = 0, off_wq = 0, off_stoff = 0, off_cap = 0, off_rdk = 0, off_gs = 0,
@@ -281,7 +318,7 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
             c = kind == RQ_SRC_REALDATA ? (p->rd_k[j] >= 0 ? b->rd_cap[p->rd_k[j]] : (int64_t)m)
                                         : (int64_t)std::ceil((m + 8.0 * std::sqrt(var) + 32.0) * scale);
         if (c > (int64_t)1 << 30) return RQ_EINVAL;
-        c = (c + 7) & ~(int64_t)7;   // 64-byte chunks for the generator's stores
+        c = (c + 15) & ~(int64_t)15;   // whole 128-byte lines: the merge's loads, the generator's stores
         p->cap[j] = (int)c;
         p->st_off[j] = p->capsum;
         p->capsum += c;
@@ -396,6 +433,7 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
                     const int score = waves * 8 + col_lds * 2 + (gs ? 0 : 100000);
                     if (score > best) {
                         best = score;
+                        p->wpc = waves;
                         p->gs = gs;
                         p->gs_slots = std::min<int64_t>((int64_t)align_up((size_t)p->chunk, (size_t)wpb),
                                                         (int64_t)blocks * wpb * rq_cu_count());
@@ -459,6 +497,7 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
                 const int score = waves * 4 + (W == 16 ? 2 : W == 32 ? 1 : 0);
                 if (score > best) {
                     best = score;
+                    p->wpc = waves;
                     p->gwin = W; p->fw_h = H; p->gwpb = wpb; p->gcol_lds = c16; p->gcol16 = c16;
                     p->g_col = o_col; p->g_ptr = o_ptr; p->g_odf = o_odf; p->g_cbf = o_cbf;
                     p->g_wave = sh; p->g_wave_stride = stride; p->g_rank_off = r_off;
@@ -471,6 +510,32 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     }
     if (!p->fw) p->fwm = false;
     if (p->fw) p->mrg = p->fwm;   // the merge kernel feeds the fused sweep too
+
+    // pipelined chunks for the merged-stream sweeps (not the sequential LOG sweep, whose
+    // global per-sink slots are sized for one grid): the batch in an even number of
+    // chunks of <= 16384 replicas on two streams, so the two streams' generation, merge,
+    // sweep and scan run side by side and one chunk's sweep tail is the other's work.
+    // C3, 10k replicas (profiles/r04_pipe_ab.txt): one stream 3.02 ms per step; two
+    // streams x 2 chunks of 5000 2.82 ms; 3 x 3334 3.36; 5 x 2000 4.15; 10 x 1000 5.98
+    // (the sweep is latency-bound per replica: a chunk much below the resident wave
+    // slots leaves them empty)
+    p->nbuf = 1;
+    p->order = p->mrg && !p->log;
+    if (const char* e = getenv("RQ_ORDER")) p->order = p->order && atoi(e) != 0;   // A/B only
+    if (p->mrg && !p->log) {
+        int nb = 2;
+        if (const char* e = getenv("RQ_PIPE")) nb = std::max(1, std::min(3, atoi(e)));   // A/B only
+        if (b->chunk <= 0) {
+            int64_t nch = (p->R + 16383) / 16384;
+            if (nb > 1) nch = std::max<int64_t>(2, (nch + 1) & ~(int64_t)1);   // even: both streams busy
+            if (const char* e = getenv("RQ_PIPE_CHUNK"))   // A/B only
+                nch = (p->R + std::max<int64_t>(64, atoll(e)) - 1) / std::max<int64_t>(64, atoll(e));
+            nch = std::max<int64_t>(1, std::min(nch, p->R));
+            p->chunk = (p->R + nch - 1) / nch;
+        }
+        const int64_t nch = (p->R + p->chunk - 1) / p->chunk;
+        p->nbuf = (int)std::min<int64_t>(nb, nch);
+    }
 
     const size_t A = 256;
     const int64_t C = p->chunk;
@@ -485,6 +550,10 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     p->off_pwmax = o;   o = o + sizeof(double) * (nseg ? (size_t)b->n_grid * g->n_str : 0);
     p->tables_bytes = o;
     o = align_up(o, A);
+    // one buffer set per pipelined stream; offsets relative to the set's base
+    p->off_set0 = o;
+    const size_t o_set = o;
+    o = 0;
     const int64_t strm = p->fw && !p->fwm ? 0 : C;   // the generating fused sweep keeps its arrivals in LDS
     p->off_streams = o; o = align_up(o + sizeof(double) * (size_t)strm * p->capsum, A);
     p->off_slen = o;    o = align_up(o + sizeof(int) * (size_t)strm * g->n_str, A);
@@ -492,12 +561,15 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     p->off_mt = o;      o = align_up(o + sizeof(double) * (size_t)mrgc * p->capsum, A);
     p->off_mj = o;      o = align_up(o + sizeof(uint16_t) * (size_t)mrgc * p->capsum, A);
     p->off_mlen = o;    o = align_up(o + sizeof(int) * (size_t)mrgc, A);
+    p->off_ord = o;     o = align_up(o + sizeof(int) * (size_t)(p->order ? C : 0), A);
     p->off_rt = o;      o = align_up(o + sizeof(double) * (size_t)C * p->cap_rows, A);
     p->off_rs = o;      o = align_up(o + sizeof(double) * (size_t)C * p->cap_rows, A);
     p->off_rv = o;      o = align_up(o + sizeof(uint32_t) * (size_t)C * p->cap_rows, A);
     p->off_rc = o;      o = align_up(o + sizeof(uint32_t) * (size_t)C * p->cap_rows * p->nK, A);
     p->off_sall = o;    o = align_up(o + sizeof(int) * (size_t)C, A);
     p->off_wq = o;      o = align_up(o + 2 * sizeof(int), A);   // [0] sweep, [1] scan queue
+    p->set_stride = o;
+    o = o_set + (size_t)p->nbuf * p->set_stride;
     // LOG + gs: per resident wave, rank int + gtag/gcnt/gsum int per sink
     p->gs_stride = p->gs ? (int64_t)align_up(16 * (size_t)p->n_sinks_pad, A) : 0;
     p->off_gs = o;      o = align_up(o + (size_t)(p->gs ? p->gs_slots : 0) * p->gs_stride, A);
@@ -879,8 +951,21 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
     const int ctrl_stream_kind =
         (b->ctrl_kind == RQ_SRC_OPT || b->ctrl_kind == RQ_SRC_OPTPW || b->ctrl_kind == RQ_SRC_NONE)
             ? RQ_SRC_NONE : b->ctrl_kind;
-    for (int64_t c0 = 0; c0 < p.R; c0 += p.chunk) {
+    // pipelined chunks: chunk k runs on stream k % nbuf (the caller's stream and up to two
+    // side streams, forked after the tables / status above and joined before returning)
+    // with buffer set k % nbuf, so a set is reused only in its own stream's order
+    hipStream_t pst[3] = {s, nullptr, nullptr};
+    if (p.nbuf > 1) {
+        if ((rc = t_pipe.get(p.nbuf - 1, pst + 1)) != RQ_OK) return rc;
+        if (hipEventRecord(t_pipe.fork, s) != hipSuccess) return RQ_EHIP;
+        for (int k = 1; k < p.nbuf; ++k)
+            if (hipStreamWaitEvent(pst[k], t_pipe.fork, 0) != hipSuccess) return RQ_EHIP;
+    }
+    int64_t ci = 0;
+    for (int64_t c0 = 0; c0 < p.R; c0 += p.chunk, ++ci) {
         const int64_t C = std::min(p.chunk, p.R - c0);
+        hipStream_t s = pst[ci % p.nbuf];
+        char* wsb = ws + p.off_set0 + (size_t)(ci % p.nbuf) * p.set_stride;   // this chunk's buffer set
         GenArgs ga{};
         ga.n_chunk = C;
         ga.chunk0 = c0;
@@ -913,8 +998,9 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
         ga.capsum = p.capsum;
         ga.start = g->start;
         ga.end = g->end;
-        ga.streams = (double*)(ws + p.off_streams);
-        ga.slen = (int*)(ws + p.off_slen);
+        ga.streams = (double*)(wsb + p.off_streams);
+        ga.slen = (int*)(wsb + p.off_slen);
+        ga.slen_stride = p.chunk;
         ga.status = out->status;
         if (b->n_rd > 0) {
             ga.rd_k = (const int*)(ws + p.off_rdk);
@@ -935,10 +1021,11 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             ma.st_off = ga.st_off;
             ma.streams = ga.streams;
             ma.slen = ga.slen;
+            ma.slen_stride = ga.slen_stride;
             ma.end = g->end;
-            ma.out_t = (double*)(ws + p.off_mt);
-            ma.out_j = (uint16_t*)(ws + p.off_mj);
-            ma.out_len = (int*)(ws + p.off_mlen);
+            ma.out_t = (double*)(wsb + p.off_mt);
+            ma.out_j = (uint16_t*)(wsb + p.off_mj);
+            ma.out_len = (int*)(wsb + p.off_mlen);
             ma.status = out->status;
 #ifdef RQ_PHASE_CLOCK
             if (getenv("RQ_CLK_MERGE")) ma.clk = phase_clk();   // else the sweep's phases only
@@ -978,22 +1065,28 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
         sa.fol = g->d_fol.p;
         sa.st_off = (const int64_t*)(ws + p.off_stoff);
         sa.capsum = p.capsum;
-        sa.streams = (const double*)(ws + p.off_streams);
-        sa.slen = (const int*)(ws + p.off_slen);
+        sa.streams = (const double*)(wsb + p.off_streams);
+        sa.slen = (const int*)(wsb + p.off_slen);
+        sa.slen_stride = p.chunk;
         if (p.mrg) {
-            sa.mrg_t = (const double*)(ws + p.off_mt);
-            sa.mrg_j = (const uint16_t*)(ws + p.off_mj);
-            sa.mrg_len = (const int*)(ws + p.off_mlen);
+            sa.mrg_t = (const double*)(wsb + p.off_mt);
+            sa.mrg_j = (const uint16_t*)(wsb + p.off_mj);
+            sa.mrg_len = (const int*)(wsb + p.off_mlen);
+            if (p.order) {
+                int* ord = (int*)(wsb + p.off_ord);
+                if (rq_launch_order(sa.mrg_len, C, ord, s) != hipSuccess) return RQ_EHIP;
+                sa.order = ord;
+            }
         }
         sa.start = g->start;
         sa.end = g->end;
         sa.max_events = b->max_events;
         sa.cap_rows = p.cap_rows;
-        sa.rows_t = (double*)(ws + p.off_rt);
-        sa.rows_sum = (double*)(ws + p.off_rs);
-        sa.rows_valid = (uint32_t*)(ws + p.off_rv);
-        sa.rows_cnt = (uint32_t*)(ws + p.off_rc);
-        sa.sall = (int*)(ws + p.off_sall);
+        sa.rows_t = (double*)(wsb + p.off_rt);
+        sa.rows_sum = (double*)(wsb + p.off_rs);
+        sa.rows_valid = (uint32_t*)(wsb + p.off_rv);
+        sa.rows_cnt = (uint32_t*)(wsb + p.off_rc);
+        sa.sall = (int*)(wsb + p.off_sall);
         sa.counts = out->counts;
         sa.status = out->status;
         if (b->flags & RQ_RUN_EVENT_LOG) {
@@ -1057,9 +1150,9 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             // so the launch tail is spread over every CU instead of whole 16-wave blocks
             static const int wq_off = getenv("RQ_FW_STATIC") ? atoi(getenv("RQ_FW_STATIC")) : 0;   // A/B only
             // both queues of this chunk (sweep, scan) zeroed by one memset
-            if (hipMemsetAsync(ws + p.off_wq, 0, 2 * sizeof(int), s) != hipSuccess) return RQ_EHIP;
-            if (!wq_off) {   // both sweep kinds take replicas past the first from the queue
-                sa.wq = (int*)(ws + p.off_wq);
+            if (hipMemsetAsync(wsb + p.off_wq, 0, 2 * sizeof(int), s) != hipSuccess) return RQ_EHIP;
+            if (!wq_off || p.gs) {   // both sweep kinds take replicas past the first from the queue (GS needs it)
+                sa.wq = (int*)(wsb + p.off_wq);
             }
             TimedLaunch tl(K_SWEEP, s);
             const hipError_t e = p.fw ? rq_launch_sweep_fw(sa, p.nK, p.gcol16, p.fwm ? 0 : p.gwin, p.bits, s)
@@ -1073,7 +1166,7 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
         sc.chunk0 = c0;
         sc.nrows = out->counts + 3;
         sc.nrows_stride = 4;
-        sc.sall = (const int*)(ws + p.off_sall);
+        sc.sall = (const int*)(wsb + p.off_sall);
         sc.row_stride = p.cap_rows;
         sc.rows_t = sa.rows_t;
         sc.rows_sum = sa.rows_sum;
@@ -1081,12 +1174,16 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
         sc.rows_cnt = sa.rows_cnt;
         sc.end = g->end;
         sc.metrics = out->metrics;
-        sc.wq = (int*)(ws + p.off_wq) + 1;
+        sc.wq = (int*)(wsb + p.off_wq) + 1;
         {
             TimedLaunch tl(K_SCAN, s);
             if (rq_launch_scan(sc, p.nK, s) != hipSuccess) return RQ_EHIP;
         }
     }
+    for (int k = 1; k < p.nbuf; ++k)   // join: the caller's stream waits for every side stream
+        if (hipEventRecord(t_pipe.join[k - 1], pst[k]) != hipSuccess ||
+            hipStreamWaitEvent(pst[0], t_pipe.join[k - 1], 0) != hipSuccess)
+            return RQ_EHIP;
     return RQ_OK;
 }
 

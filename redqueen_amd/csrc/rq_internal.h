@@ -38,7 +38,8 @@ struct GenArgs {
     int64_t capsum;
     double start, end;
     double* streams;
-    int* slen;
+    int* slen;                       // [n_str][slen_stride]: lane-coalesced stores
+    int64_t slen_stride;             // >= n_chunk (the chunk buffers' replica capacity)
     int32_t* status;
     // per-replica RealData times (rq_batch_desc.rd_*): stream j -> source k or -1
     const int* rd_k;
@@ -70,7 +71,8 @@ struct SweepArgs {
     const int64_t* st_off;
     int64_t capsum;
     const double* streams;
-    const int* slen;
+    const int* slen;           // [n_str][slen_stride]
+    int64_t slen_stride;
     double start, end;
     int64_t max_events;
     int64_t cap_rows;
@@ -118,6 +120,10 @@ struct SweepArgs {
     const double* mrg_t;
     const uint16_t* mrg_j;
     const int* mrg_len;
+    // longest-first play order of the chunk's replicas (rq_order_replicas over mrg_len):
+    // the wave slots and the work queue take chunk replica order[q] for queue position q
+    // (null: q itself).  Outputs stay indexed by replica, so no result bit depends on it.
+    const int* order;
 };
 
 // rq_merge_streams: one block per replica merges its pre-generated per-source streams
@@ -129,7 +135,8 @@ struct MergeArgs {
     int64_t capsum;
     const int64_t* st_off;
     const double* streams;
-    const int* slen;
+    const int* slen;        // [n_str][slen_stride]
+    int64_t slen_stride;
     double end;
     double* out_t;          // [C][capsum]
     uint16_t* out_j;        // [C][capsum]
@@ -137,9 +144,9 @@ struct MergeArgs {
     int32_t* status;        // RQ_ST_TIE when > RQ_MG_CAP arrivals share one time
     unsigned long long* clk;   // RQ_PHASE_CLOCK builds only: per-phase s_memtime sums [8]
 };
+#define RQ_NPSUM1_LDS 516   // doubles of wave_npsum<1> scratch (== rq::npsum_lds_doubles<1>())
 // threads per block of the merged-stream sweep instances (1024: <= 128 VGPRs)
 #ifndef RQ_MRG_LB
-#define RQ_NPSUM1_LDS 516   // doubles of wave_npsum<1> scratch (== rq::npsum_lds_doubles<1>())
 #define RQ_MRG_LB 1024
 #endif
 // wall events per branch-free batch of the merged-stream K = 1 sink-bit sweep
@@ -171,6 +178,8 @@ hipError_t rq_launch_scan(const ScanArgs& a, int nK, hipStream_t s);
 int rq_sweep_blocks_per_cu(int spl, int nK, int col16, int W, int log, int bits, int wpb, size_t lds);
 // spl = 0 in rq_launch_sweep / rq_sweep_blocks_per_cu: the fast sweep reading merged streams
 hipError_t rq_launch_merge(const MergeArgs& a, hipStream_t s);
+// longest-first order of n <= 65536 replicas by len (descending; ties in any order)
+hipError_t rq_launch_order(const int* len, int64_t n, int* order, hipStream_t s);
 hipError_t rq_launch_sweep_fw(const SweepArgs& a, int nK, int col16, int W, int bits, hipStream_t s);
 int rq_fw_blocks_per_cu(int nK, int col16, int W, int bits, int wpb, size_t lds, int pw);
 int rq_cu_count();   // CUs of the current device (256 on MI355X when the query fails)

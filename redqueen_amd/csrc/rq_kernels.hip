@@ -77,18 +77,23 @@ __global__ __launch_bounds__(256) void rq_gen_streams(GenArgs a)
         if (gen.step(&tv, a.end)) RQ_EMIT(tv);
     }
 #undef RQ_EMIT
-    {   // the last partial chunk: values sit in sb[8-r .. 7]
+    {   // the last partial chunk: values sit in sb[8-r .. 7]; written as one whole 64-byte
+        // chunk (slots past n hold stale values nobody reads: readers stop at slen), so
+        // no line takes 8-byte partial writes
         const int r = n & 7;
-        double* d = out + (n - r);
-        if (r > 0) d[r - 1] = sb7;
-        if (r > 1) d[r - 2] = sb6;
-        if (r > 2) d[r - 3] = sb5;
-        if (r > 3) d[r - 4] = sb4;
-        if (r > 4) d[r - 5] = sb3;
-        if (r > 5) d[r - 6] = sb2;
-        if (r > 6) d[r - 7] = sb1;
+        if (r > 0) {
+            auto pick = [&](int m) -> double {   // sb[m & 7] by a select tree (no scratch)
+                const double x0 = (m & 1) ? sb1 : sb0, x1 = (m & 1) ? sb3 : sb2;
+                const double x2 = (m & 1) ? sb5 : sb4, x3 = (m & 1) ? sb7 : sb6;
+                const double y0 = (m & 2) ? x1 : x0, y1 = (m & 2) ? x3 : x2;
+                return (m & 4) ? y1 : y0;
+            };
+            double4* d = reinterpret_cast<double4*>(out + (n - r));
+            d[0] = make_double4(pick(8 - r), pick(9 - r), pick(10 - r), pick(11 - r));
+            d[1] = make_double4(pick(12 - r), pick(13 - r), pick(14 - r), pick(15 - r));
+        }
     }
-    a.slen[rl * a.n_str + j] = n;
+    a.slen[(int64_t)j * a.slen_stride + rl] = n;   // consecutive lanes, consecutive ints
     if (ovf) atomicOr(&a.status[o], RQ_ST_STREAM_OVERFLOW);
 }
 
@@ -166,7 +171,8 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
     // first replica: the wave's static slot; with a work queue (a.wq) the wave then
     // takes replicas nslot, nslot + 1, ... until the chunk is exhausted
     const int64_t nslot = (int64_t)gridDim.x * a.wpb;
-    for (int64_t rl = (int64_t)blockIdx.x * a.wpb + w; rl < a.n_chunk;) {
+    for (int64_t qi = (int64_t)blockIdx.x * a.wpb + w; qi < a.n_chunk;) {
+    const int64_t rl = a.order ? (int64_t)a.order[qi] : qi;   // longest first (rq_order_replicas)
     const int64_t o = a.chunk0 + rl;
     const int64_t i = rq_global_replica(a.rep0 + o, a.n_rep, a.gen.rep_lo, a.gen.rep_cnt);
     const int g = (int)(i / a.n_rep);
@@ -184,7 +190,6 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
 
     // ---- arrivals: lane owns sources [lane*SPL, lane*SPL+SPL) ----
     const double* st = a.streams + rl * a.capsum;
-    const int* slen = a.slen + rl * a.n_str;
     double head[SPL];
     int pos[SPL], fil[SPL], len[SPL], off[SPL];
     // fast sweep: a register window of each source's next W arrivals (INF past its
@@ -199,7 +204,7 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
     for (int q = 0; q < SPL; ++q) {
         const int j = lane * SPL + q;
         off[q] = j < a.n_str && !MRG ? (int)a.st_off[j] : 0;
-        len[q] = j < a.n_str && !MRG ? slen[j] : 0;
+        len[q] = j < a.n_str && !MRG ? a.slen[(int64_t)j * a.slen_stride + rl] : 0;
         pos[q] = 0;
         fil[q] = 0;
     }
@@ -956,7 +961,7 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
     if (!a.wq) break;
     int nx = 0;
     if (lane == 0) nx = atomicAdd(a.wq, 1);
-    rl = nslot + __builtin_amdgcn_readfirstlane(nx);
+    qi = nslot + __builtin_amdgcn_readfirstlane(nx);
     }   // replica loop
 }
 

@@ -107,7 +107,7 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
     int L = 0;
     const double* src = a.streams;
     if (j < a.n_str) {
-        L = a.slen[rl * a.n_str + j];
+        L = a.slen[(int64_t)j * a.slen_stride + rl];
         src = a.streams + rl * a.capsum + a.st_off[j];
     }
     // the stream's aligned chunks [p8, p8 + 8) in c and [p8 + 8, p8 + 16) in nx, with
@@ -177,7 +177,7 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
         double tau = t_lo + span;
         if (!(tau > t_lo)) tau = next_up(t_lo);
         const double scale = (double)MG_M / (tau - t_lo);
-        const int p0 = p;
+        const int p0 = p, p8_0 = p8;
         // ---- every arrival before tau into the buffer (a lane stops at a full buffer) ----
         bool more = true;
         uint32_t nb1 = 0;   // one-wave blocks: the buffer cursor
@@ -276,8 +276,8 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
         if (nr_all > (uint32_t)MG_CAP) {
             if (tau != next_up(t_lo)) {
                 // too many for one round: undo it and halve the cut
-                p = p0;
-                RQ_MG_RELOAD(p0);
+                p = p0;   // the chunks in registers still hold p0 unless a burst or the shift moved them
+                if (p8 != p8_0) RQ_MG_RELOAD(p0);
                 head = RQ_MG_HEAD();
                 for (int k = tid; k < MG_M; k += MG_B) cnt[k] = 0;
                 __syncthreads();
@@ -373,5 +373,70 @@ hipError_t rq_launch_merge(const MergeArgs& a, hipStream_t s)
         hipLaunchKernelGGL(rq_merge_streams<64>, dim3((unsigned)a.n_chunk), dim3(64), 0, s, a);
     else
         hipLaunchKernelGGL(rq_merge_streams<RQ_MG_B>, dim3((unsigned)a.n_chunk), dim3(RQ_MG_B), 0, s, a);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Longest-first replica order for the sweeps' work queues (LPT): the sweep of a
+// replica costs about its merged length, and the waves take replicas in queue order,
+// so the longest go first and the launch ends on short ones.  One block: a counting
+// sort of the lengths into OB buckets of (max - len) (descending length; replicas of
+// one bucket in any order -- outputs are indexed by replica, so the order changes no
+// result bit, only which wave plays which replica when).
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int OB = 1024;   // threads = buckets
+}
+
+__global__ __launch_bounds__(OB) void rq_order_replicas(const int* __restrict__ len, int n, int* __restrict__ order)
+{
+    __shared__ uint32_t hist[OB];
+    __shared__ int wmn[OB / 64], wmx[OB / 64];
+    __shared__ uint32_t wsm[OB / 64];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    int mn = 0x7fffffff, mx = 0;
+    for (int i = tid; i < n; i += OB) {
+        const int v = len[i];
+        mn = v < mn ? v : mn;
+        mx = v > mx ? v : mx;
+    }
+    hist[tid] = 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const int a = __shfl_xor(mn, o), b = __shfl_xor(mx, o);
+        mn = a < mn ? a : mn;
+        mx = b > mx ? b : mx;
+    }
+    if (lane == 0) {
+        wmn[w] = mn;
+        wmx[w] = mx;
+    }
+    __syncthreads();
+    mn = wmn[0];
+    mx = wmx[0];
+    for (int k = 1; k < OB / 64; ++k) {
+        mn = wmn[k] < mn ? wmn[k] : mn;
+        mx = wmx[k] > mx ? wmx[k] : mx;
+    }
+    const int64_t span = (int64_t)mx - mn + 1;
+    auto bucket = [&](int v) -> int { return (int)(((int64_t)(mx - v) * OB) / span); };
+    for (int i = tid; i < n; i += OB) atomicAdd(&hist[bucket(len[i])], 1u);
+    __syncthreads();
+    const uint32_t h = hist[tid];
+    const uint32_t incl = wave_scan_add(h);
+    if (lane == 63) wsm[w] = incl;
+    __syncthreads();
+    uint32_t wo = 0;
+    for (int k = 0; k < w; ++k) wo += wsm[k];
+    hist[tid] = wo + incl - h;   // bucket base (every thread read its own count above)
+    __syncthreads();
+    for (int i = tid; i < n; i += OB) order[atomicAdd(&hist[bucket(len[i])], 1u)] = i;
+}
+
+hipError_t rq_launch_order(const int* len, int64_t n, int* order, hipStream_t s)
+{
+    if (n <= 0) return hipSuccess;
+    if (n > 65536) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(rq_order_replicas, dim3(1), dim3(OB), 0, s, len, (int)n, order);
     return hipGetLastError();
 }

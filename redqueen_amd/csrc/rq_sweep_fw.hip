@@ -87,7 +87,8 @@ __device__ __forceinline__ void sweep_fw_body(SweepArgs a)
     // replicas nslot, nslot + 1, ... in queue order until the chunk is exhausted (every
     // wave leaves once the counter passes n_chunk)
     const int64_t nslot = (int64_t)gridDim.x * a.wpb;
-    for (int64_t rl = (int64_t)blockIdx.x * a.wpb + w; rl < a.n_chunk;) {
+    for (int64_t qi = (int64_t)blockIdx.x * a.wpb + w; qi < a.n_chunk;) {
+    const int64_t rl = a.order ? (int64_t)a.order[qi] : qi;   // longest first (rq_order_replicas)
     const int64_t o = a.chunk0 + rl;
     const int64_t i = rq_global_replica(a.rep0 + o, a.n_rep, a.gen.rep_lo, a.gen.rep_cnt);
     const int g = (int)(i / a.n_rep);
@@ -508,7 +509,7 @@ __device__ __forceinline__ void sweep_fw_body(SweepArgs a)
     if (!a.wq) break;
     int nx = 0;
     if (lane == 0) nx = atomicAdd(a.wq, 1);
-    rl = nslot + __builtin_amdgcn_readfirstlane(nx);
+    qi = nslot + __builtin_amdgcn_readfirstlane(nx);
     }   // replica loop
 }
 

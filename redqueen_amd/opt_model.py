@@ -302,12 +302,17 @@ def _sig_bad_sources(g, edge_list, s_pw, q):
             if int(j) != g.src_id and not (int(j) in pw and np.max(pw[int(j)]) > 0.0)}
 
 
-def _sig_reach_check(g, edge_list, s_pw, q, ev_src, bad=None):
+def _sig_reach_check(g, edge_list, s_pw, q, ev_src, bad=None, max_events=None):
     """OptPWSignificance raises where the reference does: in a run in which an event
     of a source from _sig_bad_sources is actually played (ev_src = the run's event
-    sources)."""
+    sources) AND handed to the controller's get_next_interval.  run_dynamic hands
+    every played event to the dynamic sources at the start of the next loop step
+    (opt_model.py:271-281), which a max_events cap ends first: the run's last event
+    when it reached the cap is never seen by the controller."""
     if bad is None:
         bad = _sig_bad_sources(g, edge_list, s_pw, q)
+    if max_events is not None and len(ev_src) >= max_events:
+        ev_src = ev_src[:max(0, int(max_events) - 1)]
     hit = [int(j) for j in np.unique(ev_src) if int(j) in bad]
     if hit:
         raise ValueError("cannot convert float NaN to integer (OptPWSignificance.take_one_sample: "
@@ -420,7 +425,7 @@ class Manager:
             s_pw = ctrl._s_pw_for(g.n_followers)
             res = g.run("sig", q=ctrl.q, s_pw=s_pw, period=float(ctrl.time_period), ctrl_seed=seed,
                         max_events=maxev, event_log=True)
-            _sig_reach_check(g, self.edge_list, s_pw, ctrl.q, res.events(0)[1])
+            _sig_reach_check(g, self.edge_list, s_pw, ctrl.q, res.events(0)[1], max_events=maxev)
         elif isinstance(ctrl, Poisson2):
             res = g.run("poisson", ctrl_seed=seed, ctrl_rate=[float(ctrl.rate)], max_events=maxev,
                         event_log=True)

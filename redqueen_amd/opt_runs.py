@@ -12,6 +12,7 @@ import numpy as np
 
 from .utils import add_perf as _add_perf_ks
 from .utils import find_opt_oracle
+from . import utils
 
 
 class _Options:
@@ -104,6 +105,11 @@ def worker_oracle(params):
     RealData broadcaster on the same world (opt_runs.py:129-155)."""
     seed, capacity, max_events, sim_opts, queue = params
     opt_oracle = find_opt_oracle(capacity, sim_opts, max_events=max_events)
+    return _oracle_op(seed, sim_opts, opt_oracle, queue)
+
+
+def _oracle_op(seed, sim_opts, opt_oracle, queue=None):
+    """worker_oracle after its search (opt_runs.py:135-155)."""
     oracle_df = opt_oracle['df']   # sic: KeyError when q = 1 already meets the target
     opt_oracle_mgr = sim_opts.create_manager_with_times(oracle_df.t[oracle_df.events == 1] +
                                                         perf_opts.oracle_eps)
@@ -134,9 +140,15 @@ def extract_perf_fields(return_obj, exclude_fields=None, include_fields=None):
 
 
 def _world_key(so):
-    """The world of a SimOpts without its sources' seeds (batchable replicas share it)."""
+    """The world of a SimOpts without its sources' seeds (batchable replicas share it):
+    the network, the sources' parameters and the followers' significance s (one batch
+    runs every replica with one s per grid point)."""
     from .batch import _val_key
+    s = so.s
+    s_key = repr(sorted((int(k), float(v)) for k, v in s.items())) if isinstance(s, dict) \
+        else _val_key(np.ravel(np.asarray(s, dtype=np.float64)))
     return (so.src_id, float(so.end_time), tuple(map(tuple, so.edge_list)), tuple(so.sink_ids),
+            s_key,
             repr([(n if isinstance(n, str) else n.__name__,
                    sorted((k, _val_key(v)) for k, v in kw.items() if k != "seed"))
                   for n, kw in so.other_sources]))
@@ -249,14 +261,30 @@ def run_inference_queue(N=None, T=None, num_segments=None, sim_opts_gen=None, lo
                 op = worker_opt((seed, w.update({"q": q}), num_segments, None))
                 pp = worker_poisson((seed, op["capacity"], op["sim_opts"], None))
                 pairs.append((op, pp))
-    for op, pp in pairs:
+    # the Oracle legs: every replica's q search in lockstep, one rq_oracle_dp launch per
+    # search round over all of them (utils.find_opt_oracle_batch); the wall of a seed is
+    # the same at every q, so it is simulated once per seed
+    walls = {}
+    for op, _ in pairs:
+        if op["seed"] not in walls:
+            walls[op["seed"]] = utils._wall_df(op["sim_opts"])
+    try:
+        searches = utils.find_opt_oracle_batch(
+            [op["capacity"] for op, _ in pairs], [op["sim_opts"] for op, _ in pairs],
+            [op["world_events"] for op, _ in pairs], walls=[walls[op["seed"]] for op, _ in pairs])
+    except Exception:   # a search raised: every replica's own search below, as the reference
+        searches = [None] * len(pairs)
+    for (op, pp), srch in zip(pairs, searches):
         raw_results.append(op)
         results.append(extract_perf_fields(op))
         capacities[op["q"]].append((op["seed"], op["capacity"]))
         raw_results.append(pp)
         results.append(extract_perf_fields(pp))
         try:
-            orc = worker_oracle((op["seed"], op["capacity"], op["world_events"], op["sim_opts"], None))
+            if srch is None:
+                orc = worker_oracle((op["seed"], op["capacity"], op["world_events"], op["sim_opts"], None))
+            else:
+                orc = _oracle_op(op["seed"], op["sim_opts"], srch)
         except Exception as e:   # the reference's worker_combined: an 'Exception' record
             logging.error("Exception while handling: %r", {"type": "Exception", "error": e,
                                                            "broadcaster_type": "Oracle"})

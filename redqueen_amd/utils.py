@@ -411,37 +411,33 @@ def get_oracle_df(sim_opts, with_cost=False):
         return oracle_df
 
 
-def find_opt_oracle(target_events, sim_opts, max_events=None, tol=1e-2, verbose=False):
-    """Sweep q and get the best run of the oracle (utils.py:260-340): the
-    reference's exponential search + bisection, each step one GPU DP on the
-    (deterministic) wall, which is simulated once."""
+def _oracle_search(target_events, max_events=None, tol=1e-2, verbose=False):
+    """find_opt_oracle's q search (utils.py:260-340) as a coroutine: yields the next q
+    to try, receives (event count, cost) of the oracle there, and returns (q, key) -- key is
+    the reference's result key ('oracle_df' when q = 1 already meets the target,
+    utils.py:277, else 'df').  The exponential search and the bisection are the
+    reference's step for step; only the DP evaluations are batched by the driver."""
     q_hi, q_init, q_lo = 1.0 * 2, 1.0, 1.0 / 2
-    wall = _wall_df(sim_opts)
-
-    def oracle(q):
-        return oracle_ranking(df=wall, sim_opts=sim_opts.update({'q': q}))
 
     def terminate_cond(opt_events):
         return np.abs(opt_events - target_events) / (target_events * 1.0) < tol or \
             (opt_events == np.ceil(target_events)) or \
             (opt_events == np.floor(target_events))
 
-    oracle_df, cost = oracle(q_init)
-    num_events = oracle_df.events.sum()
+    num_events, _ = yield q_init
     if terminate_cond(num_events):
-        return {'q': q_init, 'cost': cost, 'oracle_df': oracle_df}   # sic: key (utils.py:277)
+        return q_init, 'oracle_df'   # sic: key (utils.py:277)
 
     if num_events > target_events:
         while True:
             q_lo = q_init
             q_init *= 2
             q_hi = q_init
-            oracle_df, cost = oracle(q_init)
-            num_events = oracle_df.events.sum()
+            num_events, _ = yield q_init
             if verbose:
                 logTime('q_lo = {}, q_hi = {}, num_events = {} '.format(q_lo, q_hi, num_events))
             if terminate_cond(num_events):
-                return {'q': q_init, 'cost': cost, 'df': oracle_df}
+                return q_init, 'df'
             if num_events <= target_events:
                 break
     elif num_events < target_events:
@@ -449,12 +445,11 @@ def find_opt_oracle(target_events, sim_opts, max_events=None, tol=1e-2, verbose=
             q_hi = q_init
             q_init /= 2
             q_lo = q_init
-            oracle_df, cost = oracle(q_init)
-            num_events = oracle_df.events.sum()
+            num_events, _ = yield q_init
             if verbose:
                 logTime('q_lo = {}, q_hi = {}, num_events = {} '.format(q_lo, q_hi, num_events))
             if terminate_cond(num_events):
-                return {'q': q_init, 'cost': cost, 'df': oracle_df}
+                return q_init, 'df'
             if num_events >= target_events or num_events == max_events:
                 break
 
@@ -463,16 +458,72 @@ def find_opt_oracle(target_events, sim_opts, max_events=None, tol=1e-2, verbose=
 
     while True:
         q_try = (q_lo + q_hi) / 2.0
-        oracle_df, cost = oracle(q_try)
-        opt_events = oracle_df.events.sum()
+        opt_events, cost = yield q_try
         if verbose:
             logTime('q_try = {}, events = {}, cost = {}'.format(q_try, opt_events, cost))
         if terminate_cond(opt_events):
-            return {'q': q_try, 'cost': cost, 'df': oracle_df}
+            return q_try, 'df'
         elif opt_events < target_events:
             q_hi = q_try
         else:
             q_lo = q_try
+
+
+def find_opt_oracle_batch(targets, sim_opts_list, max_events=None, walls=None, tol=1e-2,
+                          verbose=False):
+    """find_opt_oracle for many (target, sim_opts) at once: every search advances in
+    lockstep and each round of q evaluations is ONE rq_oracle_dp launch over all the
+    searches still running (one workgroup per wall).  ``walls``: the wall dataframes
+    (default: each sim_opts' wall, simulated once).  Returns the reference's result
+    dicts, in order."""
+    import pandas as pd
+    n = len(targets)
+    max_events = [None] * n if max_events is None else list(max_events)
+    if walls is None:
+        walls = [_wall_df(so) for so in sim_opts_list]
+    prep = []
+    for k in range(n):
+        wdf = walls[k]
+        follower_ids = sorted(wdf.sink_id.unique())
+        assert len(follower_ids) == 1, "Oracle has been implemented only for 1 follower."
+        event_times, w = _oracle_w(wdf, sim_opts_list[k].end_time)
+        if event_times.shape[0] > 1e6:   # oracle_ranking returns [] (utils.py:205-207)
+            logging.error('Not running for n > 1e6 events')
+            raise ValueError("not enough values to unpack (expected 2, got 0)")
+        prep.append((event_times, w, _scalar_s(sim_opts_list[k].s)))
+    gens = [_oracle_search(targets[k], max_events[k], tol, verbose) for k in range(n)]
+    q_next = [g.send(None) for g in gens]
+    last = [None] * n
+    out = [None] * n
+    active = list(range(n))
+    while active:
+        res = oracle_dp_batch([prep[k][1] for k in active], [float(q_next[k]) for k in active],
+                              [prep[k][2] for k in active])
+        still = []
+        for k, (cost, ev, rk) in zip(active, res):
+            last[k] = (q_next[k], cost, ev, rk)
+            try:
+                q_next[k] = gens[k].send((int(ev.sum()), cost))
+                still.append(k)
+            except StopIteration as stop:
+                q, key = stop.value
+                event_times, w, _ = prep[k]
+                oracle_df = pd.DataFrame.from_dict({
+                    'ranks': rk, 'events': ev,
+                    'at': np.concatenate([[0.0], event_times.values]),
+                    't': np.concatenate([[0.0], event_times.values]),
+                    't_delta': w[1:]})
+                out[k] = {'q': q, 'cost': cost, key: oracle_df}
+        active = still
+    return out
+
+
+def find_opt_oracle(target_events, sim_opts, max_events=None, tol=1e-2, verbose=False):
+    """Sweep q and get the best run of the oracle (utils.py:260-340): the
+    reference's exponential search + bisection, each step one GPU DP on the
+    (deterministic) wall, which is simulated once."""
+    return find_opt_oracle_batch([target_events], [sim_opts], [max_events], tol=tol,
+                                 verbose=verbose)[0]
 
 
 def find_opt_oracle_q(target_events, sim_opts, tol=1e-1, verbose=False):

@@ -45,6 +45,10 @@ for k, rs in rows.items():
         info["frac_active_inst"] = d.get("SQ_ACTIVE_INST_ANY", 0) / wc
         info["frac_wait_any"] = d.get("SQ_WAIT_ANY", 0) / wc
         info["frac_wait_inst"] = d.get("SQ_WAIT_INST_ANY", 0) / wc
+        # wave-slot occupancy of the launch: mean wave lifetime over the launch's duration
+        # (SQ_WAVE_CYCLES in units of 4 cycles; GRBM_GUI_ACTIVE summed over the 8 XCDs)
+        if d.get("SQ_WAVES", 0) > 0 and d.get("GRBM_GUI_ACTIVE", 0) > 0:
+            info["wave_slot_occupancy"] = wc * 4.0 / (d["SQ_WAVES"] * d["GRBM_GUI_ACTIVE"] / 8.0)
     out[k] = info
 meta = {}
 for kv in sys.argv[2:]:

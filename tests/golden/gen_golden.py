@@ -474,6 +474,26 @@ def gen_errors():
             rec["sig_%s_err" % name] = np.asarray(["none"])
         except Exception as e:
             rec["sig_%s_err" % name] = np.asarray([type(e).__name__])
+    # under a max_events cap run_dynamic stops before it hands the last event to the
+    # controller (opt_model.py:271-281): a capped run whose LAST event is the first one
+    # of the unreached source does not raise, one event more does
+    so = SimOpts(**worlds["zerosig"][0])
+    sig = worlds["zerosig"][1]
+    m = so.create_manager_with_significance(3, time_period=10.0, significance=sig)
+    try:
+        m.run_dynamic()
+    except ValueError:
+        pass
+    k = m.state.get_num_events() - 1   # the offending event was applied, then raised on
+    rec["sig_cap_k"] = np.asarray([k])
+    rec["sig_cap_k_src"] = np.asarray([m.state.events[k].src_id])
+    for cap in (k + 1, k + 2):
+        m = so.create_manager_with_significance(3, time_period=10.0, significance=sig)
+        try:
+            m.run_dynamic(max_events=cap)
+            rec["sig_cap_%d_err" % (cap - k)] = np.asarray(["none"])
+        except Exception as e:
+            rec["sig_cap_%d_err" % (cap - k)] = np.asarray([type(e).__name__])
     np.savez_compressed(os.path.join(HERE, "errors.npz"), **rec)
 
 
@@ -626,6 +646,59 @@ def gen_c3_dist(n, start=0, procs=0):
     os.replace(tmp, path)
 
 
+# C4 corners: README graph at the extreme q of the reference's grid (opt_runs.py:289-291)
+# x three follower-significance vectors (the notebook's sim_opts_unequal (0.5, 1.5),
+# opt_broadcast.ipynb:5550, and a strongly unequal (1, 0.25)).  Replica r runs world
+# randomize_other_sources(200 r) (seeds 200 r, 200 r + 99) and RedQueen seed 200 r + 50:
+# no stream is shared between replicas or between the controller and a wall source.
+C4_CORNER_Q = [1e-4, 1e7]
+C4_CORNER_S = [(1.0, 1.0), (0.5, 1.5), (1.0, 0.25)]
+C4_SEED_STRIDE = 200
+C4_OPT_SEED_OFFSET = 50
+
+
+def c4_corners():
+    return [(q, s) for q in C4_CORNER_Q for s in C4_CORNER_S]
+
+
+def _c4_worker(args):
+    p, r = args
+    q, s = c4_corners()[p]
+    kw = dict(README)
+    kw.update(q=q, s=np.asarray(s, dtype=float))
+    so = SimOpts(**kw)
+    u = C4_SEED_STRIDE * r
+    m = so.randomize_other_sources(u).create_manager_with_opt(seed=u + C4_OPT_SEED_OFFSET)
+    m.run_dynamic()
+    df = m.state.get_dataframe()
+    met, own, world = metrics(df, so)
+    return np.concatenate([[own, world, m.state.get_num_events()], met])
+
+
+def gen_c4_dist(n, start=0, procs=0):
+    """The reference's ensembles at the six C4 corners (c4_corners()): n replicas per
+    point, appended to dist_c4.npz from replica `start` (which must be the file's
+    current count), data[point, replica, col]."""
+    path = os.path.join(HERE, "dist_c4.npz")
+    pts = len(c4_corners())
+    jobs = [(p, r) for r in range(start, start + n) for p in range(pts)]
+    with mp.Pool(procs or os.cpu_count()) as pool:
+        res = np.asarray(pool.map(_c4_worker, jobs, chunksize=8))
+    res = res.reshape(n, pts, -1).transpose(1, 0, 2)
+    if start:
+        old = np.load(path)["data"]
+        assert old.shape[1] == start, (old.shape, start)
+        res = np.concatenate([old, res], axis=1)
+    cols = ["posts", "world", "events"] + ["top%d" % k for k in KS] + ["avg", "r2"]
+    tmp = path + ".tmp.npz"
+    np.savez_compressed(tmp, data=res, cols=np.asarray(cols),
+                        q=np.asarray([q for q, _ in c4_corners()]),
+                        s=np.asarray([s for _, s in c4_corners()]),
+                        seed_stride=np.asarray([C4_SEED_STRIDE]),
+                        opt_seed_offset=np.asarray([C4_OPT_SEED_OFFSET]))
+    os.replace(tmp, path)
+
+
 G120_SEED_STRIDE = 20000   # > 99 x the broadcaster count: no shared streams
 
 
@@ -745,12 +818,18 @@ if __name__ == "__main__":
     ap.add_argument("--c3-start", type=int, default=0, help="append to dist_c3.npz from this replica")
     ap.add_argument("--procs", type=int, default=0)
     ap.add_argument("--g120-dist", type=int, default=0, help="only dist_g120.npz with N replicas")
+    ap.add_argument("--c4-dist", type=int, default=0, help="only dist_c4.npz: N more replicas")
+    ap.add_argument("--c4-start", type=int, default=0, help="append to dist_c4.npz from here")
     a = ap.parse_args()
     steps = {"npsum": gen_npsum, "draws": gen_draws, "readme": gen_readme, "kats": gen_kats,
              "adv": gen_adversarial, "graphs": gen_graphs, "frac": gen_frac,
              "oracle": gen_oracle, "sweepq": gen_sweepq, "sig": gen_sig, "realdata": gen_realdata,
              "plugin": gen_plugin, "errors": gen_errors}
-    if a.g120_dist:
+    if a.c4_dist:
+        gen_c4_dist(a.c4_dist, a.c4_start, a.procs)
+        print("done c4 dist", flush=True)
+        a.worlds = True   # nothing else
+    elif a.g120_dist:
         gen_g120_dist(a.g120_dist, a.procs)
         print("done g120 dist", flush=True)
         a.worlds = True   # nothing else

@@ -84,3 +84,50 @@ def test_run_sharded_two_ranks_equals_unsharded():
             assert np.array_equal(rm, m.cpu().numpy()), (name, r)
             assert np.array_equal(rc, c.cpu().numpy()), (name, r)
             assert np.array_equal(rg, gm), (name, r)
+
+
+def _bench_worker(rank, world, port, q):
+    """bench.py's own step function (make_step) on this rank, gloo for the exchange."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    import torch.distributed as dist
+    import bench
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = {}
+    for wl, R in (("c4", 6), ("c3", 48)):
+        so, _ = bench.workload(wl)
+        step, n, _ = bench.make_step(wl, _graph(so), so, R, world, rank, torch.device("cuda", 0), (1,))
+        _, means = step(1)
+        out[wl] = (n, means.cpu().numpy())
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_step_two_ranks_equals_one():
+    """bench.py's step at world size 2 (C4: each rank the replica window of every grid
+    point; C3: each rank its own replicas) gathers the same rows and so computes the
+    same ensemble / per-grid-point means, bit for bit, as one rank running the whole
+    step (the driver's N-GPU bench runs exactly this step over RCCL)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import bench
+    ctx = mp.get_context("spawn")
+    qu = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, 2, port, qu)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(qu.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for wl, R in (("c4", 6), ("c3", 48)):
+        so, _ = bench.workload(wl)
+        step, n, _ = bench.make_step(wl, _graph(so), so, 2 * R, 1, 0, torch.device("cuda", 0), (1,))
+        _, means = step(1)
+        for r in (0, 1):
+            assert got[r][wl][0] == n
+            assert np.array_equal(got[r][wl][1], means.cpu().numpy()), (wl, r)

@@ -113,3 +113,35 @@ def test_reference_configs_exist():
     for o in (R.poisson_inf_opts, R.hawkes_inf_opts, R.piecewise_inf_opts):
         so = o.sim_opts_gen(3)
         assert so.end_time == R.simulation_opts.T and R._randomize_seed(so) is not None
+
+
+def test_per_seed_significance_unbatchable():
+    """worlds that differ only in the followers' significance s must not
+    share one batch (the batch runs one s); each replica then runs its own s, and every
+    row still equals the engine oracle on that replica's own SimOpts."""
+    O, R, SimOpts = _ctx()
+    base = _gen(SimOpts)
+
+    def gen(seed):
+        return base(seed).update({"s": np.asarray([1.0 + seed])})
+    assert R._world_key(gen(0)) != R._world_key(gen(1))
+    assert R._world_key(base(0)) == R._world_key(base(1))
+    out = R.run_inference_queue(N=2, T=20.0, num_segments=4, sim_opts_gen=gen, log_q_high=3,
+                                log_q_low=-1)
+    _check_against_oracle(O, R, out, gen, 2, 20.0)
+
+
+def test_oracle_batch_equals_single_searches():
+    """utils.find_opt_oracle_batch (every search in lockstep, one DP launch per round)
+    returns what find_opt_oracle returns search by search."""
+    O, R, SimOpts = _ctx()
+    from redqueen_amd import utils as U
+    gen = _gen(SimOpts)
+    sos = [gen(s).update({"q": q}) for s in range(3) for q in (0.1, 10.0)]
+    targets = [3.0, 7.0, 12.0, 2.0, 5.0, 9.0]
+    got = U.find_opt_oracle_batch(targets, sos, [None] * len(sos))
+    for t, so, g in zip(targets, sos, got):
+        want = U.find_opt_oracle(t, so)
+        assert set(g) == set(want) and g["q"] == want["q"] and g["cost"] == want["cost"]
+        key = "df" if "df" in g else "oracle_df"
+        assert g[key].equals(want[key])

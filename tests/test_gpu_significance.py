@@ -158,3 +158,39 @@ def test_silent_unreached_source_does_not_raise():
     m = so.create_manager_with_significance(3, time_period=10.0, significance=sig)
     m.run_dynamic()
     assert m.state.get_num_events() > 0
+
+
+def test_capped_last_event_like_reference(golden):
+    """Under a max_events cap run_dynamic stops before it hands its last event to the
+    controller (opt_model.py:271-281): the reference does not raise when the capped
+    run's LAST event is the first one of a source that reaches no follower with
+    positive significance, and raises one event later (errors.npz sig_cap_*: k = the
+    index of that event in the reference's run).  The facade and the batch agree, at
+    the k of the engine's own run."""
+    torch, engine, graphs, O = _ctx()
+    from redqueen_amd import batch
+    from redqueen_amd.opt_model import SimOpts
+    g = golden("errors.npz")
+    assert str(g["sig_cap_1_err"][0]) == "none" and str(g["sig_cap_2_err"][0]) == "ValueError"
+    w, sig = _err_worlds()["zerosig"]
+    so = SimOpts(**w)
+    first_raise = None
+    for cap in range(1, 200):
+        m = so.create_manager_with_significance(3, time_period=10.0, significance=sig)
+        try:
+            m.run_dynamic(max_events=cap)
+        except ValueError:
+            first_raise = cap
+            break
+        df = m.state.get_dataframe()
+        assert 1001 not in set(df.src_id[df.event_id < df.event_id.max()])
+    assert first_raise is not None and first_raise >= 2
+    k = first_raise - 2   # cap k + 1 ran, cap k + 2 raised
+    m = so.create_manager_with_significance(3, time_period=10.0, significance=sig)
+    m.run_dynamic(max_events=k + 1)
+    ev = m.state.get_dataframe().groupby("event_id").src_id.first().values
+    assert len(ev) == k + 1 and ev[k] == 1001
+    # the batch on the same run (controller seed 3, the world's own seeds)
+    batch.run_significance(so, sig, 10.0, seeds=[3], randomize=False, max_events=k + 1)
+    with pytest.raises(ValueError):
+        batch.run_significance(so, sig, 10.0, seeds=[3], randomize=False, max_events=k + 2)
