@@ -204,7 +204,7 @@ def main():
     g = engine.Graph(so["src_id"], so["other_sources"], so["sink_ids"], so["edge_list"],
                      so["end_time"])
     # replicas per GPU per step (c4: per grid point per GPU)
-    R = a.replicas or {"c5": 8192, "c4": 1000}.get(a.workload, 10000)
+    R = a.replicas or {"c5": 4096, "c4": 1000}.get(a.workload, 10000)
     Ks = (1,)
     step, rep_step, pkw = make_step(a.workload, g, so, R, world, rank, dev, Ks)
     plan = g.run("opt", plan_only=True, **pkw)

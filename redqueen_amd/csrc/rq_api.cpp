@@ -520,8 +520,7 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     // (the sweep is latency-bound per replica: a chunk much below the resident wave
     // slots leaves them empty)
     p->nbuf = 1;
-    p->order = p->mrg && !p->log;
-    if (const char* e = getenv("RQ_ORDER")) p->order = p->order && atoi(e) != 0;   // A/B only
+    p->order = false;
     if (p->mrg && !p->log) {
         int nb = 2;
         if (const char* e = getenv("RQ_PIPE")) nb = std::max(1, std::min(3, atoi(e)));   // A/B only
@@ -533,9 +532,29 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
             nch = std::max<int64_t>(1, std::min(nch, p->R));
             p->chunk = (p->R + nch - 1) / nch;
         }
-        const int64_t nch = (p->R + p->chunk - 1) / p->chunk;
+        int64_t nch = (p->R + p->chunk - 1) / p->chunk;
         p->nbuf = (int)std::min<int64_t>(nb, nch);
+        // device-memory budget of the buffer sets in flight (C5: ~47 MB per replica):
+        // smaller chunks (an even count) until nbuf of them fit
+        if (p->nbuf > 1 && b->chunk <= 0) {
+            double budget = 200.0 * (1 << 30);
+            if (const char* e = getenv("RQ_WS_BUDGET_GB")) budget = atof(e) * (1 << 30);   // tuning only
+            const double per_rep = 8.0 * (double)p->capsum + 4.0 * g->n_str + 10.0 * (double)p->capsum +
+                                   (double)p->cap_rows * (20.0 + 4.0 * p->nK) + 16.0;
+            const int64_t fit = std::max<int64_t>(1, (int64_t)(budget / (p->nbuf * per_rep)));
+            if (p->chunk > fit) {
+                nch = (p->R + fit - 1) / fit;
+                nch = (nch + 1) & ~(int64_t)1;
+                p->chunk = (p->R + nch - 1) / nch;
+            }
+        }
     }
+
+    // longest-first order (rq_order_replicas) only where the sweep's work queue hands out
+    // replicas: a chunk larger than the resident wave slots (else every replica has its
+    // own wave from the start and the order changes nothing)
+    if (p->mrg && !p->log && p->chunk > (int64_t)std::max(1, p->wpc) * rq_cu_count()) p->order = true;
+    if (const char* e = getenv("RQ_ORDER")) p->order = p->order && atoi(e) != 0;   // A/B only
 
     const size_t A = 256;
     const int64_t C = p->chunk;

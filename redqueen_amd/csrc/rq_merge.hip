@@ -338,8 +338,16 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
                 const double y = st[k];
                 r += (y < x || (y == x && sk[k] < kx)) ? 1 : 0;
             }
-            out_t[outpos + g0 + r] = x;
-            out_j[outpos + g0 + r] = (uint16_t)(kx >> MG_SB);
+#ifndef RQ_MG_NT
+#define RQ_MG_NT 0
+#endif
+            if (RQ_MG_NT) {   // streaming stores: the output must not evict the input lines
+                __builtin_nontemporal_store(x, &out_t[outpos + g0 + r]);
+                __builtin_nontemporal_store((uint16_t)(kx >> MG_SB), &out_j[outpos + g0 + r]);
+            } else {
+                out_t[outpos + g0 + r] = x;
+                out_j[outpos + g0 + r] = (uint16_t)(kx >> MG_SB);
+            }
         }
         RQ_MG_TICK(6);
         outpos += nr;
@@ -379,64 +387,59 @@ hipError_t rq_launch_merge(const MergeArgs& a, hipStream_t s)
 // ---------------------------------------------------------------------------
 // Longest-first replica order for the sweeps' work queues (LPT): the sweep of a
 // replica costs about its merged length, and the waves take replicas in queue order,
-// so the longest go first and the launch ends on short ones.  One block: a counting
-// sort of the lengths into OB buckets of (max - len) (descending length; replicas of
-// one bucket in any order -- outputs are indexed by replica, so the order changes no
-// result bit, only which wave plays which replica when).
+// so the longest go first and the launch ends on short ones.  One wave (it must find a
+// slot while another stream's sweep holds the chip): a counting sort of the lengths
+// into OB buckets of (max - len) (descending length; replicas of one bucket in any
+// order -- outputs are indexed by replica, so the order changes no result bit, only
+// which wave plays which replica when).
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int OB = 1024;   // threads = buckets
+constexpr int OB = 1024;   // buckets (16 per lane)
 }
 
-__global__ __launch_bounds__(OB) void rq_order_replicas(const int* __restrict__ len, int n, int* __restrict__ order)
+__global__ __launch_bounds__(64) void rq_order_replicas(const int* __restrict__ len, int n, int* __restrict__ order)
 {
     __shared__ uint32_t hist[OB];
-    __shared__ int wmn[OB / 64], wmx[OB / 64];
-    __shared__ uint32_t wsm[OB / 64];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int lane = threadIdx.x;
     int mn = 0x7fffffff, mx = 0;
-    for (int i = tid; i < n; i += OB) {
+    for (int i = lane; i < n; i += 64) {
         const int v = len[i];
         mn = v < mn ? v : mn;
         mx = v > mx ? v : mx;
     }
-    hist[tid] = 0;
+    for (int k = lane; k < OB; k += 64) hist[k] = 0;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         const int a = __shfl_xor(mn, o), b = __shfl_xor(mx, o);
         mn = a < mn ? a : mn;
         mx = b > mx ? b : mx;
     }
-    if (lane == 0) {
-        wmn[w] = mn;
-        wmx[w] = mx;
-    }
-    __syncthreads();
-    mn = wmn[0];
-    mx = wmx[0];
-    for (int k = 1; k < OB / 64; ++k) {
-        mn = wmn[k] < mn ? wmn[k] : mn;
-        mx = wmx[k] > mx ? wmx[k] : mx;
-    }
     const int64_t span = (int64_t)mx - mn + 1;
     auto bucket = [&](int v) -> int { return (int)(((int64_t)(mx - v) * OB) / span); };
-    for (int i = tid; i < n; i += OB) atomicAdd(&hist[bucket(len[i])], 1u);
-    __syncthreads();
-    const uint32_t h = hist[tid];
-    const uint32_t incl = wave_scan_add(h);
-    if (lane == 63) wsm[w] = incl;
-    __syncthreads();
-    uint32_t wo = 0;
-    for (int k = 0; k < w; ++k) wo += wsm[k];
-    hist[tid] = wo + incl - h;   // bucket base (every thread read its own count above)
-    __syncthreads();
-    for (int i = tid; i < n; i += OB) order[atomicAdd(&hist[bucket(len[i])], 1u)] = i;
+    wave_lds_sync();
+    for (int i = lane; i < n; i += 64) atomicAdd(&hist[bucket(len[i])], 1u);
+    wave_lds_sync();
+    // exclusive scan: lane l owns buckets [16 l, 16 l + 16)
+    uint32_t h[OB / 64], sum = 0;
+#pragma unroll
+    for (int k = 0; k < OB / 64; ++k) {
+        h[k] = hist[lane * (OB / 64) + k];
+        sum += h[k];
+    }
+    uint32_t base = wave_scan_add(sum) - sum;
+#pragma unroll
+    for (int k = 0; k < OB / 64; ++k) {
+        hist[lane * (OB / 64) + k] = base;
+        base += h[k];
+    }
+    wave_lds_sync();
+    for (int i = lane; i < n; i += 64) order[atomicAdd(&hist[bucket(len[i])], 1u)] = i;
 }
 
 hipError_t rq_launch_order(const int* len, int64_t n, int* order, hipStream_t s)
 {
     if (n <= 0) return hipSuccess;
     if (n > 65536) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(rq_order_replicas, dim3(1), dim3(OB), 0, s, len, (int)n, order);
+    hipLaunchKernelGGL(rq_order_replicas, dim3(1), dim3(64), 0, s, len, (int)n, order);
     return hipGetLastError();
 }

@@ -39,7 +39,9 @@ def main():
         for mode in ("batched", "per_replica"):
             if mode == "per_replica":
                 def one_by_one(targets, sos, max_events=None, walls=None, **kw):
-                    raise RuntimeError("force the per-replica searches")
+                    # each replica's search on its own: one DP launch per search step
+                    return [batch_fn([t], [so], [me], walls=[w], **kw)[0]
+                            for t, so, me, w in zip(targets, sos, max_events, walls)]
                 U.find_opt_oracle_batch = one_by_one
             t0 = time.perf_counter()
             out = R.run_inference_queue(opts=cfg[name])

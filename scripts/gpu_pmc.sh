@@ -26,6 +26,10 @@ timeout -k 10 -s KILL 120 rocprofv3 --pmc FETCH_SIZE $P -d "$OUT/p3" -o p3 -- py
 echo "fetch ok"
 timeout -k 10 -s KILL 120 rocprofv3 --pmc WRITE_SIZE $P -d "$OUT/p4" -o p4 -- python3 $B > "$OUT/p4.log" 2>&1 || { echo p4 failed; tail -5 "$OUT/p4.log"; exit 1; }
 echo "write ok"
+# read requests by size: exact read bytes for any access width (FETCH_SIZE tallies every
+# request as 64 B: x2 is exact only for whole-line reads, profiles/r04_calib_half.txt)
+timeout -k 10 -s KILL 120 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum $P -d "$OUT/p5" -o p5 -- python3 $B > "$OUT/p5.log" 2>&1 || { echo p5 failed; tail -5 "$OUT/p5.log"; exit 1; }
+echo "rdreq ok"
 timeout -k 10 -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU $P -d "$OUT/p1" -o p1 -- python3 $B > "$OUT/p1.log" 2>&1 || { echo p1 failed; tail -5 "$OUT/p1.log"; exit 1; }
 echo "sq1 ok"
 timeout -k 10 -s KILL 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT $P -d "$OUT/p2" -o p2 -- python3 $B > "$OUT/p2.log" 2>&1 || { echo p2 failed; tail -5 "$OUT/p2.log"; exit 1; }

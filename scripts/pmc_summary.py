@@ -38,6 +38,14 @@ for k, rs in rows.items():
             "lds": int(r0.get("LDS_Block_Size", 0) or 0), "counters": d}
     if "FETCH_SIZE" in d:
         info["hbm_read_bytes"] = d["FETCH_SIZE"] * 1024 * 2
+    if "TCC_EA0_RDREQ_sum" in d and "TCC_EA0_RDREQ_64B_sum" in d:
+        # read bytes by request size (exact for any access width; FETCH_SIZE x2 is exact
+        # only for whole-line reads: profiles/r04_calib_half.txt)
+        n32 = d.get("TCC_EA0_RDREQ_32B_sum", 0.0)
+        n64 = d.get("TCC_EA0_RDREQ_64B_sum", 0.0)
+        n128 = d.get("TCC_EA0_RDREQ_128B_sum", 0.0)
+        info["hbm_read_bytes_by_req"] = 32 * n32 + 64 * n64 + 128 * n128
+        info["rdreq"] = {"all": d["TCC_EA0_RDREQ_sum"], "32B": n32, "64B": n64, "128B": n128}
     if "WRITE_SIZE" in d:
         info["hbm_write_bytes"] = d["WRITE_SIZE"] * 1024
     if "SQ_WAVE_CYCLES" in d and d["SQ_WAVE_CYCLES"] > 0:

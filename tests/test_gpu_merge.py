@@ -135,3 +135,23 @@ def test_merged_tie_group_beyond_round_capacity():
     met, (t_o, _, s_o) = O.engine_metrics(O.Scenario(so, ("opt", 4)), (1, 2))
     top, avg, r2, _ = met
     assert np.array_equal(b.metrics[0].cpu().numpy(), np.asarray(list(top) + [avg, r2]))
+
+
+@pytest.mark.parametrize("wl", ["c3", "g120"])
+def test_pipelined_chunks_and_longest_first_order(wl):
+    """rq_run_batch's chunk plans change no result bit: one chunk larger than the resident
+    sweep slots (the work queue hands out replicas in the longest-first order of
+    rq_order_replicas), the default two pipelined chunks, and many small chunks on two
+    streams (fork / join events) give identical per-replica outputs."""
+    torch, engine, graphs, O = _ctx()
+    so = getattr(graphs, wl)()
+    g = _graph(engine, so)
+    R = 9000 if wl == "c3" else 12000
+    kw = dict(q=so["q"], s=so["s"], n_rep=R, ctrl_seed=77, world_seed=77, randomize=True, Ks=(1,))
+    one = g.run("opt", chunk=R, **kw)
+    assert g.run("opt", chunk=R, plan_only=True, **kw)["chunk"] == R
+    dflt = g.run("opt", **kw)
+    small = g.run("opt", chunk=700, **kw)
+    assert int(one.status.max().item()) == 0
+    _same(torch, one, dflt)
+    _same(torch, one, small)
