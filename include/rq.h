@@ -151,23 +151,28 @@ typedef struct rq_batch_desc {
     int64_t max_events;          /* run_dynamic(max_events); < 0 = unbounded                     */
     int32_t flags;               /* RQ_RUN_EVENT_LOG                                              */
     double cap_scale;            /* >= 1: multiplies every auto-sized capacity                   */
-    int64_t chunk;               /* replicas in flight per launch wave (0 = library default)     */
+    int64_t chunk;               /* replicas per launch (0 = library default: the batch in an   */
+                                 /* even number of chunks of <= 16384, pipelined on two streams */
+                                 /* within a 200 GiB workspace budget)                          */
     int64_t replica0;            /* this call runs global replicas [replica0, replica0+n_local):  */
     int64_t n_local;             /* a shard of the grid (0 = all n_grid*n_rep); outputs are      */
                                  /* indexed locally, seeds and grid point use the global id     */
-    int32_t sweep_mode;          /* 0 auto: fast tiled sweep unless the run needs the sequential
-                                    one (max_events, RealData); the fast sweeps write the event
-                                    log themselves; 1 fast whenever max_events allows; 2 force the sequential sweep;
-                                    3 as 0 but never a K=1 sink-bit variant (per-sink ranks);
-                                    4 / 5 as 0 / 1 on the legacy kernels (arrival streams
-                                    pre-generated into HBM by rq_gen_streams and merged into one
-                                    (t, source) sequence per replica by rq_merge_streams) --
-                                    kept for A/B parity checks of the fused sweep;
-                                    6 as 4, the general sweep merging the per-source streams
-                                    itself (register windows; the round-2 kernel);
-                                    7 as 0, the fused sweep generating its arrivals in-kernel
-                                    (LDS rings) instead of playing merged streams            */
-                                 /* sweep; both are bit-identical, auto picks the faster one    */
+    int32_t sweep_mode;          /* 0 auto: a fast tiled sweep unless the run needs the exact
+                                    sequential one (max_events, RealData, a multigraph, > 512
+                                    sources); the fast sweeps write the event log themselves.
+                                    The fast sweeps play MERGED streams: rq_gen_streams writes
+                                    every source's arrivals, rq_merge_streams merges them into
+                                    one (t, stream) sequence per replica, and the sweep plays it
+                                    in tiles of 64 entries (the fused sweep for <= 64 sources,
+                                    the general sweep above);
+                                    1 fast whenever max_events allows; 2 force the sequential
+                                    sweep; 3 as 0 but never a K=1 sink-bit variant (per-sink
+                                    ranks); 4 / 5 as 0 / 1 on the general sweep instead of the
+                                    fused one; 6 as 4 with the general sweep merging the
+                                    per-source streams itself (register windows, the round-2
+                                    kernel); 7 as 0 with the fused sweep generating its arrivals
+                                    in-kernel (LDS rings, the round-2 kernel).  Every variant
+                                    gives the same bits; 6 and 7 are kept for A/B checks      */
     /* RQ_SRC_OPTPW (create_manager_with_significance, opt_model.py:850-884): the follower
        significance s_pw[g][f][k] over n_seg equal segments of time_period, rows in the
        order of rq_graph_followers (sorted follower ids), q from q[g] */

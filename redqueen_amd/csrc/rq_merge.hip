@@ -66,6 +66,17 @@ __device__ __forceinline__ Chunk load_chunk(const double* p)
     return Chunk{q[0], q[1]};
 }
 
+// the second half of a 128-byte line, whose first half was read before: nothing reads
+// the line again, so it is loaded non-temporally (the L2 may drop it first and keep the
+// lines whose second half is still to come)
+typedef double rq_v4d __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ Chunk load_chunk_last(const double* p)
+{
+    const rq_v4d* q = reinterpret_cast<const rq_v4d*>(p);
+    const rq_v4d x = __builtin_nontemporal_load(q), y = __builtin_nontemporal_load(q + 1);
+    return Chunk{make_double4(x.x, x.y, x.z, x.w), make_double4(y.x, y.y, y.z, y.w)};
+}
+
 // arrival k (0..15) of the two chunks; both halves selected as values (a select of the
 // chunks themselves would put them in scratch memory)
 __device__ __forceinline__ double sel16(Chunk c, Chunk nx, int k)
@@ -263,7 +274,13 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
         if (p - p8 >= 8) {   // into nx: its successor's load overlaps the rest of the round
             c = nx;
             p8 += 8;
-            nx = RQ_MG_CHUNK(p8 + 8);
+#ifndef RQ_MG_NTL
+#define RQ_MG_NTL 1
+#endif
+            if (RQ_MG_NTL && ((p8 + 8) & 8))   // the second half of its line: the line's last use
+                nx = load_chunk_last(src + ((p8 + 8) < lastc ? (p8 + 8) : lastc));
+            else
+                nx = RQ_MG_CHUNK(p8 + 8);
         }
         if constexpr (MG_W == 1) {
             if (lane == 0) nb = nb1;
@@ -339,9 +356,11 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
                 r += (y < x || (y == x && sk[k] < kx)) ? 1 : 0;
             }
 #ifndef RQ_MG_NT
-#define RQ_MG_NT 0
+#define RQ_MG_NT 1
 #endif
-            if (RQ_MG_NT) {   // streaming stores: the output must not evict the input lines
+            // streaming stores: the output must not evict the input lines (C3 merge reads
+            // 1.71 -> 1.37 x its 8 B per arrival, profiles/r04_merge_traffic.txt)
+            if (RQ_MG_NT) {
                 __builtin_nontemporal_store(x, &out_t[outpos + g0 + r]);
                 __builtin_nontemporal_store((uint16_t)(kx >> MG_SB), &out_j[outpos + g0 + r]);
             } else {
