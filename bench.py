@@ -204,7 +204,9 @@ def main():
     g = engine.Graph(so["src_id"], so["other_sources"], so["sink_ids"], so["edge_list"],
                      so["end_time"])
     # replicas per GPU per step (c4: per grid point per GPU)
-    R = a.replicas or {"c5": 4096, "c4": 1000}.get(a.workload, 10000)
+    # C5: 8192 = two pipelined chunks of 4096 (the general sweep's resident waves): 16.0k
+    # replicas/s against 15.8k at 4096 (profiles/r04_c5_ab.txt)
+    R = a.replicas or {"c5": 8192, "c4": 1000}.get(a.workload, 10000)
     Ks = (1,)
     step, rep_step, pkw = make_step(a.workload, g, so, R, world, rank, dev, Ks)
     plan = g.run("opt", plan_only=True, **pkw)

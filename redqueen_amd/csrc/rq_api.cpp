@@ -190,6 +190,7 @@ struct Plan {
     // per-source merge inside the sweep instead)
     bool mrg = false;
     size_t off_mt = 0, off_mj = 0, off_mlen = 0;
+    int64_t mrg_stride = 0;   // merged entries per replica (capacity)
     // the fused sweep's phases B / C on merged streams (rq_gen_streams + rq_merge_streams
     // instead of in-kernel generation; sweep_mode 7: the in-kernel generating sweep)
     bool fwm = false;
@@ -305,7 +306,7 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
             p->rd_k[jk] = k;
         }
     }
-    double wall_caps = 0.0;
+    double wall_caps = 0.0, wall_mean = 0.0, wall_var = 0.0;
     int64_t ctrl_cap = 0;
     for (int j = 0; j < g->n_str; ++j) {
         int kind = g->kind[j];
@@ -322,10 +323,32 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
         p->cap[j] = (int)c;
         p->st_off[j] = p->capsum;
         p->capsum += c;
-        if (j == g->ctrl_idx) ctrl_cap = c;
-        else wall_caps += (double)c;
+        if (j == g->ctrl_idx) {
+            ctrl_cap = c;
+        } else {
+            wall_caps += (double)c;
+            if (kind != RQ_SRC_NONE) {
+                wall_mean += kind == RQ_SRC_REALDATA ? (double)c : m;
+                wall_var += var;
+            }
+        }
     }
-    double rows = wall_caps + ((ck == RQ_SRC_OPT || ck == RQ_SRC_OPTPW) ? wall_caps + 1.0 : (double)ctrl_cap) + 8.0;
+    // the wall events of a replica together: mean + 8 sigma of their SUM (the streams'
+    // own 8-sigma capacities add up to far more: C5 769k against 511k); a replica past it
+    // is flagged (RQ_ST_STREAM_OVERFLOW / RQ_ST_ROWS_OVERFLOW) and Graph.run(check=True)
+    // reruns the batch with doubled capacities
+    double squeeze = 1.0;   // tests only: undersized capacities exercise the overflow reruns
+    if (const char* e = getenv("RQ_CAP_SQUEEZE")) squeeze = std::max(0.01, std::min(1.0, atof(e)));
+    const double walls_agg = std::ceil((wall_mean + 8.0 * std::sqrt(wall_var) + 32.0) * scale * squeeze);
+    const bool opt_ctrl = ck == RQ_SRC_OPT || ck == RQ_SRC_OPTPW;
+    // merged sequence per replica: every arrival of every stream (the controlled one too)
+    p->mrg_stride = std::min<int64_t>(p->capsum, ((int64_t)walls_agg + ctrl_cap + 64 + 15) & ~(int64_t)15);
+    // pivot rows <= events: walls + posts; RedQueen posts at most once per wall event (+1),
+    // so the old bound was 2 x the walls; posts are sized max(4096, walls / 4) now (C3: ~180
+    // per replica, C5: ~1400; the C4 grid's q = 1e-4 corner: 1816 on 2075 walls)
+    double rows = wall_caps + (opt_ctrl ? wall_caps + 1.0 : (double)ctrl_cap) + 8.0;
+    rows = std::min(rows, walls_agg + (opt_ctrl ? std::max(4096.0, std::ceil(walls_agg / 4.0)) + 1.0
+                                                : (double)ctrl_cap) + 8.0);
     if (b->max_events >= 0) rows = std::min(rows, (double)b->max_events + 1.0);
     // a multiple of 32 rows: replica row bases stay aligned to the scan's 32-row trips
     p->cap_rows = (std::max<int64_t>(64, (int64_t)rows) + 31) & ~(int64_t)31;
@@ -539,8 +562,9 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
         if (p->nbuf > 1 && b->chunk <= 0) {
             double budget = 200.0 * (1 << 30);
             if (const char* e = getenv("RQ_WS_BUDGET_GB")) budget = atof(e) * (1 << 30);   // tuning only
-            const double per_rep = 8.0 * (double)p->capsum + 4.0 * g->n_str + 10.0 * (double)p->capsum +
-                                   (double)p->cap_rows * (20.0 + 4.0 * p->nK) + 16.0;
+            const double rows_b = (double)p->cap_rows * (20.0 + 4.0 * p->nK);
+            const double per_rep = std::max(8.0 * (double)p->capsum, rows_b) + 4.0 * g->n_str +
+                                   10.0 * (double)p->mrg_stride + 16.0;
             const int64_t fit = std::max<int64_t>(1, (int64_t)(budget / (p->nbuf * per_rep)));
             if (p->chunk > fit) {
                 nch = (p->R + fit - 1) / fit;
@@ -550,11 +574,12 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
         }
     }
 
-    // longest-first order (rq_order_replicas) only where the sweep's work queue hands out
-    // replicas: a chunk larger than the resident wave slots (else every replica has its
-    // own wave from the start and the order changes nothing)
-    if (p->mrg && !p->log && p->chunk > (int64_t)std::max(1, p->wpc) * rq_cu_count()) p->order = true;
-    if (const char* e = getenv("RQ_ORDER")) p->order = p->order && atoi(e) != 0;   // A/B only
+    // longest-first order (rq_order_replicas) of the replicas the sweep's work queue hands
+    // out (a chunk larger than the resident wave slots): measured neutral on C3 (3.01 vs
+    // 3.02 ms per step) and slower on C5 (8192 replicas in one chunk: sweep 424 ms against
+    // 400 ms in index order, profiles/r04_c5_ab.txt) -- off unless RQ_ORDER=1 (A/B)
+    if (const char* e = getenv("RQ_ORDER"))
+        p->order = atoi(e) != 0 && p->mrg && !p->log && p->chunk > (int64_t)std::max(1, p->wpc) * rq_cu_count();
 
     const size_t A = 256;
     const int64_t C = p->chunk;
@@ -574,17 +599,26 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     const size_t o_set = o;
     o = 0;
     const int64_t strm = p->fw && !p->fwm ? 0 : C;   // the generating fused sweep keeps its arrivals in LDS
-    p->off_streams = o; o = align_up(o + sizeof(double) * (size_t)strm * p->capsum, A);
+    const size_t strm_bytes = sizeof(double) * (size_t)strm * p->capsum;
     p->off_slen = o;    o = align_up(o + sizeof(int) * (size_t)strm * g->n_str, A);
     const int64_t mrgc = p->mrg ? C : 0;   // merged sequences: t f64, stream u16, length
-    p->off_mt = o;      o = align_up(o + sizeof(double) * (size_t)mrgc * p->capsum, A);
-    p->off_mj = o;      o = align_up(o + sizeof(uint16_t) * (size_t)mrgc * p->capsum, A);
+    p->off_mt = o;      o = align_up(o + sizeof(double) * (size_t)mrgc * p->mrg_stride, A);
+    p->off_mj = o;      o = align_up(o + sizeof(uint16_t) * (size_t)mrgc * p->mrg_stride, A);
     p->off_mlen = o;    o = align_up(o + sizeof(int) * (size_t)mrgc, A);
     p->off_ord = o;     o = align_up(o + sizeof(int) * (size_t)(p->order ? C : 0), A);
+    const size_t o_rows = o;
     p->off_rt = o;      o = align_up(o + sizeof(double) * (size_t)C * p->cap_rows, A);
     p->off_rs = o;      o = align_up(o + sizeof(double) * (size_t)C * p->cap_rows, A);
     p->off_rv = o;      o = align_up(o + sizeof(uint32_t) * (size_t)C * p->cap_rows, A);
     p->off_rc = o;      o = align_up(o + sizeof(uint32_t) * (size_t)C * p->cap_rows * p->nK, A);
+    // the per-source streams are dead once merged (rq_merge_streams runs before the sweep
+    // writes its first row, in the same stream's order): they share the pivot rows' bytes
+    if (p->mrg && strm_bytes <= o - o_rows) {
+        p->off_streams = o_rows;
+    } else {
+        p->off_streams = o;
+        o = align_up(o + strm_bytes, A);
+    }
     p->off_sall = o;    o = align_up(o + sizeof(int) * (size_t)C, A);
     p->off_wq = o;      o = align_up(o + 2 * sizeof(int), A);   // [0] sweep, [1] scan queue
     p->set_stride = o;
@@ -1045,6 +1079,7 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             ma.out_t = (double*)(wsb + p.off_mt);
             ma.out_j = (uint16_t*)(wsb + p.off_mj);
             ma.out_len = (int*)(wsb + p.off_mlen);
+            ma.mrg_stride = p.mrg_stride;
             ma.status = out->status;
 #ifdef RQ_PHASE_CLOCK
             if (getenv("RQ_CLK_MERGE")) ma.clk = phase_clk();   // else the sweep's phases only
@@ -1091,6 +1126,7 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             sa.mrg_t = (const double*)(wsb + p.off_mt);
             sa.mrg_j = (const uint16_t*)(wsb + p.off_mj);
             sa.mrg_len = (const int*)(wsb + p.off_mlen);
+            sa.mrg_stride = p.mrg_stride;
             if (p.order) {
                 int* ord = (int*)(wsb + p.off_ord);
                 if (rq_launch_order(sa.mrg_len, C, ord, s) != hipSuccess) return RQ_EHIP;

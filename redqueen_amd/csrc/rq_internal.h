@@ -116,10 +116,11 @@ struct SweepArgs {
     int64_t gs_stride;
     int gs_slots;
     // general fast sweep on merged streams (rq_merge_streams): replica rl's arrivals of
-    // every source in play order, mrg_t / mrg_j [rl * capsum + k], k < mrg_len[rl]
+    // every source in play order, mrg_t / mrg_j [rl * mrg_stride + k], k < mrg_len[rl]
     const double* mrg_t;
     const uint16_t* mrg_j;
     const int* mrg_len;
+    int64_t mrg_stride;        // entries per replica of mrg_t / mrg_j
     // longest-first play order of the chunk's replicas (rq_order_replicas over mrg_len):
     // the wave slots and the work queue take chunk replica order[q] for queue position q
     // (null: q itself).  Outputs stay indexed by replica, so no result bit depends on it.
@@ -138,9 +139,10 @@ struct MergeArgs {
     const int* slen;        // [n_str][slen_stride]
     int64_t slen_stride;
     double end;
-    double* out_t;          // [C][capsum]
-    uint16_t* out_j;        // [C][capsum]
+    double* out_t;          // [C][mrg_stride]
+    uint16_t* out_j;        // [C][mrg_stride]
     int* out_len;           // [C]
+    int64_t mrg_stride;     // capacity per replica: past it the replica is flagged RQ_ST_STREAM_OVERFLOW
     int32_t* status;        // RQ_ST_TIE when > RQ_MG_CAP arrivals share one time
     unsigned long long* clk;   // RQ_PHASE_CLOCK builds only: per-phase s_memtime sums [8]
 };

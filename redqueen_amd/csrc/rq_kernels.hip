@@ -255,8 +255,8 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
         for (int q = 0; q < SPL; ++q) load_win(q);
     }
     // MRG: the replica's merged sequence; lane l holds entry mpos + l of the next tile
-    const double* mt = MRG ? a.mrg_t + rl * a.capsum : nullptr;
-    const uint16_t* mj = MRG ? a.mrg_j + rl * a.capsum : nullptr;
+    const double* mt = MRG ? a.mrg_t + rl * a.mrg_stride : nullptr;
+    const uint16_t* mj = MRG ? a.mrg_j + rl * a.mrg_stride : nullptr;
     const int mlen = MRG ? a.mrg_len[rl] : 0;
     int mpos = 0;
     double nxt_t = RQ_INF;

@@ -163,8 +163,8 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
     }
     double span = (a.end - t_lo) * ((double)MG_TARGET / (double)(total > 1 ? total : 1));
     int64_t outpos = 0;
-    double* out_t = a.out_t + rl * a.capsum;
-    uint16_t* out_j = a.out_j + rl * a.capsum;
+    double* out_t = a.out_t + rl * a.mrg_stride;
+    uint16_t* out_j = a.out_j + rl * a.mrg_stride;
     int status = 0;
     __syncthreads();   // wmin / wsum read before the first round rewrites them
 #ifdef RQ_PHASE_CLOCK
@@ -310,6 +310,10 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
             // of equal times is a time prefix) and flag the replica
             nr = MG_CAP;
             status |= RQ_ST_TIE;
+        }
+        if (outpos + (int64_t)nr > a.mrg_stride) {   // past the merged capacity (uniform)
+            status |= RQ_ST_STREAM_OVERFLOW;
+            break;
         }
         double t_next = wmin[0];
 #pragma unroll

@@ -116,8 +116,8 @@ __device__ __forceinline__ void sweep_fw_body(SweepArgs a)
     else gen.none();
     int pos = 0, fil = 0;   // arrivals consumed / generated by this lane's source
     // MRG: the replica's merged sequence; lane l holds entry mpos + l of the next tile
-    const double* mt = MRG ? a.mrg_t + rl * a.capsum : nullptr;
-    const uint16_t* mj = MRG ? a.mrg_j + rl * a.capsum : nullptr;
+    const double* mt = MRG ? a.mrg_t + rl * a.mrg_stride : nullptr;
+    const uint16_t* mj = MRG ? a.mrg_j + rl * a.mrg_stride : nullptr;
     const int mlen = MRG ? a.mrg_len[rl] : 0;
     int mpos = 0;
     double nxt_t = RQ_INF;

@@ -61,11 +61,14 @@ class Graph:
             cls = _source_class(name)
             if cls is not None and getattr(cls, "_rq_kind", None) is None:
                 # graph-level times: the instance its own kwargs make (the seed as given);
-                # randomized batches replace them per replica (run(randomize=True))
-                from .opt_model import plugin_times
-                self.plugins.append((idx, cls, dict(kw), int(kw["src_id"])))
+                # randomized batches replace them per replica (run(randomize=True)).  A
+                # dynamic plugin must be self-driven: every run checks it (_verify_dynamic)
+                from .opt_model import source_times
+                inst = cls(**kw)
+                dyn = bool(getattr(inst, "is_dynamic", True))
+                self.plugins.append((idx, cls, dict(kw), int(kw["src_id"]), dyn))
                 kw = {"src_id": kw["src_id"],
-                      "times": plugin_times(cls(**kw), float(start_time), sink_ids, edge_list,
+                      "times": source_times(inst, float(start_time), sink_ids, edge_list,
                                             float(end_time))}
             self.has_realdata = self.has_realdata or kind == L.SRC_REALDATA
             if kind == L.SRC_OPT:
@@ -159,10 +162,15 @@ class Graph:
     def run(self, *args, stream=None, **kw):
         """Enqueue one batch on ``stream`` (default: the current torch stream).  Every
         tensor the batch reads or writes is allocated with that stream current, so
-        the caching allocator, the library and the status check all agree on it."""
+        the caching allocator, the library and the status check all agree on it.
+        With a dynamic plugin among the sources, the batch's first replica is checked to
+        be self-driven (_verify_dynamic) before the result is returned."""
         use = stream or torch.cuda.current_stream()
         with torch.cuda.stream(use):
-            return self._run(*args, stream=use, **kw)
+            res = self._run(*args, stream=use, **kw)
+            if any(p[4] for p in self.plugins) and not kw.get("plan_only"):
+                self._verify_dynamic(args, dict(kw, stream=use), res)
+            return res
 
     def _run(self, ctrl="opt", q=1.0, s=None, n_rep=1, ctrl_seed=0, world_seed=0,
             randomize=False, seed_mod=0, ctrl_rate=None, Ks=(1,), max_events=None,
@@ -317,7 +325,6 @@ class Graph:
         batch: replica i's instance gets seed u_i + 99 idx (randomize_other_sources,
         opt_model.py:795-804) and the host runs its initialize() / get_all_times();
         the times reach the kernels as per-replica RealData streams (rq_batch_desc.rd_*)."""
-        from .opt_model import plugin_times
         wseed = world_seed.to(torch.int64).cpu().numpy() if torch.is_tensor(world_seed) else None
         nrd = len(self.plugins)
         if nrd > L.MAX_RD:
@@ -326,11 +333,8 @@ class Graph:
         chunks = []
         for i in gids:   # increasing: rd_off is a prefix over the global ids
             i = int(i)
-            k = i % seed_mod if seed_mod > 0 else i
-            u = int(wseed[i]) if wseed is not None else int(world_seed) + k
-            for c, (idx, cls, kw, _sid) in enumerate(self.plugins):
-                t = plugin_times(cls(**dict(kw, seed=(u + 99 * idx) & 0xFFFFFFFF)), self.start_time,
-                                 self.sink_ids, self._edges, self.end_time)
+            for c, inst in enumerate(self._plugin_instances(i, wseed, world_seed, seed_mod)):
+                t = self._plugin_source_times(inst)
                 counts[i, c] = t.size
                 chunks.append(t)
         off = np.concatenate([[0], np.cumsum(counts.ravel())]).astype(np.int64)
@@ -345,6 +349,48 @@ class Graph:
         b.rd_cap = cap.ctypes.data_as(L._pi64)
         b.rd_times = td.data_ptr()
         b.rd_off = to.data_ptr()
+
+    def _plugin_instances(self, i, wseed, world_seed, seed_mod):
+        """Fresh instances of the registered plugins for global replica i of a
+        randomized batch: seed u_i + 99 idx (randomize_other_sources, opt_model.py:795-804)."""
+        k = i % seed_mod if seed_mod > 0 else i
+        u = int(wseed[i]) if wseed is not None else int(world_seed) + k
+        return [cls(**dict(kw, seed=(u + 99 * idx) & 0xFFFFFFFF))
+                for idx, cls, kw, _sid, _dyn in self.plugins]
+
+    def _plugin_source_times(self, inst):
+        from .opt_model import source_times
+        return source_times(inst, self.start_time, self.sink_ids, self._edges, self.end_time)
+
+    def _verify_dynamic(self, args, kw, res):
+        """A dynamic plugin is played from its own schedule: check that it is self-driven
+        on the batch's first replica -- rerun that replica with its event log and feed a
+        fresh copy of each dynamic plugin the whole event sequence in play order
+        (opt_model.verify_dynamic_plugin), which raises when its schedule reacts to
+        another source's event."""
+        from .opt_model import verify_dynamic_plugin
+        gids = res.global_ids
+        if not len(gids):
+            return
+        kw = dict(kw)
+        kw.update(replica0=int(kw.get("replica0", 0)), n_local=1, event_log=True, check=True)
+        probe = self._run(*args, **kw)
+        t_ev, s_ev = probe.events(0)
+        i = int(gids[0])
+        if kw.get("randomize"):
+            ws = kw.get("world_seed", 0)
+            wseed = ws.to(torch.int64).cpu().numpy() if torch.is_tensor(ws) else None
+            make = lambda: self._plugin_instances(i, wseed, ws, int(kw.get("seed_mod", 0)))  # noqa: E731
+        else:
+            make = lambda: [cls(**kw_) for _idx, cls, kw_, _sid, _dyn in self.plugins]  # noqa: E731
+        for fresh, gen, p in zip(make(), make(), self.plugins):
+            if not p[4]:
+                continue
+            times = self._plugin_source_times(gen)
+            me = kw.get("max_events")
+            verify_dynamic_plugin(fresh, self.start_time, self.sink_ids, self._edges, self.end_time,
+                                  t_ev, s_ev, times,
+                                  max_events=None if me is None or me == float("inf") else int(me))
 
     def _plan_variant(self, lib, b):
         info = (C.c_int64 * 8)()

@@ -126,8 +126,14 @@ class Broadcaster:
     ``init_state(start_time, all_sink_ids, follower_sink_ids, end_time)``.  The host
     calls them (once per run, or once per replica of a randomized batch) and the
     times play as RealData-kind streams on the GPU.  A DYNAMIC plugin
-    (``get_next_interval`` queried on every event) has no kernel: running one
-    raises NotImplementedError (RQ_EUNSUPPORTED)."""
+    (``get_next_interval`` queried on every event, opt_model.py:351-369) runs when it
+    is SELF-DRIVEN -- its schedule moves only on its own events, as Poisson's and
+    Hawkes' do: the host plays its own events through ``get_next_event_time`` to get
+    its times (dynamic_plugin_times), the GPU plays them, and every run then feeds a
+    fresh copy of the plugin the run's whole event sequence, in play order, as
+    run_dynamic would (verify_dynamic_plugin): a plugin whose schedule reacts to
+    another source's event (the reference's SmartPoisson, say) raises
+    NotImplementedError (RQ_EUNSUPPORTED) instead of returning a different run."""
     _rq_kind = None
 
     def __init__(self, src_id, seed):
@@ -153,11 +159,123 @@ class Broadcaster:
         assert not self.is_dynamic
         raise NotImplementedError()
 
+    def get_next_event_time(self, event):
+        """opt_model.py:351-369: the delay to this source's next event after `event`
+        (None: the start); the host calls it only for dynamic plugins."""
+        cur_time = self.get_current_time(event)
+        self.used = True
+        if event is None or event.src_id == self.src_id:
+            self.last_self_event_time = cur_time
+        t_delta = self.get_next_interval(event)
+        if t_delta is not None:
+            self.t_delta = t_delta
+        ret_t_delta = self.last_self_event_time + self.t_delta - cur_time
+        if ret_t_delta < 0:
+            logging.warning('src_id: {}, event_id: {}, returned t_delta = {} < 0, set to 0 instead.'
+                            .format(self.src_id, event.event_id, ret_t_delta))
+            ret_t_delta = 0.0
+        return ret_t_delta
+
+    def get_current_time(self, event):
+        return event.cur_time if event is not None else self.start_time
+
     def get_next_interval(self, event):  # pragma: no cover - engine-side
         raise NotImplementedError("arrival processes run in librq.so (gfx950)")
 
     def _kwargs(self):
         return {"src_id": self.src_id, "seed": self.seed}
+
+
+def _schedule(obj):
+    """The absolute time of a dynamic source's next event: last_self_event_time +
+    t_delta (Broadcaster.get_next_event_time, opt_model.py:351-369)."""
+    if obj.t_delta is None:
+        raise TypeError("unsupported operand type(s) for +: 'float' and 'NoneType' "
+                        "(broadcaster %s returned no first interval)" % type(obj).__name__)
+    return obj.last_self_event_time + obj.t_delta
+
+
+DYNAMIC_PLUGIN_MAX_EVENTS = 10 ** 7
+
+
+def dynamic_plugin_times(obj, start_time, sink_ids, edge_list, end_time):
+    """Own event times of a SELF-DRIVEN dynamic plugin instance (see Broadcaster): the
+    first call get_next_event_time(None) at start_time, then one call per own event,
+    as run_dynamic makes them (opt_model.py:251-311); an event's time is the schedule
+    last_self_event_time + t_delta (the engine plays every source's own times).  The
+    events handed over carry the plugin's own src_id, cur_time and sink list; their
+    event_id and time_delta are unknown here (-1, NaN) -- a plugin that reads them is
+    not self-driven and fails the run's verification."""
+    followers = [e[1] for e in edge_list if e[0] == obj.src_id]
+    obj.init_state(start_time, list(sink_ids), followers, end_time)
+    obj.get_next_event_time(None)
+    t = []
+    nxt = _schedule(obj)
+    while nxt <= end_time:
+        if nxt < (t[-1] if t else start_time):
+            # run_dynamic clamps a negative delay to 0 relative to the LAST event of any
+            # source (opt_model.py:364-367): that depends on the other sources
+            raise NotImplementedError("broadcaster %s (src_id %r) scheduled an event before its "
+                                      "previous one: not supported by the GPU engine"
+                                      % (type(obj).__name__, obj.src_id))
+        if len(t) >= DYNAMIC_PLUGIN_MAX_EVENTS:
+            raise ValueError("broadcaster %s (src_id %r) posted more than %d events"
+                             % (type(obj).__name__, obj.src_id, DYNAMIC_PLUGIN_MAX_EVENTS))
+        t.append(nxt)
+        obj.get_next_event_time(Event(-1, float("nan"), nxt, obj.src_id, followers))
+        nxt = _schedule(obj)
+    return np.asarray(t, dtype=np.float64)
+
+
+def verify_dynamic_plugin(fresh, start_time, sink_ids, edge_list, end_time, ev_t, ev_src,
+                          times, max_events=None):
+    """Feed a fresh copy of a dynamic plugin every event of a run in play order
+    (ev_t / ev_src: the engine's event log), as run_dynamic does (opt_model.py:271-311:
+    get_next_event_time(last_event) for every event, event ids from 100, time_delta on
+    the accumulated State.time); its schedule must put each of its own events where the
+    engine played them (`times`).  Raises NotImplementedError otherwise: the plugin's
+    schedule depends on other sources' events, which the engine cannot play."""
+    sinks = {}
+    for a_, b_ in edge_list:
+        sinks.setdefault(a_, []).append(b_)
+    fresh.init_state(start_time, list(sink_ids), sinks.get(fresh.src_id, []), end_time)
+    fresh.get_next_event_time(None)
+    own = iter(np.asarray(times, dtype=np.float64))
+    state_time = start_time
+    n = len(ev_t)
+    bad = None
+    for k in range(n):
+        t, src = float(ev_t[k]), int(ev_src[k])
+        if src == fresh.src_id:
+            want = next(own, None)
+            sched = _schedule(fresh)
+            if want is None or sched != want or t != want:
+                bad = (k, t, sched)
+                break
+        ev = Event(100 + k, t - state_time, t, src, list(sinks.get(src, [])))
+        state_time += ev.time_delta
+        if max_events is not None and k + 1 >= max_events:
+            break   # run_dynamic stops before it hands the last event over
+        fresh.get_next_event_time(ev)
+    else:
+        if max_events is None or n < max_events:
+            sched = _schedule(fresh)
+            if next(own, None) is not None or sched <= end_time:
+                bad = (n, None, sched)
+    if bad is not None:
+        raise NotImplementedError(
+            "dynamic broadcaster %s (src_id %r) is not self-driven: its schedule reacts to "
+            "other sources' events (at event %d: played %r, its schedule %r); the GPU engine "
+            "plays dynamic plugins whose schedule moves only on their own events "
+            "(RQ_EUNSUPPORTED)" % (type(fresh).__name__, fresh.src_id, bad[0], bad[1], bad[2]))
+
+
+def source_times(obj, start_time, sink_ids, edge_list, end_time):
+    """Times of a registered plugin instance: static (plugin_times) or self-driven
+    dynamic (dynamic_plugin_times)."""
+    if getattr(obj, "is_dynamic", True):
+        return dynamic_plugin_times(obj, start_time, sink_ids, edge_list, end_time)
+    return plugin_times(obj, start_time, sink_ids, edge_list, end_time)
 
 
 def plugin_times(obj, start_time, sink_ids, edge_list, end_time):
@@ -167,8 +285,8 @@ def plugin_times(obj, start_time, sink_ids, edge_list, end_time):
     raises ValueError (the reference would play it with a negative time_delta)."""
     if getattr(obj, "is_dynamic", True):
         raise NotImplementedError(
-            "broadcaster %s is dynamic (get_next_interval per event): only static plugin "
-            "broadcasters run on the GPU engine (RQ_EUNSUPPORTED)" % type(obj).__name__)
+            "broadcaster %s is dynamic (get_next_interval per event): use source_times "
+            "(self-driven dynamic plugins)" % type(obj).__name__)
     followers = [e[1] for e in edge_list if e[0] == obj.src_id]
     obj.init_state(start_time, list(sink_ids), followers, end_time)
     obj.initialize()
@@ -392,12 +510,20 @@ class Manager:
             ctrl_id = min(ids) - 1
         else:
             ctrl_id = ctrl.src_id
-        # registered plugin broadcasters: their own initialize() / get_all_times()
-        other_desc = [(type(s).__name__, s._kwargs()) if s._rq_kind is not None else
-                      ("RealData", {"src_id": s.src_id,
-                                    "times": plugin_times(s, self.start_time, self.sink_ids,
-                                                          self.edge_list, self.end_time)})
-                      for s in others]
+        # registered plugin broadcasters: their own initialize() / get_all_times(), or a
+        # self-driven dynamic plugin's own schedule (verified against the run below)
+        import copy
+        probes = []
+        other_desc = []
+        for s in others:
+            if s._rq_kind is not None:
+                other_desc.append((type(s).__name__, s._kwargs()))
+                continue
+            fresh = copy.deepcopy(s) if getattr(s, "is_dynamic", True) else None
+            t = source_times(s, self.start_time, self.sink_ids, self.edge_list, self.end_time)
+            other_desc.append(("RealData", {"src_id": s.src_id, "times": t}))
+            if fresh is not None:
+                probes.append((fresh, t))
         if isinstance(ctrl, (Opt, OptPWSignificance)):
             fl = [e[1] for e in self.edge_list if e[0] == ctrl.src_id]
             if len(set(fl)) != len(fl):
@@ -438,6 +564,9 @@ class Manager:
         for s in self.sources:
             s.used = True
         t, src = res.events(0)
+        for fresh, times in probes:
+            verify_dynamic_plugin(fresh, self.start_time, self.sink_ids, self.edge_list,
+                                  self.end_time, t, src, times, max_events=maxev)
         self.state._set_log(t, src, self.edge_list, res)
         self.result = res
         return self

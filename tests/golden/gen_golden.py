@@ -33,6 +33,8 @@ installed and there is no network) and records, as plain data:
                    df (deterministic), its metrics and final State.time
   plugin.npz       a registered static broadcaster (registerSource): df + metrics of the
                    seeded world and of randomize_other_sources(u), u = 0..15
+  dynplugin.npz    a registered DYNAMIC self-driven broadcaster (Renewal) beside a static
+                   one: df + metrics of the seeded world and of randomize_other_sources(u)
   errors.npz       reference behaviour on a scalar-s u_int_opt and on OptPWSignificance
                    events that reach no follower with positive significance
   sig_runs.npz     OptPWSignificance runs (notebook "Testing out significance",
@@ -548,6 +550,51 @@ def gen_plugin():
     np.savez_compressed(os.path.join(HERE, "plugin.npz"), **rec)
 
 
+def gen_dynplugin():
+    """A registered DYNAMIC, self-driven broadcaster (Renewal: gamma gaps on its own
+    events, None on the others') beside a static one, in a deterministic world (RealData
+    controlled): the df of the given seeds, the metrics of randomize_other_sources(u) for
+    u in 0..15; and the reference running a reactive dynamic plugin (KnockedOff) to the
+    end (the engine refuses that one)."""
+    from realdata_worlds import BurstyMixin, KnockedOffMixin, RenewalMixin, dyn_plugin_world
+    from redqueen.opt_model import Broadcaster
+
+    class Bursty(BurstyMixin, Broadcaster):
+        pass
+
+    class Renewal(RenewalMixin, Broadcaster):
+        pass
+
+    class KnockedOff(KnockedOffMixin, Broadcaster):
+        pass
+    SimOpts.registerSource("Bursty", Bursty)
+    SimOpts.registerSource("Renewal", Renewal)
+    SimOpts.registerSource("KnockedOff", KnockedOff)
+    w, ctrl, us = dyn_plugin_world()
+    so = SimOpts(**w)
+    rec = {}
+    m = so.create_manager_with_times(np.asarray(ctrl))
+    m.run_dynamic()
+    df = m.state.get_dataframe()
+    _df_cols(rec, "base", df)
+    met, own, world = metrics(df, so)
+    rec["base_met"], rec["base_cnt"] = met, np.asarray([own, world, len(df)])
+    mets, cnts = [], []
+    for u in us:
+        m = so.randomize_other_sources(u).create_manager_with_times(np.asarray(ctrl))
+        m.run_dynamic()
+        df = m.state.get_dataframe()
+        met, own, world = metrics(df, so)
+        mets.append(met)
+        cnts.append([own, world, m.state.get_num_events()])
+    rec["rand_met"], rec["rand_cnt"], rec["rand_u"] = np.asarray(mets), np.asarray(cnts), np.asarray(us)
+    w2 = dict(w, other_sources=[("KnockedOff", {"src_id": 2, "seed": 21, "rate": 1.0})] + w["other_sources"][1:])
+    m = SimOpts(**w2).create_manager_with_times(np.asarray(ctrl))
+    m.run_dynamic()
+    rec["knocked_events"] = np.asarray([m.state.get_num_events()])
+    np.savez_compressed(os.path.join(HERE, "dynplugin.npz"), **rec)
+
+
 def gen_sig():
     """OptPWSignificance (opt_model.py:547-623) via create_manager_with_significance
     (:850-884): the notebook cells opt_broadcast.ipynb:5469 and :5569 plus variants."""
@@ -824,7 +871,7 @@ if __name__ == "__main__":
     steps = {"npsum": gen_npsum, "draws": gen_draws, "readme": gen_readme, "kats": gen_kats,
              "adv": gen_adversarial, "graphs": gen_graphs, "frac": gen_frac,
              "oracle": gen_oracle, "sweepq": gen_sweepq, "sig": gen_sig, "realdata": gen_realdata,
-             "plugin": gen_plugin, "errors": gen_errors}
+             "plugin": gen_plugin, "errors": gen_errors, "dynplugin": gen_dynplugin}
     if a.c4_dist:
         gen_c4_dist(a.c4_dist, a.c4_start, a.procs)
         print("done c4 dist", flush=True)

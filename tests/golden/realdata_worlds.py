@@ -95,3 +95,54 @@ def plugin_world():
                         (4, 6)])
     ctrl = [0.0, 1.5, 4.0, 9.25, 12.0, 20.0, 27.5]
     return w, ctrl, list(range(16))
+
+
+class RenewalMixin:
+    """A DYNAMIC plugin broadcaster (get_next_interval queried on every event,
+    opt_model.py:351-369) that is self-driven: on its own events (and at the start) it
+    draws a gamma(2, scale) gap through self.random_state; on every other source's event
+    it returns None (the schedule stays)."""
+
+    def __init__(self, src_id, seed, scale=0.6):
+        super().__init__(src_id, seed)
+        self.scale = scale
+
+    def get_next_interval(self, event):
+        if event is None or event.src_id == self.src_id:
+            return self.random_state.gamma(2.0, self.scale)
+        return None
+
+
+class KnockedOffMixin:
+    """A DYNAMIC plugin whose schedule reacts to other sources' events (the reference's
+    SmartPoisson idea, opt_model.py:436-455): after its own post it waits; when another
+    source's event knocks it off its followers' top it schedules a post Exp(rate) later."""
+
+    def __init__(self, src_id, seed, rate=1.0):
+        super().__init__(src_id, seed)
+        self.rate = rate
+        self.on_top = False
+
+    def get_next_interval(self, event):
+        if event is None:
+            return self.random_state.exponential(scale=1.0 / self.rate)
+        if event.src_id == self.src_id:
+            self.on_top = True
+            return float("inf")
+        if self.on_top and set(event.sink_ids) & set(self.sink_ids):
+            self.on_top = False
+            return (self.get_current_time(event) - self.last_self_event_time +
+                    self.random_state.exponential(scale=1.0 / self.rate))
+        return None
+
+
+def dyn_plugin_world():
+    """A self-driven dynamic plugin (Renewal, src 2) + a static one (Bursty, src 6) + a
+    RealData controlled source: deterministic for given seeds."""
+    w = dict(src_id=4, end_time=30.0, s=1.0, q=1.0, sink_ids=[1, 2, 3, 4, 5, 6],
+             other_sources=[("Renewal", {"src_id": 2, "seed": 21, "scale": 0.6}),
+                            ("Bursty", {"src_id": 6, "seed": 12, "rate": 0.2, "size": 4})],
+             edge_list=[(2, 1), (2, 2), (2, 5), (6, 2), (6, 3), (6, 6), (4, 1), (4, 3), (4, 4),
+                        (4, 6)])
+    ctrl = [0.0, 1.5, 4.0, 9.25, 12.0, 20.0, 27.5]
+    return w, ctrl, list(range(16))

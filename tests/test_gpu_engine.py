@@ -357,3 +357,26 @@ def test_work_queue_c3():
         u = 77 + r
         met_o, t_o, s_o = _oracle(O, _world_with_seeds(so, u), ("opt", u), (1,))
         _cmp_replica(a, r, met_o, t_o, s_o, (1,))
+
+
+@pytest.mark.parametrize("wl", ["c3", "g120"])
+def test_capacity_overflow_rerun(wl, monkeypatch):
+    """The merged sequence and the pivot rows are sized from the SUM of a replica's wall
+    events (mean + 8 sigma); a replica past them is flagged (RQ_ST_STREAM_OVERFLOW /
+    RQ_ST_ROWS_OVERFLOW) and Graph.run(check=True) reruns the batch with doubled
+    capacities.  Forced here by undersized capacities (RQ_CAP_SQUEEZE): the flagged first
+    pass leaves no trace -- the result equals the normal run bit for bit, and the oracle."""
+    torch, engine, graphs, O = _ctx()
+    from redqueen_amd import _lib as L
+    so = getattr(graphs, wl)()
+    g = _graph(engine, so)
+    kw = dict(q=so["q"], s=so["s"], n_rep=64, ctrl_seed=9, world_seed=9, randomize=True, Ks=(1,))
+    ref = g.run("opt", **kw)
+    monkeypatch.setenv("RQ_CAP_SQUEEZE", "0.45")
+    raw = g.run("opt", check=False, **kw)
+    assert int(((raw.status & (L.ST_ROWS_OVERFLOW | L.ST_STREAM_OVERFLOW)) != 0).sum().item()) > 0
+    got = g.run("opt", **kw)
+    assert int(got.status.max().item()) == 0
+    assert torch.equal(got.metrics, ref.metrics) and torch.equal(got.counts, ref.counts)
+    met_o, t_o, s_o = _oracle(O, _world_with_seeds(so, 9 + 5), ("opt", 9 + 5), (1,))
+    _cmp_replica(got, 5, met_o, t_o, s_o, (1,))

@@ -138,17 +138,22 @@ def test_merged_tie_group_beyond_round_capacity():
 
 
 @pytest.mark.parametrize("wl", ["c3", "g120"])
-def test_pipelined_chunks_and_longest_first_order(wl):
+def test_pipelined_chunks_and_longest_first_order(wl, monkeypatch):
     """rq_run_batch's chunk plans change no result bit: one chunk larger than the resident
-    sweep slots (the work queue hands out replicas in the longest-first order of
-    rq_order_replicas), the default two pipelined chunks, and many small chunks on two
-    streams (fork / join events) give identical per-replica outputs."""
+    sweep slots in index order and in the longest-first order of rq_order_replicas
+    (RQ_ORDER=1: the work queue hands the replicas out by length), the default two
+    pipelined chunks, and many small chunks on two streams (fork / join events) give
+    identical per-replica outputs."""
     torch, engine, graphs, O = _ctx()
     so = getattr(graphs, wl)()
     g = _graph(engine, so)
     R = 9000 if wl == "c3" else 12000
     kw = dict(q=so["q"], s=so["s"], n_rep=R, ctrl_seed=77, world_seed=77, randomize=True, Ks=(1,))
+    idx = g.run("opt", chunk=R, **kw)
+    monkeypatch.setenv("RQ_ORDER", "1")
     one = g.run("opt", chunk=R, **kw)
+    monkeypatch.delenv("RQ_ORDER")
+    _same(torch, one, idx)
     assert g.run("opt", chunk=R, plan_only=True, **kw)["chunk"] == R
     dflt = g.run("opt", **kw)
     small = g.run("opt", chunk=700, **kw)

@@ -5,7 +5,10 @@ per run, or once per replica with the seeds randomize_other_sources gives it,
 :795-804) and the engine plays the times as RealData streams -- per-replica ones
 through rq_batch_desc.rd_* (ABI v3).  Expected values: tests/golden/plugin.npz,
 written by gen_golden.py with the same class over the reference's Broadcaster.
-A dynamic plugin has no kernel and raises NotImplementedError (RQ_EUNSUPPORTED)."""
+A DYNAMIC plugin runs when it is self-driven (its schedule moves only on its own
+events): its own times come from its get_next_event_time on the host and every run
+verifies it against the run's event sequence; a reactive one raises
+NotImplementedError (RQ_EUNSUPPORTED).  Expected values: tests/golden/dynplugin.npz."""
 import os
 import sys
 
@@ -66,22 +69,77 @@ def test_registered_static_broadcaster_randomized_batch(golden):
     assert np.array_equal(r2.metrics.cpu().numpy(), d["rand_met"][5:12])
 
 
-def test_dynamic_plugin_is_unsupported():
-    engine, SimOpts, Bursty, (w, ctrl, us) = _setup()
-    from redqueen_amd.opt_model import Broadcaster
+def _dyn_setup():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from realdata_worlds import BurstyMixin, KnockedOffMixin, RenewalMixin, dyn_plugin_world
+    from redqueen_amd import engine
+    from redqueen_amd.opt_model import Broadcaster, SimOpts
 
-    class Chatty(Broadcaster):
-        def __init__(self, src_id, seed):
-            super().__init__(src_id, seed)
+    class Bursty(BurstyMixin, Broadcaster):
+        pass
 
-        def get_next_interval(self, event):
-            return 1.0
-    SimOpts.registerSource("Chatty", Chatty)
-    w2 = dict(w, other_sources=[("Chatty", {"src_id": 2, "seed": 1})],
-              edge_list=[e for e in w["edge_list"] if e[0] != 6])
+    class Renewal(RenewalMixin, Broadcaster):
+        pass
+
+    class KnockedOff(KnockedOffMixin, Broadcaster):
+        pass
+    SimOpts.registerSource("Bursty", Bursty)
+    SimOpts.registerSource("Renewal", Renewal)
+    SimOpts.registerSource("KnockedOff", KnockedOff)
+    return engine, SimOpts, dyn_plugin_world()
+
+
+def test_self_driven_dynamic_plugin_single_run(golden):
+    """A registered DYNAMIC broadcaster whose schedule moves only on its own events
+    (Renewal: gamma gaps through its own RandomState, None on the others'): the host
+    plays its own events through get_next_event_time, the GPU plays the times, and the
+    run's whole event sequence is fed back to a fresh copy of it to verify it is
+    self-driven.  The df equals the reference's run_dynamic df bit for bit."""
+    engine, SimOpts, (w, ctrl, us) = _dyn_setup()
+    from redqueen_amd import utils as U
+    d = golden("dynplugin.npz")
+    so = SimOpts(**w)
+    m = so.create_manager_with_times(np.asarray(ctrl))
+    m.run_dynamic()
+    df = m.state.get_dataframe()
+    for c in COLS:
+        assert np.array_equal(df[c].values, d["base_" + c]), c
+    got = U.replay_metrics(df, so.src_id, so.end_time, KS)
+    assert np.array_equal(np.asarray(got["top_k"] + [got["avg_rank"], got["r_2"]]), d["base_met"])
+
+
+def test_self_driven_dynamic_plugin_randomized_batch(golden):
+    """16 replicas in one batch with randomize_other_sources seeds: every replica's
+    metrics and counts equal the reference's run (the batch's first replica is checked
+    to be self-driven through its own event log)."""
+    engine, SimOpts, (w, ctrl, us) = _dyn_setup()
+    d = golden("dynplugin.npz")
+    g = engine.Graph(w["src_id"], w["other_sources"], w["sink_ids"], w["edge_list"],
+                     w["end_time"], ctrl_a=ctrl)
+    assert [(p[3], p[4]) for p in g.plugins] == [(2, True), (6, False)]
+    res = g.run("times", n_rep=len(us), world_seed=0, randomize=True, Ks=KS)
+    m = res.metrics.cpu().numpy()
+    c = res.counts.cpu().numpy()
+    assert np.array_equal(m, d["rand_met"]), m - d["rand_met"]
+    assert np.array_equal(c[:, :3], d["rand_cnt"])
+
+
+def test_reactive_dynamic_plugin_refused(golden):
+    """A dynamic plugin whose schedule reacts to other sources' events (KnockedOff, the
+    reference's SmartPoisson idea): the reference runs it (dynplugin.npz knocked_events),
+    the engine cannot play it and raises NotImplementedError (RQ_EUNSUPPORTED) -- for a
+    manager and for a batch -- instead of returning a different run."""
+    engine, SimOpts, (w, ctrl, us) = _dyn_setup()
+    d = golden("dynplugin.npz")
+    assert int(d["knocked_events"][0]) > 0
+    w2 = dict(w, other_sources=[("KnockedOff", {"src_id": 2, "seed": 21, "rate": 1.0})] +
+              w["other_sources"][1:])
     so = SimOpts(**w2)
     with pytest.raises(NotImplementedError):
         so.create_manager_with_times(np.asarray(ctrl)).run_dynamic()
+    g = engine.Graph(w2["src_id"], w2["other_sources"], w2["sink_ids"], w2["edge_list"],
+                     w2["end_time"], ctrl_a=ctrl)
     with pytest.raises(NotImplementedError):
-        engine.Graph(w2["src_id"], w2["other_sources"], w2["sink_ids"], w2["edge_list"],
-                     w2["end_time"])
+        g.run("times", n_rep=4, world_seed=0, randomize=True, Ks=KS)
