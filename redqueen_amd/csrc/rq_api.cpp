@@ -191,6 +191,9 @@ struct Plan {
     bool mrg = false;
     size_t off_mt = 0, off_mj = 0, off_mlen = 0;
     int64_t mrg_stride = 0;   // merged entries per replica (capacity)
+    int n_grp = 1;            // > RQ_MG_B sources: groups of the two-level merge
+    int64_t sub_stride = 0;   //   entries per (replica, group) of the first level
+    size_t off_sub_t = 0, off_sub_j = 0, off_sub_len = 0;
     // the fused sweep's phases B / C on merged streams (rq_gen_streams + rq_merge_streams
     // instead of in-kernel generation; sweep_mode 7: the in-kernel generating sweep)
     bool fwm = false;
@@ -356,7 +359,7 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     // vectors (sqrt_s_by_q, old_ranks: one entry per edge) no longer match the ranks (one
     // per distinct follower) and its first non-own event raises ValueError
     if (g->ctrl_dup && (ck == RQ_SRC_OPT || ck == RQ_SRC_OPTPW)) return RQ_EINVAL;
-    if (g->n_str > RQ_MAX_STREAMS) return RQ_EUNSUPPORTED;
+    if (g->n_str > RQ_MAX_STREAMS_MRG) return RQ_EUNSUPPORTED;
     p->spl = g->n_str <= 64 ? 1 : g->n_str <= 128 ? 2 : g->n_str <= 256 ? 4 : 8;
     p->n_sinks_pad = (g->n_sinks + 1) | 1;   // odd stride: spreads replicas over LDS banks
     const size_t per_wave = (size_t)p->n_sinks_pad * 4;
@@ -371,11 +374,15 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
              b->sweep_mode == 2 || (has_rd && b->sweep_mode != 1 && b->sweep_mode != 5);
     for (int q = 0; q < b->nK; ++q) p->log = p->log || b->Ks[q] > 32767;   // int16 ranks
     // a multigraph (duplicate edges make fractional pivot cells, the exact sequential
-    // sweep's business) and > 512 sources (the fast instances own <= 8 per lane)
-    p->log = p->log || g->multi || g->n_str > 512;
+    // sweep's business); > 512 sources: the fast general sweep plays the two-level merged
+    // sequence (rq_merge_streams per group of 512, then over the groups), the windowed
+    // sweep (mode 6) owns <= 8 sources per lane
+    p->log = p->log || g->multi || (g->n_str > 512 && b->sweep_mode == 6);
     const int nwl = (g->n_sinks + 31) / 32;
 
   replan:
+    // the sequential sweep owns <= 32 sources per lane
+    if (p->log && g->n_str > RQ_MAX_STREAMS) return RQ_EUNSUPPORTED;
     if (p->log) p->spl = g->n_str <= 64 ? 1 : g->n_str <= 512 ? 8 : g->n_str <= 1024 ? 16 : 32;
     p->mstride = g->nw | 1;   // odd row stride: one LDS bank per stream for a given word
     p->bits = !p->log && p->nK == 1 && b->Ks[0] == 1 && g->nw > 0 && b->sweep_mode != 3 &&
@@ -392,7 +399,8 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     p->gs = false;
     // the fast general sweep plays the merged (t, stream) sequence: the merge kernel reads
     // every stream line once (one source per thread, <= RQ_MG_B sources)
-    p->mrg = !p->log && b->sweep_mode != 6 && g->n_str <= RQ_MG_B;
+    p->mrg = !p->log && b->sweep_mode != 6;
+    p->n_grp = g->n_str > RQ_MG_B ? (g->n_str + RQ_MG_B - 1) / RQ_MG_B : 1;
     if (const char* e = getenv("RQ_MRG")) p->mrg = p->mrg && atoi(e) != 0;   // A/B only
 
     // general sweep: pick (ring depth W, waves per block) for the most waves per CU
@@ -564,7 +572,8 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
             if (const char* e = getenv("RQ_WS_BUDGET_GB")) budget = atof(e) * (1 << 30);   // tuning only
             const double rows_b = (double)p->cap_rows * (20.0 + 4.0 * p->nK);
             const double per_rep = std::max(8.0 * (double)p->capsum, rows_b) + 4.0 * g->n_str +
-                                   10.0 * (double)p->mrg_stride + 16.0;
+                                   10.0 * (double)p->mrg_stride + 16.0 +
+                                   (p->n_grp > 1 ? 10.0 * (double)p->capsum + 512.0 * p->n_grp : 0.0);
             const int64_t fit = std::max<int64_t>(1, (int64_t)(budget / (p->nbuf * per_rep)));
             if (p->chunk > fit) {
                 nch = (p->R + fit - 1) / fit;
@@ -601,6 +610,18 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     const int64_t strm = p->fw && !p->fwm ? 0 : C;   // the generating fused sweep keeps its arrivals in LDS
     const size_t strm_bytes = sizeof(double) * (size_t)strm * p->capsum;
     p->off_slen = o;    o = align_up(o + sizeof(int) * (size_t)strm * g->n_str, A);
+    // two-level merge: per (replica, group) the first level's sequences
+    p->sub_stride = 0;
+    if (p->mrg && p->n_grp > 1)
+        for (int gq = 0; gq < p->n_grp; ++gq) {
+            int64_t c = 0;
+            for (int j = gq * RQ_MG_B; j < std::min(g->n_str, (gq + 1) * RQ_MG_B); ++j) c += p->cap[j];
+            p->sub_stride = std::max(p->sub_stride, (c + 15) & ~(int64_t)15);
+        }
+    const int64_t subc = p->sub_stride > 0 ? C * p->n_grp : 0;
+    p->off_sub_t = o;   o = align_up(o + sizeof(double) * (size_t)subc * p->sub_stride, A);
+    p->off_sub_j = o;   o = align_up(o + sizeof(uint16_t) * (size_t)subc * p->sub_stride, A);
+    p->off_sub_len = o; o = align_up(o + sizeof(int) * (size_t)subc, A);
     const int64_t mrgc = p->mrg ? C : 0;   // merged sequences: t f64, stream u16, length
     p->off_mt = o;      o = align_up(o + sizeof(double) * (size_t)mrgc * p->mrg_stride, A);
     p->off_mj = o;      o = align_up(o + sizeof(uint16_t) * (size_t)mrgc * p->mrg_stride, A);
@@ -1085,7 +1106,24 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             if (getenv("RQ_CLK_MERGE")) ma.clk = phase_clk();   // else the sweep's phases only
 #endif
             TimedLaunch tl(K_MERGE, s);
-            if (rq_launch_merge(ma, s) != hipSuccess) return RQ_EHIP;
+            if (p.n_grp > 1) {
+                // level 1: each group of RQ_MG_B streams into its own sequence
+                MergeArgs m1 = ma;
+                m1.out_t = (double*)(wsb + p.off_sub_t);
+                m1.out_j = (uint16_t*)(wsb + p.off_sub_j);
+                m1.out_len = (int*)(wsb + p.off_sub_len);
+                m1.mrg_stride = p.sub_stride;
+                if (rq_launch_merge_groups(m1, s) != hipSuccess) return RQ_EHIP;
+                // level 2: the groups' sequences into the replica's play order
+                ma.sub_t = m1.out_t;
+                ma.sub_j = m1.out_j;
+                ma.sub_len = m1.out_len;
+                ma.n_grp = p.n_grp;
+                ma.sub_stride = p.sub_stride;
+                if (rq_launch_merge_sub(ma, s) != hipSuccess) return RQ_EHIP;
+            } else if (rq_launch_merge(ma, s) != hipSuccess) {
+                return RQ_EHIP;
+            }
         }
 
         SweepArgs sa{};

@@ -144,6 +144,15 @@ struct MergeArgs {
     int* out_len;           // [C]
     int64_t mrg_stride;     // capacity per replica: past it the replica is flagged RQ_ST_STREAM_OVERFLOW
     int32_t* status;        // RQ_ST_TIE when > RQ_MG_CAP arrivals share one time
+    // two-level merge (> RQ_MG_B sources): the first level merges group g's streams
+    // [g RQ_MG_B, (g + 1) RQ_MG_B) of replica rl (grid y = group) into out_* at
+    // [(rl n_grp + g) mrg_stride]; the second level (sub-merge) takes those n_grp
+    // sequences -- sub_t / sub_j / sub_len, sub_stride entries each -- as its streams
+    const double* sub_t;
+    const uint16_t* sub_j;
+    const int* sub_len;
+    int n_grp;
+    int64_t sub_stride;
     unsigned long long* clk;   // RQ_PHASE_CLOCK builds only: per-phase s_memtime sums [8]
 };
 #define RQ_NPSUM1_LDS 516   // doubles of wave_npsum<1> scratch (== rq::npsum_lds_doubles<1>())
@@ -180,6 +189,11 @@ hipError_t rq_launch_scan(const ScanArgs& a, int nK, hipStream_t s);
 int rq_sweep_blocks_per_cu(int spl, int nK, int col16, int W, int log, int bits, int wpb, size_t lds);
 // spl = 0 in rq_launch_sweep / rq_sweep_blocks_per_cu: the fast sweep reading merged streams
 hipError_t rq_launch_merge(const MergeArgs& a, hipStream_t s);
+// > RQ_MG_B sources: level 1 over n_grp groups (a.n_str streams, grid C x n_grp), then
+// the second level over the groups' sequences (a.sub_*, a.n_grp "streams")
+hipError_t rq_launch_merge_groups(const MergeArgs& a, hipStream_t s);
+hipError_t rq_launch_merge_sub(const MergeArgs& a, hipStream_t s);
+#define RQ_MAX_STREAMS_MRG 65535   // merged entries carry the stream as u16
 // longest-first order of n <= 65536 replicas by len (descending; ties in any order)
 hipError_t rq_launch_order(const int* len, int64_t n, int* order, hipStream_t s);
 hipError_t rq_launch_sweep_fw(const SweepArgs& a, int nK, int col16, int W, int bits, hipStream_t s);

@@ -96,7 +96,18 @@ __device__ __forceinline__ int sub_of(double t, double t_lo, double scale)
 
 }  // namespace
 
-template <int MG_B>
+// the u16 stream of arrival k (0..15) of two 8-entry chunks of a sub-merge input
+__device__ __forceinline__ uint32_t selj16(uint4 c, uint4 nx, int k)
+{
+    const uint4 v = (k & 8) ? nx : c;
+    const uint32_t w0 = (k & 2) ? v.y : v.x, w1 = (k & 2) ? v.w : v.z;
+    const uint32_t w = (k & 4) ? w1 : w0;
+    return (k & 1) ? (w >> 16) : (w & 0xFFFFu);
+}
+
+// SUB: the second level of a two-level merge (> RQ_MG_B sources): thread g owns the
+// merged sequence of stream group g (its entries carry their own stream ids)
+template <int MG_B, bool SUB>
 __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
 {
     constexpr int MG_W = MgCfg<MG_B>::W, MG_CAP = MgCfg<MG_B>::CAP, MG_M = MgCfg<MG_B>::M;
@@ -114,10 +125,23 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int64_t rl = blockIdx.x;
-    const int j = tid;
+    // the first level of a two-level merge: block (rl, group) merges streams
+    // [group MG_B, group MG_B + MG_B); one level: gridDim.y == 1
+    const int grp = SUB ? 0 : (int)blockIdx.y, ngrp = SUB ? 1 : (int)gridDim.y;
+    const int j = (SUB ? 0 : grp * MG_B) + tid;
     int L = 0;
     const double* src = a.streams;
-    if (j < a.n_str) {
+    const uint16_t* srcj = nullptr;   // SUB: the entries' own stream ids
+    if constexpr (SUB) {
+        srcj = a.sub_j;
+        src = a.sub_t;
+        if (tid < a.n_grp) {
+            const int64_t q = rl * a.n_grp + tid;
+            L = a.sub_len[q];
+            src = a.sub_t + q * a.sub_stride;
+            srcj = a.sub_j + q * a.sub_stride;
+        }
+    } else if (j < a.n_str) {
         L = a.slen[(int64_t)j * a.slen_stride + rl];
         src = a.streams + rl * a.capsum + a.st_off[j];
     }
@@ -130,14 +154,20 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
     // start for an empty stream -- so they land straight in c / nx and are waited for
     // only where the values are used)
     Chunk c, nx;
+    uint4 cj = make_uint4(0, 0, 0, 0), nxj = make_uint4(0, 0, 0, 0);   // SUB: the chunks' stream ids
     int p = 0, p8 = 0;
     const int lastc = L > 0 ? (L - 1) & ~7 : 0;
 #define RQ_MG_CHUNK(q) load_chunk(src + ((q) < lastc ? (q) : lastc))
+#define RQ_MG_JCHUNK(q) (*reinterpret_cast<const uint4*>(srcj + ((q) < lastc ? (q) : lastc)))
 #define RQ_MG_RELOAD(p0)                 \
     do {                                 \
         p8 = (p0) & ~7;                  \
         c = RQ_MG_CHUNK(p8);             \
         nx = RQ_MG_CHUNK(p8 + 8);        \
+        if (SUB) {                       \
+            cj = RQ_MG_JCHUNK(p8);       \
+            nxj = RQ_MG_JCHUNK(p8 + 8);  \
+        }                                \
     } while (0)
 #define RQ_MG_HEAD() (p < L ? sel16(c, nx, p - p8) : RQ_INF)
     RQ_MG_RELOAD(0);
@@ -163,8 +193,8 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
     }
     double span = (a.end - t_lo) * ((double)MG_TARGET / (double)(total > 1 ? total : 1));
     int64_t outpos = 0;
-    double* out_t = a.out_t + rl * a.mrg_stride;
-    uint16_t* out_j = a.out_j + rl * a.mrg_stride;
+    double* out_t = a.out_t + (rl * ngrp + grp) * a.mrg_stride;
+    uint16_t* out_j = a.out_j + (rl * ngrp + grp) * a.mrg_stride;
     int status = 0;
     __syncthreads();   // wmin / wsum read before the first round rewrites them
 #ifdef RQ_PHASE_CLOCK
@@ -227,7 +257,7 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
                     const int sb = sub_of<MG_M>(cv[k], t_lo, scale);
                     const uint32_t slot = atomicAdd(&cnt[sb], 1u);
                     bt[idx] = cv[k];
-                    bj[idx] = (uint16_t)j;
+                    bj[idx] = (uint16_t)(SUB ? selj16(cj, nxj, k) : (uint32_t)j);
                     bs[idx] = ((uint32_t)sb << MG_SB) | slot;
                 }
             }
@@ -257,7 +287,7 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
                     const int sb = sub_of<MG_M>(head, t_lo, scale);
                     const uint32_t slot = atomicAdd(&cnt[sb], 1u);
                     bt[idx] = head;
-                    bj[idx] = (uint16_t)j;
+                    bj[idx] = (uint16_t)(SUB ? selj16(cj, nxj, p - p8) : (uint32_t)j);
                     bs[idx] = ((uint32_t)sb << MG_SB) | slot;
                     ++p;
                     if (p - p8 == 16 && p < L) RQ_MG_RELOAD(p);   // a burst: both chunks consumed
@@ -281,6 +311,10 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
                 nx = load_chunk_last(src + ((p8 + 8) < lastc ? (p8 + 8) : lastc));
             else
                 nx = RQ_MG_CHUNK(p8 + 8);
+            if (SUB) {
+                cj = nxj;
+                nxj = RQ_MG_JCHUNK(p8 + 8);
+            }
         }
         if constexpr (MG_W == 1) {
             if (lane == 0) nb = nb1;
@@ -391,7 +425,7 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
 #undef RQ_MG_RELOAD
 #undef RQ_MG_CHUNK
     if (tid == 0) {
-        a.out_len[rl] = (int)outpos;
+        a.out_len[rl * ngrp + grp] = (int)outpos;
         if (status) atomicOr(&a.status[a.chunk0 + rl], status);
     }
 }
@@ -401,9 +435,30 @@ hipError_t rq_launch_merge(const MergeArgs& a, hipStream_t s)
     if (a.n_chunk <= 0) return hipSuccess;
     if (a.n_str > RQ_MG_B) return hipErrorInvalidValue;
     if (a.n_str <= 64)
-        hipLaunchKernelGGL(rq_merge_streams<64>, dim3((unsigned)a.n_chunk), dim3(64), 0, s, a);
+        hipLaunchKernelGGL((rq_merge_streams<64, false>), dim3((unsigned)a.n_chunk), dim3(64), 0, s, a);
     else
-        hipLaunchKernelGGL(rq_merge_streams<RQ_MG_B>, dim3((unsigned)a.n_chunk), dim3(RQ_MG_B), 0, s, a);
+        hipLaunchKernelGGL((rq_merge_streams<RQ_MG_B, false>), dim3((unsigned)a.n_chunk), dim3(RQ_MG_B), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t rq_launch_merge_groups(const MergeArgs& a, hipStream_t s)
+{
+    if (a.n_chunk <= 0) return hipSuccess;
+    const int ng = (a.n_str + RQ_MG_B - 1) / RQ_MG_B;
+    if (ng < 2 || ng > RQ_MG_B || a.n_str > RQ_MAX_STREAMS_MRG) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((rq_merge_streams<RQ_MG_B, false>), dim3((unsigned)a.n_chunk, (unsigned)ng), dim3(RQ_MG_B), 0,
+                       s, a);
+    return hipGetLastError();
+}
+
+hipError_t rq_launch_merge_sub(const MergeArgs& a, hipStream_t s)
+{
+    if (a.n_chunk <= 0) return hipSuccess;
+    if (a.n_grp < 1 || a.n_grp > RQ_MG_B || !a.sub_t || !a.sub_j || !a.sub_len) return hipErrorInvalidValue;
+    if (a.n_grp <= 64)
+        hipLaunchKernelGGL((rq_merge_streams<64, true>), dim3((unsigned)a.n_chunk), dim3(64), 0, s, a);
+    else
+        hipLaunchKernelGGL((rq_merge_streams<RQ_MG_B, true>), dim3((unsigned)a.n_chunk), dim3(RQ_MG_B), 0, s, a);
     return hipGetLastError();
 }
 

@@ -34,7 +34,7 @@ PEAK = 8000.0
 SECTIONS = ["sweep_event_log", "log_expand", "scan", "replay_batch", "replay_batch_eid",
             "replay_batch_eid_chunked", "replay_one_df", "replay_one_df_one_workgroup",
             "replay_one_df_facade", "oracle_dp", "seq_multigraph_c3", "seq_600_sources",
-            "seq_max_events_c3"]
+            "seq_max_events_c3", "fast_600_sources", "fast_3000_sources"]
 REPLAY = {"log_expand", "replay_batch", "replay_batch_eid", "replay_batch_eid_chunked",
           "replay_one_df", "replay_one_df_one_workgroup", "replay_one_df_facade"}
 
@@ -171,10 +171,14 @@ def seq_world(name):
         so = graphs.c3()
         extra = [e for k, e in enumerate(so["edge_list"]) if e[0] != so["src_id"] and k % 10 == 0]
         return dict(so, edge_list=list(so["edge_list"]) + extra), None
-    if name == "seq_600_sources":
-        # 600 broadcasters (> 512: the fast instances own <= 8 sources per lane)
+    if name in ("seq_600_sources", "fast_600_sources"):
+        # 600 broadcasters: the fast general sweep on the two-level merged sequence, or
+        # (seq_: sweep_mode 2) the sequential sweep with 16 sources per lane
         return graphs.followers_graph(num_followers=1000, num_sources=600, degree=5,
                                       end_time=20.0, world_rate=1.0, alpha=1.0, beta=10.0), None
+    if name == "fast_3000_sources":
+        return graphs.followers_graph(num_followers=3000, num_sources=3000, degree=5,
+                                      end_time=4.0, world_rate=1.0, alpha=1.0, beta=10.0), None
     if name == "seq_max_events_c3":
         return graphs.c3(), 4000
     raise KeyError(name)
@@ -184,7 +188,7 @@ def seq(name, a, res, R=4096):
     so, max_ev = seq_world(name)
     g = graph_of(so)
     kw = dict(q=so["q"], s=so["s"], n_rep=R, ctrl_seed=0, world_seed=0, randomize=True,
-              max_events=max_ev, Ks=(1,))
+              max_events=max_ev, Ks=(1,), sweep_mode=2 if name == "seq_600_sources" else 0)
     plan = g.run("opt", plan_only=True, **kw)
     r, ms, wall = timed(lambda: g.run("opt", check=False, **kw), a.reps)
     ev = int(r.counts[:, 2].sum())
@@ -217,7 +221,8 @@ def main():
         scan(g, so, a, res)
     if want("oracle_dp"):
         oracle(a, res)
-    for k in ("seq_multigraph_c3", "seq_600_sources", "seq_max_events_c3"):
+    for k in ("seq_multigraph_c3", "seq_600_sources", "seq_max_events_c3", "fast_600_sources",
+              "fast_3000_sources"):
         if want(k):
             seq(k, a, res)
     print(json.dumps(res))

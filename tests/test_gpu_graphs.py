@@ -104,20 +104,43 @@ def _many_sources(n_src, n_sinks=120, deg=3, T=6.0, seed=11):
                 edge_list=edges)
 
 
-@pytest.mark.parametrize("n_src", [600, 1500])
-def test_more_than_512_sources(n_src):
+@pytest.mark.parametrize("n_src,seq", [(600, False), (1500, False), (3000, False), (6000, False),
+                                       (600, True), (1500, True)])
+def test_more_than_512_sources(n_src, seq):
+    """> 512 sources: the fast general sweep plays the two-level merged sequence
+    (rq_merge_streams over groups of 512 streams, then over the groups' sequences; any
+    number of sources up to 65535); the exact sequential sweep (sweep_mode 2) owns 16 / 32
+    sources per lane up to 2048.  Event logs and metrics == the engine oracle."""
     torch, engine, graphs, O = _ctx()
     so = _many_sources(n_src)
     g = _graph(engine, so)
-    plan = g.run("opt", q=1.0, s=1.0, n_rep=4, plan_only=True)
-    assert plan["variant"] in (1, 4) and plan["sources_per_lane"] == (16 if n_src <= 1024 else 32)
+    kw = dict(sweep_mode=2) if seq else {}
+    plan = g.run("opt", q=1.0, s=1.0, n_rep=4, plan_only=True, **kw)
+    if seq:
+        assert plan["variant"] in (1, 4) and plan["sources_per_lane"] == (16 if n_src <= 1024 else 32)
+    else:
+        assert plan["variant"] not in (1, 4) and plan["sources_per_lane"] == 0, plan
     Ks = (1, 2)
     res = g.run("opt", q=1.0, s=1.0, n_rep=4, ctrl_seed=2, world_seed=2, randomize=True, Ks=Ks,
-                event_log=True)
+                event_log=True, **kw)
     assert int(res.status.max().item()) == 0
     for r in (0, 3):
         met_o, t_o, s_o = _oracle(O, _world_with_seeds(so, 2 + r), ("opt", 2 + r), Ks)
         _cmp_replica(res, r, met_o, t_o, s_o, Ks)
+    if not seq:   # and without the event log, K = 1 (the per-wave sink-bit instance)
+        r1 = g.run("opt", q=1.0, s=1.0, n_rep=4, ctrl_seed=2, world_seed=2, randomize=True, Ks=(1,))
+        met_o, t_o, s_o = _oracle(O, _world_with_seeds(so, 2 + 3), ("opt", 2 + 3), (1,))
+        _cmp_replica(r1, 3, met_o, t_o, s_o, (1,))
+
+
+def test_more_than_2048_sources_sequential_unsupported():
+    """The exact sequential sweep stops at 2048 sources (32 per lane): a run that needs it
+    (here forced, sweep_mode 2) raises RQ_EUNSUPPORTED; the fast sweep takes the graph."""
+    torch, engine, graphs, O = _ctx()
+    from redqueen_amd import _lib as L
+    g = _graph(engine, _many_sources(3000))
+    with pytest.raises(L.RQError):
+        g.run("opt", q=1.0, s=1.0, n_rep=2, sweep_mode=2, Ks=(1,))
 
 
 def _wide(n_sinks=50000, n_src=40, deg=60, T=4.0):
