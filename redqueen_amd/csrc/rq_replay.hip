@@ -68,13 +68,22 @@ constexpr int RP_HS = 2 * RP_B;
 constexpr int RP_LOG_HS = RP_LOG_H - 1;
 constexpr int RP_HMAX_S = RP_HS - RP_B - 1;
 constexpr int RP_SMALL_NK = 1;
+// rq_rp_fast rows per thread: where a workgroup has its CU to itself (no more dataframes
+// than CUs: 3 with the small table, 2 with the full one, whose LDS never shares its CU),
+// else 1 (two small-table workgroups per CU).  256 C3 dataframes: 4.35 ms at 1 row per
+// thread, 3.76 at 2, 3.62 at 3 (scripts/bench_paths.py replay_batch)
+#ifndef RQ_RP_RFEW
+#define RQ_RP_RFEW 3
+#endif
+constexpr int RP_RFEW = RQ_RP_RFEW;   // the small table's rows per thread, one workgroup per CU
+static_assert(RP_RFEW * RP_B < 4096 && RP_B * 2 < 4096, "bucket counts are 12-bit");
 constexpr uint64_t RP_EMPTY_KEY = 0x8000000000000000ull;   // INT64_MIN: gets its own slot
 
 struct alignas(16) RpSlot {
     int cnt;        // rows of this sink so far (pos of its last row; 0: none yet, cell NaN)
     int lastown;    // pos of its latest own row (0: none); its last row's rank = cnt - lastown
     int lastgroup;  // t-group of its last row (-1: none)
-    int bucket;     // this batch: rows of the sink (bits 0-11), list offset (bits 12-22)
+    int bucket;     // this batch: rows of the sink (bits 0-11), list offset (bits 12-23)
 };
 
 __device__ __forceinline__ uint32_t rp_hash(uint64_t k, int bits)
@@ -82,12 +91,14 @@ __device__ __forceinline__ uint32_t rp_hash(uint64_t k, int bits)
     return (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> (64 - bits));
 }
 
-// open addressing, linear probing; returns the slot of key k (inserting it)
+// open addressing, linear probing; returns the slot of key k (inserting it).  A full
+// table (only possible once more sinks than the tier takes arrive in one batch) sets
+// *full and returns the sentinel slot mask + 1: the caller's tier gives the dataframe up.
 __device__ __forceinline__ uint32_t rp_insert(unsigned long long* keys, uint32_t mask, int bits,
-                                              uint64_t k, int* count)
+                                              uint64_t k, int* count, int* full)
 {
     uint32_t h = rp_hash(k, bits);
-    while (true) {
+    for (uint32_t p = 0; p <= mask; ++p) {
         const unsigned long long cur = keys[h];
         if (cur == k) return h;
         if (cur == RP_EMPTY_KEY) {
@@ -101,6 +112,8 @@ __device__ __forceinline__ uint32_t rp_insert(unsigned long long* keys, uint32_t
         }
         h = (h + 1) & mask;
     }
+    *full = 1;
+    return mask + 1;
 }
 
 __device__ __forceinline__ int64_t df_begin(const RpArgs& a, int64_t d) { return a.df_off ? a.df_off[d] : 0; }
@@ -124,6 +137,14 @@ __device__ __forceinline__ int64_t scan_add_i64_of_i32(int v)
 {
     const int hi = scan_add_i32(v >> 16);
     const int lo = scan_add_i32(v & 0xFFFF);
+    return (int64_t)hi * 65536 + (int64_t)lo;
+}
+// inclusive 64-lane sum of int64 values of magnitude < 2^47 (16-bit low halves and
+// the high parts scanned apart: exact)
+__device__ __forceinline__ int64_t scan_add_i64_small(int64_t v)
+{
+    const int hi = scan_add_i32((int)(v >> 16));
+    const int lo = scan_add_i32((int)(v & 0xFFFF));
     return (int64_t)hi * 65536 + (int64_t)lo;
 }
 // 16-lane (row 0) inclusive scans of the wave totals
@@ -179,11 +200,14 @@ struct RpAcc {
 // rq_rp_fast: one workgroup per dataframe
 // ============================================================================
 // TIER 0: small LDS table (first pass), 1: full LDS table (the dataframes tier 0 gave up:
-// RP_MID), 2: global table (those tier 1 gave up: RP_GLOBAL)
-template <int NK, int TIER>
+// RP_MID), 2: global table (those tier 1 gave up: RP_GLOBAL).  A batch is R * RP_B rows:
+// thread tid owns rows tid * R .. tid * R + R - 1 (row order within the thread, so every
+// block scan runs over per-thread partial sums: one barrier set per R * RP_B rows).
+template <int NK, int TIER, int R>
 __device__ __forceinline__ void rp_fast_body(RpArgs a)
 {
     constexpr bool GLOBAL = TIER == 2;
+    constexpr int BR = R * RP_B;
     const int64_t d = blockIdx.x;
     const int tid = threadIdx.x;
     const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -213,11 +237,11 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
         sp += (bytes + 15) & ~(size_t)15;
         return p;
     };
-    double* tb = reinterpret_cast<double*>(carve(8 * (RP_B + 2)));       // [0] prev, [1+i], [RP_B+1] next
-    int64_t* eb = reinterpret_cast<int64_t*>(carve(8 * (RP_B + 1)));     // [0] prev eid, [1+i]
-    int* gb = reinterpret_cast<int*>(carve(4 * RP_B));                    // t-group of row i
-    unsigned char* ob = carve(RP_B);                                      // own flag of row i
-    int* lst = reinterpret_cast<int*>(carve(4 * RP_B));                   // sink buckets: rows
+    double* tb = reinterpret_cast<double*>(carve(8 * (BR + 2)));         // [0] prev, [1+i], [BR+1] next
+    int64_t* eb = reinterpret_cast<int64_t*>(carve(8 * (BR + 1)));       // [0] prev eid, [1+i]
+    int* gb = reinterpret_cast<int*>(carve(4 * BR));                      // t-group of row i
+    unsigned char* ob = carve(BR);                                        // own flag of row i
+    int* lst = reinterpret_cast<int*>(carve(4 * BR));                     // sink buckets: rows
     int64_t* wsum = reinterpret_cast<int64_t*>(carve(8 * 16));            // wave totals (int64)
     int* ws32 = reinterpret_cast<int*>(carve(4 * 16 * (NK + 6)));         // wave totals (int)
     int* misc = reinterpret_cast<int*>(carve(4 * 16));                    // flags, counters
@@ -240,7 +264,8 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
     }
     tmask = (uint32_t)(tcap - 1);
     // misc: [0] unique sinks, [1] sentinel-key seen, [2] dup, [3] unsorted, [4] eid bad,
-    //       [5] own events, [6] world events, [7] key dump cursor, [8] bucket allocator
+    //       [5] own events, [6] world events, [7] key dump cursor, [8] bucket allocator,
+    //       [9] table full (a batch's new sinks found no empty slot: this tier gives up)
     if (tid < 16) misc[tid] = 0;
     if (TIER == a.first_tier && tid == 0) inf->flags = 0;   // this call's status (the first pass)
     for (int64_t h = tid; h <= tcap; h += RP_B) {
@@ -280,94 +305,116 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
     // issued at the top of batch b and consumed only at its end (prep), so they are
     // in flight across its barriers and nothing loaded is carried over the loop's
     // back edge (the waitcnt pass would otherwise wait for them early).
-    //   tb[0] = t of the previous batch's last row, tb[1 + i] = row i, tb[RP_B + 1] =
+    //   tb[0] = t of the previous batch's last row, tb[1 + i] = row i, tb[BR + 1] =
     //   t of the first row of the following batch; eb likewise for event ids.
-    bool own_c = false;       // this thread's row of the current batch: own post?
-    uint32_t slot_c = 0;      // ... its sink's slot
-    auto prep = [&](int64_t nb0, double t_, int64_t s_, int64_t k_, int64_t e_, double t_after,
-                    double t_before, int64_t e_before) {
-        const bool v = nb0 + tid < r1;
-        tb[1 + tid] = v ? t_ : 0.0;
-        if (has_eid) eb[1 + tid] = e_;
+    bool own_c[R];       // this thread's rows of the current batch: own posts?
+    uint32_t slot_c[R];  // ... their sinks' slots
+    auto load = [&](int64_t nb0, double (&t_)[R], int64_t (&s_)[R], int64_t (&k_)[R],
+                    int64_t (&e_)[R]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int64_t ii = nb0 + tid * R + r;
+            t_[r] = 0.0;
+            s_[r] = k_[r] = e_[r] = 0;
+            if (ii < r1) {
+                t_[r] = a.t[ii];
+                s_[r] = a.src[ii];
+                k_[r] = a.sink[ii];
+                if (has_eid) e_[r] = a.eid[ii];
+            }
+        }
+    };
+    auto prep = [&](int64_t nb0, const double (&t_)[R], const int64_t (&s_)[R], const int64_t (&k_)[R],
+                    const int64_t (&e_)[R], double t_after, double t_before,
+                    int64_t e_before) __attribute__((always_inline)) {
         if (tid == 0) {
             tb[0] = t_before;
             eb[0] = e_before;
-            tb[RP_B + 1] = t_after;
+            tb[BR + 1] = t_after;
         }
-        own_c = v && s_ == a.src_id;
-        slot_c = 0;
-        if (v) {
-            if ((uint64_t)k_ == RP_EMPTY_KEY) {
-                slot_c = (uint32_t)tcap;   // the sentinel id's own slot
-                if (misc[1] == 0 && atomicExch(&misc[1], 1) == 0) atomicAdd(&misc[0], 1);
-            } else {
-                slot_c = rp_insert(tkeys, tmask, tbits, (uint64_t)k_, &misc[0]);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int row = tid * R + r;
+            const bool v = nb0 + row < r1;
+            tb[1 + row] = v ? t_[r] : 0.0;
+            if (has_eid) eb[1 + row] = e_[r];
+            own_c[r] = v && s_[r] == a.src_id;
+            slot_c[r] = 0;
+            if (v) {
+                if ((uint64_t)k_[r] == RP_EMPTY_KEY) {
+                    slot_c[r] = (uint32_t)tcap;   // the sentinel id's own slot
+                    if (misc[1] == 0 && atomicExch(&misc[1], 1) == 0) atomicAdd(&misc[0], 1);
+                } else {
+                    slot_c[r] = rp_insert(tkeys, tmask, tbits, (uint64_t)k_[r], &misc[0], &misc[9]);
+                }
             }
         }
     };
     {
-        const int64_t i0 = r0 + tid;
-        double t0 = 0.0, ta = 0.0;
-        int64_t s0 = 0, k0 = 0, e0 = 0;
-        if (i0 < r1) {
-            t0 = a.t[i0];
-            s0 = a.src[i0];
-            k0 = a.sink[i0];
-            if (has_eid) e0 = a.eid[i0];
-        }
-        if (tid == 0 && r0 + RP_B < r1) ta = a.t[r0 + RP_B];
+        double t0[R];
+        int64_t s0[R], k0[R], e0[R];
+        load(r0, t0, s0, k0, e0);
+        double ta = 0.0;
+        if (tid == 0 && r0 + BR < r1) ta = a.t[r0 + BR];
         prep(r0, t0, s0, k0, e0, ta, 0.0, 0);
     }
 
-    for (int64_t b0 = r0; b0 < r1; b0 += RP_B) {
-        const int64_t i = b0 + tid;
-        const bool valid = i < r1;
-        const bool has_next = b0 + RP_B < r1;
+    for (int64_t b0 = r0; b0 < r1; b0 += BR) {
+        const bool has_next = b0 + BR < r1;
         // next batch (in flight across this batch's barriers)
-        const int64_t in = i + RP_B;
-        double tn = 0.0, tnn = 0.0;
-        int64_t sn = 0, kn = 0, en = 0;
-        if (in < r1) {
-            tn = a.t[in];
-            sn = a.src[in];
-            kn = a.sink[in];
-            if (has_eid) en = a.eid[in];
-        }
-        if (tid == 0 && b0 + 2 * RP_B < r1) tnn = a.t[b0 + 2 * RP_B];
+        double tn[R];
+        int64_t sn[R], kn[R], en[R];
+        load(b0 + BR, tn, sn, kn, en);
+        double tnn = 0.0;
+        if (tid == 0 && b0 + 2 * BR < r1) tnn = a.t[b0 + 2 * BR];
 
         // ---- A: neighbours of every row; its ticket in its sink's bucket ----
         __syncthreads();
-        const int last = (int)((r1 - b0) < RP_B ? (r1 - b0) : RP_B);
-        const double ti = tb[1 + tid];
-        const double t_prev = tb[tid], t_next = tb[tid + 2];
+        const int last = (int)((r1 - b0) < BR ? (r1 - b0) : BR);
         const double t_last = tb[last];
         const int64_t e_last = has_eid ? eb[last] : 0;
-        const bool first_row = i == r0;
-        const bool start = valid && (first_row || ti != t_prev);
-        const bool endg = valid && (i == r1 - 1 || t_next != ti);
-        const bool own = own_c;
-        RpSlot* sl = tst + slot_c;
-        const int ticket = valid ? bk_add(sl) : 0;   // rows of this sink before me: unordered
-        ob[tid] = own ? 1 : 0;
-        if (valid && !first_row && ti < t_prev) misc[3] = 1;
-        int ev_own = 0, ev_world = 0;
-        if (has_eid && valid) {
-            const int64_t ei = eb[1 + tid], e_prev = eb[tid];
-            const bool fe = first_row || ei != e_prev;
-            if (!first_row && ei < e_prev) misc[4] = 1;
-            ev_own = fe && own;
-            ev_world = fe && !own;
+        bool valid[R], start[R], endg[R];
+        double ti[R], tnx[R];
+        int ticket[R];
+        int st_loc = 0, evo = 0, evw = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int row = tid * R + r;
+            const int64_t i = b0 + row;
+            valid[r] = i < r1;
+            ti[r] = tb[1 + row];
+            const double t_prev = tb[row];
+            tnx[r] = tb[row + 2];
+            const bool first_row = i == r0;
+            start[r] = valid[r] && (first_row || ti[r] != t_prev);
+            endg[r] = valid[r] && (i == r1 - 1 || tnx[r] != ti[r]);
+            ticket[r] = valid[r] ? bk_add(tst + slot_c[r]) : 0;   // rows of this sink before me: unordered
+            ob[row] = own_c[r] ? 1 : 0;
+            if (valid[r] && !first_row && ti[r] < t_prev) misc[3] = 1;
+            if (has_eid && valid[r]) {
+                const int64_t ei = eb[1 + row], e_prev = eb[row];
+                const bool fe = first_row || ei != e_prev;
+                if (!first_row && ei < e_prev) misc[4] = 1;
+                evo += fe && own_c[r];
+                evw += fe && !own_c[r];
+            }
+            st_loc += start[r];
         }
-        if (!GLOBAL && misc[0] > (TIER == 0 ? RP_HMAX_S : RP_HMAX)) aborted = true;   // uniform: read after the barrier
+        if (!GLOBAL && (misc[0] > (TIER == 0 ? RP_HMAX_S : RP_HMAX) || misc[9]))
+            aborted = true;   // uniform: read after the barrier
 
         // ---- B: t-group of every row (block scan of group starts) + event counts;
         //      buckets of more than one row get list space ----
-        const int st_incl = scan_add_i32((int)start);
-        const uint64_t bo = __ballot(ev_own), bw = __ballot(ev_world);
+        const int st_incl = scan_add_i32(st_loc);
+        int nbo = 0, nbw = 0;
+        if (has_eid) {
+            nbo = scan_add_i32(evo);
+            nbw = scan_add_i32(evw);
+        }
         if (lane == 63) {
             ws32[w] = st_incl;
-            ws32[16 + w] = popc(bo);
-            ws32[32 + w] = popc(bw);
+            ws32[16 + w] = nbo;
+            ws32[32 + w] = nbw;
         }
         __syncthreads();
         if (aborted) break;
@@ -375,89 +422,133 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
         totals_add(ws32, w, st_pre, st_tot);
         totals_add(ws32 + 16, w, dummy, n_ev_own);
         totals_add(ws32 + 32, w, dummy, n_ev_world);
-        const int64_t G = Gc + (int64_t)(st_pre + st_incl) - 1;   // this row's t-group (pivot row index)
-        gb[tid] = (int)G;
-        const RpSlot st0 = valid ? *sl : RpSlot{0, 0, -1, 0};   // state before this batch
-        // rows of my sink in this batch (low bits: the ticket-0 row may already have
-        // added the list offset)
-        const int m = valid ? ((GLOBAL ? bk_read(sl) : st0.bucket) & 0xFFF) : 0;
-        if (valid && m > 1 && ticket == 0) bk_write(sl, (atomicAdd(&misc[8], m) << 12) | m);
-        __syncthreads();
-
-        // ---- C: my place among my sink's rows in this batch ----
-        int boff = 0;
-        if (valid && m > 1) {
-            boff = bk_read(sl) >> 12;
-            lst[boff + ticket] = tid;
+        int64_t G[R];   // each row's t-group (pivot row index)
+        {
+            int64_t g = Gc + (int64_t)(st_pre + st_incl - st_loc) - 1;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                g += start[r];
+                G[r] = g;
+                gb[tid * R + r] = (int)g;
+            }
+        }
+        RpSlot st0[R];   // state before this batch
+        int m[R];        // rows of the row's sink in this batch
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            RpSlot* sl = tst + slot_c[r];
+            st0[r] = valid[r] ? *sl : RpSlot{0, 0, -1, 0};
+            // (low bits: the ticket-0 row may already have added the list offset)
+            m[r] = valid[r] ? ((GLOBAL ? bk_read(sl) : st0[r].bucket) & 0xFFF) : 0;
+            if (valid[r] && m[r] > 1 && ticket[r] == 0) bk_write(sl, (atomicAdd(&misc[8], m[r]) << 12) | m[r]);
         }
         __syncthreads();
-        // j: my sink's rows before me; pred: the last of them; own_le / own_lt: its
-        // latest own row at or before / before me (rows in batch order = tid order)
-        int j = 0, pred = -1, own_le = own ? tid : -1, own_lt = -1;
-        if (valid && m > 1) {
-            for (int k = 0; k < m; ++k) {
-                const int y = lst[boff + k];
-                if (y < tid) {
-                    ++j;
-                    pred = pred > y ? pred : y;
-                    if (ob[y]) {
-                        own_lt = own_lt > y ? own_lt : y;
-                        own_le = own_le > y ? own_le : y;
+
+        // ---- C: each row's place among its sink's rows in this batch ----
+        int boff[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            boff[r] = 0;
+            if (valid[r] && m[r] > 1) {
+                boff[r] = bk_read(tst + slot_c[r]) >> 12;
+                lst[boff[r] + ticket[r]] = tid * R + r;
+            }
+        }
+        __syncthreads();
+        int xs[R], xv[R], xc[R][NK];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int row = tid * R + r;
+            // j: my sink's rows before me; pred: the last of them; own_le / own_lt: its
+            // latest own row at or before / before me (rows in batch order)
+            int j = 0, pred = -1, own_le = own_c[r] ? row : -1, own_lt = -1;
+            if (valid[r] && m[r] > 1) {
+                for (int k = 0; k < m[r]; ++k) {
+                    const int y = lst[boff[r] + k];
+                    if (y < row) {
+                        ++j;
+                        pred = pred > y ? pred : y;
+                        if (ob[y]) {
+                            own_lt = own_lt > y ? own_lt : y;
+                            own_le = own_le > y ? own_le : y;
+                        }
                     }
                 }
             }
-        }
-        int j_le = 0, j_lt = 0;   // positions of own_le / own_lt among the bucket
-        if (valid && m > 1 && (own_le >= 0 || own_lt >= 0)) {
-            for (int k = 0; k < m; ++k) {
-                const int y = lst[boff + k];
-                j_le += y < own_le;
-                j_lt += y < own_lt;
+            int j_le = 0, j_lt = 0;   // positions of own_le / own_lt among the bucket
+            if (valid[r] && m[r] > 1 && (own_le >= 0 || own_lt >= 0)) {
+                for (int k = 0; k < m[r]; ++k) {
+                    const int y = lst[boff[r] + k];
+                    j_le += y < own_le;
+                    j_lt += y < own_lt;
+                }
+            } else if (own_le >= 0) {
+                j_le = j;   // own_le == row
             }
-        } else if (own_le >= 0) {
-            j_le = j;   // own_le == tid
-        }
-        RpAcc<NK> x;
-        x.s = 0;
-        x.v = 0;
+            xs[r] = 0;
+            xv[r] = 0;
 #pragma unroll
-        for (int q = 0; q < NK; ++q) x.c[q] = 0;
-        if (valid) {
-            const int pos = st0.cnt + j + 1;
-            const int lastown = own_le >= 0 ? st0.cnt + j_le + 1 : st0.lastown;
-            const int rank = pos - lastown;
-            int prevrank, prevg;
-            if (j > 0) {
-                prevrank = (pos - 1) - (own_lt >= 0 ? st0.cnt + j_lt + 1 : st0.lastown);
-                prevg = gb[pred];
-            } else {
-                prevrank = st0.cnt > 0 ? st0.cnt - st0.lastown : -1;
-                prevg = st0.lastgroup;
-            }
-            if (prevg == (int)G) misc[2] = 1;   // two rows of one sink at one t: a pivot mean
-            const bool pnan = prevrank < 0;
-            x.s = rank - (pnan ? 0 : prevrank);
-            x.v = pnan ? 1 : 0;
+            for (int q = 0; q < NK; ++q) xc[r][q] = 0;
+            if (valid[r]) {
+                const RpSlot s0 = st0[r];
+                const int pos = s0.cnt + j + 1;
+                const int lastown = own_le >= 0 ? s0.cnt + j_le + 1 : s0.lastown;
+                const int rank = pos - lastown;
+                int prevrank, prevg;
+                if (j > 0) {
+                    prevrank = (pos - 1) - (own_lt >= 0 ? s0.cnt + j_lt + 1 : s0.lastown);
+                    prevg = gb[pred];
+                } else {
+                    prevrank = s0.cnt > 0 ? s0.cnt - s0.lastown : -1;
+                    prevg = s0.lastgroup;
+                }
+                if (prevg == (int)G[r]) misc[2] = 1;   // two rows of one sink at one t: a pivot mean
+                const bool pnan = prevrank < 0;
+                xs[r] = rank - (pnan ? 0 : prevrank);
+                xv[r] = pnan ? 1 : 0;
 #pragma unroll
-            for (int q = 0; q < NK; ++q)
-                x.c[q] = (rank <= km1[q] ? 1 : 0) - ((!pnan && prevrank <= km1[q]) ? 1 : 0);
-            if (j == m - 1) {   // my sink's last row of this batch carries its state on
-                sl->cnt = pos;
-                sl->lastown = lastown;
-                sl->lastgroup = (int)G;
-                bk_write(sl, 0);
+                for (int q = 0; q < NK; ++q)
+                    xc[r][q] = (rank <= km1[q] ? 1 : 0) - ((!pnan && prevrank <= km1[q]) ? 1 : 0);
+                if (j == m[r] - 1) {   // my sink's last row of this batch carries its state on
+                    RpSlot* sl = tst + slot_c[r];
+                    sl->cnt = pos;
+                    sl->lastown = lastown;
+                    sl->lastgroup = (int)G[r];
+                    bk_write(sl, 0);
+                }
             }
         }
 
         // the next batch's rows (their loads have landed by now) into LDS, sinks hashed
         // (tb / eb were last read in A, two barriers ago)
-        if (has_next) prep(b0 + RP_B, tn, sn, kn, en, tnn, t_last, e_last);
+        if (has_next) prep(b0 + BR, tn, sn, kn, en, tnn, t_last, e_last);
 
         // ---- D: running totals in row order; the last row of a t-group emits its pivot row ----
-        x.s = scan_add_i64_of_i32((int)x.s);
-        x.v = scan_add_i32(x.v);
+        // this thread's rows: inclusive prefixes in registers; the threads' totals are
+        // block-scanned (|a row's change| < 2^31, so R rows' sum < 2^47: two 32-bit scans)
+        int64_t ls = 0;
+        int lv = 0, lc[NK];
 #pragma unroll
-        for (int q = 0; q < NK; ++q) x.c[q] = scan_add_i32(x.c[q]);
+        for (int q = 0; q < NK; ++q) lc[q] = 0;
+        int64_t ps[R];
+        int pv[R], pc[R][NK];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            ls += xs[r];
+            lv += xv[r];
+            ps[r] = ls;
+            pv[r] = lv;
+#pragma unroll
+            for (int q = 0; q < NK; ++q) {
+                lc[q] += xc[r][q];
+                pc[r][q] = lc[q];
+            }
+        }
+        RpAcc<NK> x;   // inclusive over the wave's threads
+        x.s = scan_add_i64_small(ls);
+        x.v = scan_add_i32(lv);
+#pragma unroll
+        for (int q = 0; q < NK; ++q) x.c[q] = scan_add_i32(lc[q]);
         if (lane == 63) {
             wsum[w] = x.s;
             ws32[80 + w] = x.v;
@@ -470,13 +561,23 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
         totals_add(ws32 + 80, w, pre.v, tot.v);
 #pragma unroll
         for (int q = 0; q < NK; ++q) totals_add(ws32 + 96 + 16 * q, w, pre.c[q], tot.c[q]);
-        if (endg) {
-            const int64_t row = r0 + G;
-            a.rows_dt[row] = (i == r1 - 1 ? a.end : t_next) - ti;
-            a.rows_sum[row] = (double)(carry.s + pre.s + x.s);
-            a.rows_valid[row] = (uint32_t)(carry.v + pre.v + x.v);
+        // this thread's exclusive base: carry + earlier waves + earlier lanes
+        const int64_t bs = carry.s + pre.s + (x.s - ls);
+        const int bv = carry.v + pre.v + (x.v - lv);
+        int bc[NK];
 #pragma unroll
-            for (int q = 0; q < NK; ++q) a.rows_cnt[row * NK + q] = (uint32_t)(carry.c[q] + pre.c[q] + x.c[q]);
+        for (int q = 0; q < NK; ++q) bc[q] = carry.c[q] + pre.c[q] + (x.c[q] - lc[q]);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (endg[r]) {
+                const int64_t i = b0 + tid * R + r;
+                const int64_t row = r0 + G[r];
+                a.rows_dt[row] = (i == r1 - 1 ? a.end : tnx[r]) - ti[r];
+                a.rows_sum[row] = (double)(bs + ps[r]);
+                a.rows_valid[row] = (uint32_t)(bv + pv[r]);
+#pragma unroll
+                for (int q = 0; q < NK; ++q) a.rows_cnt[row * NK + q] = (uint32_t)(bc[q] + pc[r][q]);
+            }
         }
         carry.s += tot.s;
         carry.v += tot.v;
@@ -525,15 +626,16 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
     }
 }
 
-template <int NK, bool GLOBAL>
+template <int NK, bool GLOBAL, int R>
 __global__ __launch_bounds__(RP_B) void rq_rp_fast(RpArgs a)
 {
-    rp_fast_body<NK, GLOBAL ? 2 : 1>(a);
+    rp_fast_body<NK, GLOBAL ? 2 : 1, R>(a);
 }
-template <int NK>
-__global__ __launch_bounds__(RP_B) __attribute__((amdgpu_waves_per_eu(8, 8))) void rq_rp_fast_s(RpArgs a)
+// R == 1: <= 64 VGPRs so two workgroups (half-size tables) share a CU
+template <int NK, int R>
+__global__ __launch_bounds__(RP_B) __attribute__((amdgpu_waves_per_eu(R == 1 ? 8 : 4, R == 1 ? 8 : 4))) void rq_rp_fast_s(RpArgs a)
 {
-    rp_fast_body<NK, 0>(a);
+    rp_fast_body<NK, 0, R>(a);
 }
 
 // ============================================================================
@@ -1527,10 +1629,11 @@ __global__ __launch_bounds__(256) void rq_rp_scan(RpArgs a)
 // ============================================================================
 namespace {
 template <int TIER>
-size_t rp_fast_lds(int nK)
+size_t rp_fast_lds(int nK, int R)
 {
     auto al = [](size_t b) { return (b + 15) & ~(size_t)15; };
-    size_t s = al(8 * (RP_B + 2)) + al(8 * (RP_B + 1)) + al(4 * RP_B) + al(RP_B) + al(4 * RP_B) +
+    const size_t br = (size_t)R * RP_B;
+    size_t s = al(8 * (br + 2)) + al(8 * (br + 1)) + al(4 * br) + al(br) + al(4 * br) +
                al(8 * 16) + al(4 * 16 * (nK + 6)) + al(4 * 16);
     const size_t h = TIER == 0 ? RP_HS : RP_H;
     if (TIER < 2) s += al(8 * (h + 1)) + al(sizeof(RpSlot) * (h + 1));
@@ -1544,27 +1647,39 @@ size_t rc_apply_lds(int nK)
            al(4 * 16) + al(sizeof(RpSlot) * RC_S);
 }
 
+int rp_num_cus()
+{
+    static thread_local int dev = -1, cus = 0;
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess) return 256;
+    if (d != dev) {
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || cus <= 0)
+            cus = 256;
+        dev = d;
+    }
+    return cus;
+}
+
 template <int NK>
 hipError_t rp_launch_t(const RpArgs& a, int phase, hipStream_t s)
 {
     const unsigned nd = (unsigned)a.n_df;
+    // no more dataframes than CUs: every workgroup has a CU to itself (2 rows per thread)
+    const bool few = nd <= (unsigned)rp_num_cus();
     switch (phase) {
     case RP_PHASE_SMALL:
         if constexpr (NK <= RP_SMALL_NK) {
-            const size_t lds = rp_fast_lds<0>(NK);
-            hipLaunchKernelGGL((rq_rp_fast_s<NK>), dim3(nd), dim3(RP_B), lds, s, a);
+            if (few) hipLaunchKernelGGL((rq_rp_fast_s<NK, RP_RFEW>), dim3(nd), dim3(RP_B), rp_fast_lds<0>(NK, RP_RFEW), s, a);
+            else hipLaunchKernelGGL((rq_rp_fast_s<NK, 1>), dim3(nd), dim3(RP_B), rp_fast_lds<0>(NK, 1), s, a);
         }
         break;
-    case RP_PHASE_FAST: {
-        const size_t lds = rp_fast_lds<1>(NK);
-        hipLaunchKernelGGL((rq_rp_fast<NK, false>), dim3(nd), dim3(RP_B), lds, s, a);
+    case RP_PHASE_FAST:   // the full table's LDS keeps one workgroup per CU anyway
+        hipLaunchKernelGGL((rq_rp_fast<NK, false, 2>), dim3(nd), dim3(RP_B), rp_fast_lds<1>(NK, 2), s, a);
         break;
-    }
-    case RP_PHASE_GLOBAL: {
-        const size_t lds = rp_fast_lds<2>(NK);
-        hipLaunchKernelGGL((rq_rp_fast<NK, true>), dim3(nd), dim3(RP_B), lds, s, a);
+    case RP_PHASE_GLOBAL:
+        if (few) hipLaunchKernelGGL((rq_rp_fast<NK, true, 2>), dim3(nd), dim3(RP_B), rp_fast_lds<2>(NK, 2), s, a);
+        else hipLaunchKernelGGL((rq_rp_fast<NK, true, 1>), dim3(nd), dim3(RP_B), rp_fast_lds<2>(NK, 1), s, a);
         break;
-    }
     case RP_PHASE_KEYS:
         hipLaunchKernelGGL(rq_rp_keys, dim3(nd), dim3(RP_B), 0, s, a);
         break;

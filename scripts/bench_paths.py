@@ -31,11 +31,11 @@ from redqueen_amd import _lib as L  # noqa: E402
 from redqueen_amd import engine, graphs, utils  # noqa: E402
 
 PEAK = 8000.0
-SECTIONS = ["sweep_event_log", "log_expand", "scan", "replay_batch", "replay_batch_eid",
+SECTIONS = ["sweep_event_log", "log_expand", "scan", "replay_batch", "replay_batch_eid", "replay_batch_1024",
             "replay_batch_eid_chunked", "replay_one_df", "replay_one_df_one_workgroup",
             "replay_one_df_facade", "oracle_dp", "seq_multigraph_c3", "seq_600_sources",
             "seq_max_events_c3", "fast_600_sources", "fast_3000_sources"]
-REPLAY = {"log_expand", "replay_batch", "replay_batch_eid", "replay_batch_eid_chunked",
+REPLAY = {"log_expand", "replay_batch", "replay_batch_eid", "replay_batch_1024", "replay_batch_eid_chunked",
           "replay_one_df", "replay_one_df_one_workgroup", "replay_one_df_facade"}
 
 
@@ -117,6 +117,21 @@ def replay(g, so, a, res, want):
                     "GBps": per_row * nrow / (ms[3] + ms[2]) / 1e6,
                     "frac": per_row * nrow / (ms[3] + ms[2]) / 1e6 / PEAK,
                     "equal_to_sweep": bool(torch.equal(m4, r2.metrics))}
+    if want("replay_batch_1024"):   # 1024 dataframes: four per CU
+        r3 = g.run("opt", q=so["q"], s=so["s"], n_rep=1024, ctrl_seed=0, world_seed=0,
+                   randomize=True, event_log=True)
+        ro3, cols3 = r3.log_columns()
+        off3 = torch.from_numpy(ro3).cuda()
+        n3 = int(ro3[-1])
+        (m6, c6), ms, wall = timed(lambda: utils.replay_columns(
+            cols3["t"], cols3["src_id"], cols3["sink_id"], None, off3, so["src_id"], so["end_time"],
+            (1,)), a.reps)
+        res["replay_batch_1024"] = {"dataframes": 1024, "rows": n3, "ms_fast": ms[3], "ms_scan": ms[2],
+                                    "wall_ms": wall * 1e3, "bytes": 24 * n3,
+                                    "GBps": 24 * n3 / (ms[3] + ms[2]) / 1e6,
+                                    "frac": 24 * n3 / (ms[3] + ms[2]) / 1e6 / PEAK,
+                                    "equal_to_sweep": bool(torch.equal(m6, r3.metrics))}
+        del r3, cols3, off3
     if want("replay_batch_eid_chunked"):   # the same batch through the chunked path, forced (A/B)
         os.environ["RQ_RP_CHUNK"] = "1"
         (m4, c4), ms, wall = timed(lambda: utils.replay_columns(
