@@ -179,7 +179,7 @@ struct Plan {
     bool log = false, bits = false;
     // K=1 on per-wave LDS sink bits for graphs past the bitset variant (> 64 sources)
     bool bl = false;
-    size_t g_fb = 0, g_etab = 0, g_inv = 0;
+    size_t g_fb = 0, g_etab = 0, g_inv = 0, g_skip = 0;
     bool g_inv_sh = false;   // general sweep: 1/c_j in the block's shared LDS (one grid point)
     bool gs = false;         // LOG sweep: per-sink state in global memory, gs_slots wave slots
     int64_t gs_slots = 0, gs_stride = 0;
@@ -481,6 +481,24 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
             if (p->log) return RQ_EUNSUPPORTED;
             p->log = true;   // no fast instance fits this graph: the exact sequential sweep
             goto replan;
+        }
+        // BL on merged streams: a per-wave stamp (the reset epoch a stream last played in)
+        // and first-lane table per stream let a tile skip the events whose stream already
+        // played since the last post -- their sinks are out of the top-1 set and valid.
+        // Only where it costs no resident waves.
+        p->g_skip = 0;
+        if (p->bl && p->mrg && !p->gs) {
+            const size_t st2 = align_up(p->g_wave_stride + 8 * (size_t)g->n_str, 16);
+            const size_t tot2 = p->g_wave + p->gwpb * st2;
+            int blocks = tot2 <= kLdsMax ? rq_sweep_blocks_per_cu(0, p->nK, p->gcol16, p->gwin, 0, 2, p->gwpb, tot2) : 0;
+            if (tot2 <= kLdsMax && blocks <= 0) blocks = (int)std::min<size_t>(kLdsMax / tot2, 16 / p->gwpb);
+            bool on = blocks * p->gwpb >= p->wpc;
+            if (const char* e = getenv("RQ_SKIP")) on = on && atoi(e) != 0;   // A/B only
+            if (on) {
+                p->g_skip = p->g_wave_stride;
+                p->g_wave_stride = st2;
+                p->g_total = tot2;
+            }
         }
     }
 
@@ -1215,6 +1233,7 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             sa.fbits = g->d_fbits.p;
             sa.nwl = (g->n_sinks + 31) / 32;
             sa.lds_fbits = p.g_fb;
+            sa.lds_skip = p.g_skip;
             sa.lds_etab = p.g_etab;
             sa.lds_invc = p.g_inv;
             sa.invc_shared = !p.fw && p.g_inv_sh;

@@ -96,6 +96,14 @@ __device__ __forceinline__ int bcast_i(int v, int src_lane)
     return __builtin_amdgcn_readlane(v, src_lane);
 }
 
+// a wave-uniform 64-bit value (a ballot, a mask built from ballots) pinned to SGPRs, so
+// the code derived from it stays on the scalar unit
+__device__ __forceinline__ uint64_t sgpr_u64(uint64_t v)
+{
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
 __device__ __forceinline__ int64_t bcast_i64(int64_t v, int src_lane)
 {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, src_lane);

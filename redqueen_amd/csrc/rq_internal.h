@@ -92,6 +92,7 @@ struct SweepArgs {
     const uint32_t* fbits;   // follower set as a sink bitset [nwl] (BL variant)
     int nwl;                 // BL: words per per-wave T / V bitset = ceil(n_sinks / 32)
     size_t lds_fbits;        // BL: the follower bitset's place in the block's shared LDS
+    size_t lds_skip;         // BL + MRG: per-wave stream stamps / first-lane table (0: no skipping)
     size_t lds_etab;         // fused sweep: rq_exp's table (64 x u64) in the block's shared LDS
     int dbg;                 // profiling: 1 skip phase C, 2 skip sink updates, 3 skip phase B
     unsigned long long* clk; // RQ_PHASE_CLOCK builds only: per-phase s_memtime sums [8]
