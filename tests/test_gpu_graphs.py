@@ -6,7 +6,10 @@ GPU, bit for bit against the engine-semantics oracle (oracle/rq_oracle.c):
   (:74-76) and the pivot cells average the repeated rows' ranks; the all-RealData
   multigraph worlds equal the REFERENCE's own df (tests/test_gpu_realdata.py,
   realdata.npz rdmg*);
-* more than 512 sources (16 and 32 sources per lane, sequential sweep);
+* more than 512 sources (the two-level merge feeding the fast sweep, up to 65535; the
+  sequential sweep at 16 and 32 sources per lane, up to 2048);
+* the repeat-stream skip of the per-wave sink-bit sweep (a stream's second event
+  before the next reset walks no sinks): on and off, bit for bit;
 * 50k sinks (per-wave sink bits for K = 1, int16 ranks for K > 1, and the
   sequential sweep with its per-sink state in global memory).
 
@@ -141,6 +144,57 @@ def test_more_than_2048_sources_sequential_unsupported():
     g = _graph(engine, _many_sources(3000))
     with pytest.raises(L.RQError):
         g.run("opt", q=1.0, s=1.0, n_rep=2, sweep_mode=2, Ks=(1,))
+
+
+def _bursty(n_src=200, n_sinks=3000, deg=40, n_fol=900, T=6.0, seed=17):
+    """Per-wave sink bits on merged streams (K = 1, too many streams x sink words for
+    the BITS tables): bursty Hawkes streams, so a stream often plays again before the
+    controller's next post."""
+    rs = np.random.RandomState(seed)
+    sinks = list(range(1, n_sinks + 1))
+    fol = sorted(int(x) for x in rs.choice(sinks, n_fol, replace=False))
+    edges = [(0, f) for f in fol]
+    others = []
+    for k in range(n_src):
+        sid = 10 + k
+        d = 0 if k % 37 == 5 else (150 if k % 29 == 3 else deg)   # no sinks / > 128 sinks
+        edges += [(sid, int(y)) for y in rs.choice(sinks, d, replace=False)]
+        if k % 2:
+            others.append(("Hawkes", {"src_id": sid, "seed": k, "l_0": 0.4, "alpha": 1.0, "beta": 1.6}))
+        else:
+            others.append(("Poisson2", {"src_id": sid, "seed": k, "rate": 0.7}))
+    return dict(src_id=0, end_time=T, q=0.05, s=1.0, sink_ids=sinks, other_sources=others,
+                edge_list=edges)
+
+
+@pytest.mark.parametrize("ctrl", ["opt", "poisson"])
+def test_repeat_stream_skip(ctrl, monkeypatch):
+    """The per-wave sink-bit sweep skips the sink walk of an event whose stream already
+    played since the last reset (a post, or -- Poisson control -- an own-stream
+    arrival): every sink of its row is out of the top-1 set and valid.  Skip on
+    (default) == skip off (RQ_SKIP=0) bit for bit, and both == the engine oracle."""
+    torch, engine, graphs, O = _ctx()
+    so = _bursty()
+    g = _graph(engine, so)
+    R, Ks = 12, (1,)
+    kw = dict(n_rep=R, ctrl_seed=30, world_seed=30, randomize=True, Ks=Ks)
+    if ctrl == "opt":
+        args, kw = ("opt",), dict(kw, q=so["q"], s=so["s"])
+    else:
+        args, kw = ("poisson",), dict(kw, ctrl_rate=[3.0])
+    plan = g.run(*args, plan_only=True, **kw)
+    assert plan["variant"] == 3 and plan["sources_per_lane"] == 0, plan
+    res = g.run(*args, **kw)
+    monkeypatch.setenv("RQ_SKIP", "0")
+    res0 = g.run(*args, **kw)
+    monkeypatch.delenv("RQ_SKIP")
+    assert int(res.status.max().item()) == 0
+    assert torch.equal(res.metrics, res0.metrics)
+    assert torch.equal(res.counts, res0.counts)
+    for r in (0, 5, R - 1):
+        c = ("opt", 30 + r) if ctrl == "opt" else ("poisson", 30 + r, 3.0)
+        met_o, t_o, s_o = _oracle(O, _world_with_seeds(so, 30 + r), c, Ks)
+        _cmp_replica(res, r, met_o, t_o, s_o, Ks)
 
 
 def _wide(n_sinks=50000, n_src=40, deg=60, T=4.0):
