@@ -133,9 +133,12 @@ def build_stamp():
         h.update(f.read())
     src = hashlib.sha256()
     root = os.path.dirname(_HERE)
+    # the files librq.so is built from (csrc/asan.mk, the host-sanitizer build, is not
+    # one of them and does not travel to the GPU box)
     for fn in sorted(glob.glob(os.path.join(_HERE, "csrc", "*")) +
                      [os.path.join(root, "include", "rq.h")]):
-        if os.path.isfile(fn):
+        if os.path.isfile(fn) and (fn.endswith((".hip", ".h", ".cpp")) or
+                                   os.path.basename(fn) == "Makefile"):
             with open(fn, "rb") as f:
                 src.update(os.path.basename(fn).encode() + b"\0" + f.read())
     return {"librq_sha256": h.hexdigest()[:16], "csrc_sha256": src.hexdigest()[:16]}
