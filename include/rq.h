@@ -152,7 +152,7 @@ typedef struct rq_batch_desc {
     int32_t flags;               /* RQ_RUN_EVENT_LOG                                              */
     double cap_scale;            /* >= 1: multiplies every auto-sized capacity                   */
     int64_t chunk;               /* replicas per launch (0 = library default: the batch in an   */
-                                 /* even number of chunks of <= 16384, pipelined on two streams */
+                                 /* even number of chunks of <= 131072, pipelined on two streams */
                                  /* within a 200 GiB workspace budget)                          */
     int64_t replica0;            /* this call runs global replicas [replica0, replica0+n_local):  */
     int64_t n_local;             /* a shard of the grid (0 = all n_grid*n_rep); outputs are      */

@@ -562,7 +562,7 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
 
     // pipelined chunks for the merged-stream sweeps (not the sequential LOG sweep, whose
     // global per-sink slots are sized for one grid): the batch in an even number of
-    // chunks of <= 16384 replicas on two streams, so the two streams' generation, merge,
+    // chunks of <= 131072 replicas on two streams, so the two streams' generation, merge,
     // sweep and scan run side by side and one chunk's sweep tail is the other's work.
     // C3, 10k replicas (profiles/r04_pipe_ab.txt): one stream 3.02 ms per step; two
     // streams x 2 chunks of 5000 2.82 ms; 3 x 3334 3.36; 5 x 2000 4.15; 10 x 1000 5.98
@@ -574,7 +574,10 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
         int nb = 2;
         if (const char* e = getenv("RQ_PIPE")) nb = std::max(1, std::min(3, atoi(e)));   // A/B only
         if (b->chunk <= 0) {
-            int64_t nch = (p->R + 16383) / 16384;
+            // two chunks (one per stream) up to 2^17 replicas each: C4's 256k replicas of
+            // the README graph 16 x 16000 -> 2 x 128000: 7.1 -> 9.2 M replicas/s (a
+            // generator launch of 16000 x 3 streams is ~0.7 waves per SIMD)
+            int64_t nch = (p->R + 131071) / 131072;
             if (nb > 1) nch = std::max<int64_t>(2, (nch + 1) & ~(int64_t)1);   // even: both streams busy
             if (const char* e = getenv("RQ_PIPE_CHUNK"))   // A/B only
                 nch = (p->R + std::max<int64_t>(64, atoll(e)) - 1) / std::max<int64_t>(64, atoll(e));

@@ -25,6 +25,7 @@
 // sends the batch to the exact sequential sweep (engine.Graph.run(check=True)).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstdlib>
 
 #include "rq_device.h"
 #include "rq_internal.h"
@@ -430,10 +431,81 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
     }
 }
 
+// A handful of streams (C4 / C2: the README graph's three, ~2100 arrivals per replica):
+// the bucket rounds ran a 64-lane block with 3 lanes walking, so here the merge is a
+// RANKING instead.  A block stages its replica's streams in LDS (coalesced), then every
+// arrival finds its place in the play order at once: its index in its own stream plus,
+// per other stream j', the arrivals of j' that play before it -- those at an earlier
+// time, or at the same time when j' < j (equal times in stream order, as the bucket
+// rounds emit them) -- by binary search in LDS, and is written there.  No equal-time
+// cap; the same (t, stream) sequence.
+template <int NS>
+__global__ __launch_bounds__(256) void rq_merge_rank(MergeArgs a)
+{
+    extern __shared__ double mr_sh[];
+    const int64_t rl = blockIdx.x;
+    const int tid = threadIdx.x;
+    const double* base = a.streams + rl * a.capsum;
+    int len[NS], off[NS];
+    int64_t total = 0;
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+        len[j] = j < a.n_str ? a.slen[(int64_t)j * a.slen_stride + rl] : 0;
+        off[j] = j < a.n_str ? (int)a.st_off[j] : 0;
+        total += len[j];
+    }
+#pragma unroll
+    for (int j = 0; j < NS; ++j)
+        for (int i = tid; i < len[j]; i += blockDim.x) mr_sh[off[j] + i] = base[off[j] + i];
+    __syncthreads();
+    double* ot = a.out_t + rl * a.mrg_stride;
+    uint16_t* oj = a.out_j + rl * a.mrg_stride;
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+        for (int i = tid; i < len[j]; i += blockDim.x) {
+            const double t = mr_sh[off[j] + i];
+            int64_t r = i;
+#pragma unroll
+            for (int q = 0; q < NS; ++q) {
+                if (q == j || len[q] == 0) continue;
+                // arrivals of stream q before t: t' < t, or t' <= t for q < j
+                const double* v = mr_sh + off[q];
+                int lo = 0, hi = len[q];
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    const double x = v[mid];
+                    if (x < t || (q < j && x == t)) lo = mid + 1;
+                    else hi = mid;
+                }
+                r += lo;
+            }
+            if (r < a.mrg_stride) {
+                __builtin_nontemporal_store(t, &ot[r]);
+                __builtin_nontemporal_store((uint16_t)j, &oj[r]);
+            }
+        }
+    }
+    if (tid == 0) {
+        a.out_len[rl] = (int)(total < a.mrg_stride ? total : a.mrg_stride);
+        if (total > a.mrg_stride) atomicOr(&a.status[a.chunk0 + rl], RQ_ST_STREAM_OVERFLOW);
+    }
+}
+
 hipError_t rq_launch_merge(const MergeArgs& a, hipStream_t s)
 {
     if (a.n_chunk <= 0) return hipSuccess;
     if (a.n_str > RQ_MG_B) return hipErrorInvalidValue;
+    const char* e = getenv("RQ_MERGE_SMALL");   // A/B and the bucket merge's own tests only
+    const bool small_on = !e || atoi(e) != 0;
+    // <= 8 streams whose buffers fit a block's LDS: the ranking merge
+    const size_t lds = (size_t)a.capsum * sizeof(double);
+    if (small_on && a.n_str <= 8 && lds <= 64 * 1024) {
+        if (a.n_str <= 4)
+            hipLaunchKernelGGL((rq_merge_rank<4>), dim3((unsigned)a.n_chunk), dim3(256), lds, s, a);
+        else
+            hipLaunchKernelGGL((rq_merge_rank<8>), dim3((unsigned)a.n_chunk), dim3(256), lds, s, a);
+        return hipGetLastError();
+    }
     if (a.n_str <= 64)
         hipLaunchKernelGGL((rq_merge_streams<64, false>), dim3((unsigned)a.n_chunk), dim3(64), 0, s, a);
     else

@@ -86,6 +86,32 @@ def test_merged_poisson_controlled_many_sources():
           g.run("poisson", event_log=True, sweep_mode=6, **kw))
 
 
+@pytest.mark.parametrize("world", ["readme", "eight"])
+def test_small_merge_equals_bucket_merge(world, monkeypatch):
+    """<= 8 streams: one thread merges a replica (rq_merge_small) -- the same merged
+    sequence as the bucket rounds of rq_merge_streams (RQ_MERGE_SMALL=0), event for
+    event, and the engine oracle."""
+    torch, engine, graphs, O = _ctx()
+    so = graphs.readme() if world == "readme" else \
+        graphs.followers_graph(num_followers=40, num_sources=7, degree=3, end_time=30.0,
+                               kinds=("Poisson2", "Hawkes"), world_rate=1.5, alpha=1.5, beta=2.5,
+                               seed=8, network_seed=9)
+    g = _graph(engine, so)
+    kw = dict(q=so["q"], s=so["s"], n_rep=700, ctrl_seed=21, world_seed=21, randomize=True,
+              Ks=(1, 2), event_log=True)
+    assert g.run("opt", plan_only=True, **kw)["sources_per_lane"] == 0   # merged streams
+    a = g.run("opt", **kw)
+    monkeypatch.setenv("RQ_MERGE_SMALL", "0")
+    b = g.run("opt", **kw)
+    monkeypatch.delenv("RQ_MERGE_SMALL")
+    _same(torch, a, b)
+    assert int(a.status.max().item()) == 0
+    from tests.test_gpu_engine import _cmp_replica, _oracle, _world_with_seeds
+    for r in (0, 699):
+        met_o, t_o, s_o = _oracle(O, _world_with_seeds(so, 21 + r), ("opt", 21 + r), (1, 2))
+        _cmp_replica(a, r, met_o, t_o, s_o, (1, 2))
+
+
 def _tie_world(n_at5):
     T = np.sort(np.concatenate([np.full(n_at5, 5.0), np.full(700, 7.25), np.linspace(0.5, 19.5, 301)]))
     return dict(src_id=1, end_time=20.0, s=np.asarray([1.0, 2.0, 0.5]), q=0.7, sink_ids=[10, 11, 12, 13],
@@ -97,12 +123,15 @@ def _tie_world(n_at5):
                            (5, 13), (5, 10)])
 
 
-def test_merged_equal_time_groups():
+@pytest.mark.parametrize("small", ["0", "1"])
+def test_merged_equal_time_groups(small, monkeypatch):
     """Equal-time groups larger than a merge round's buffer share (1500 arrivals at one
     time, 700 at another) on the fast sweeps forced by sweep_mode 5 (legacy kernels:
     merged) and 6 with sweep_mode-1-like RealData handling: the merged order equals the
-    windowed one, TIE flagged."""
+    windowed one.  The bucket merge (RQ_MERGE_SMALL=0) flags TIE; the per-thread merge
+    of a few streams (the default at <= 8) has no equal-time cap."""
     torch, engine, graphs, O = _ctx()
+    monkeypatch.setenv("RQ_MERGE_SMALL", small)
     so = _tie_world(1500)
     g = _graph(engine, so)
     for seed in (1, 2):
@@ -110,7 +139,8 @@ def test_merged_equal_time_groups():
                   event_log=True, check=False)
         b = g.run("opt", q=so["q"], s=so["s"], n_rep=4, ctrl_seed=seed, Ks=(1, 3), sweep_mode=1,
                   event_log=True, check=False)
-        assert int(a.status[0].item()) & 4
+        if small == "0":   # (the sweep flags equal times too: no assertion the other way)
+            assert int(a.status[0].item()) & 4
         # the fused sweep (mode 1) and the merged general sweep (mode 5) play the same events
         for i in range(4):
             ta, sa = a.events(i)
@@ -119,15 +149,20 @@ def test_merged_equal_time_groups():
         assert torch.equal(a.counts, b.counts) and torch.equal(a.metrics, b.metrics)
 
 
-def test_merged_tie_group_beyond_round_capacity():
-    """3000 arrivals at one time: more than one merge round holds.  The merge emits them
-    in rounds and flags RQ_ST_TIE; with check=True the engine reruns the batch on the
-    exact sequential sweep, so the result equals sweep_mode 2 and the oracle."""
+@pytest.mark.parametrize("small", ["0", "1"])
+def test_merged_tie_group_beyond_round_capacity(small, monkeypatch):
+    """3000 arrivals at one time: more than one merge round holds.  The bucket merge
+    (RQ_MERGE_SMALL=0) emits them in rounds and flags RQ_ST_TIE; with check=True the
+    engine reruns the batch on the exact sequential sweep, so the result equals
+    sweep_mode 2 and the oracle.  The per-thread merge of a few streams orders them
+    exactly."""
     torch, engine, graphs, O = _ctx()
+    monkeypatch.setenv("RQ_MERGE_SMALL", small)
     so = _tie_world(3000)
     g = _graph(engine, so)
     a = g.run("opt", q=so["q"], s=so["s"], n_rep=2, ctrl_seed=4, Ks=(1, 2), sweep_mode=5, check=False)
-    assert int(a.status[0].item()) & 4
+    if small == "0":
+        assert int(a.status[0].item()) & 4
     assert int(a.counts[0, 2].item()) > 0
     b = g.run("opt", q=so["q"], s=so["s"], n_rep=2, ctrl_seed=4, Ks=(1, 2), sweep_mode=5)
     c = g.run("opt", q=so["q"], s=so["s"], n_rep=2, ctrl_seed=4, Ks=(1, 2), sweep_mode=2)
