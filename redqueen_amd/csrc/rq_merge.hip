@@ -479,9 +479,12 @@ __global__ __launch_bounds__(256) void rq_merge_rank(MergeArgs a)
                 }
                 r += lo;
             }
+            // plain stores: the inputs are in LDS (nothing to protect in L2), and the
+            // scattered 8-B / 2-B entries of a line merge in L2 before the write-back
+            // (nontemporal stores wrote 2.0 x the 10 B per entry; C4 27.7 -> 25.9 ms)
             if (r < a.mrg_stride) {
-                __builtin_nontemporal_store(t, &ot[r]);
-                __builtin_nontemporal_store((uint16_t)j, &oj[r]);
+                ot[r] = t;
+                oj[r] = (uint16_t)j;
             }
         }
     }
