@@ -161,10 +161,9 @@ struct MergeArgs {
 #ifndef RQ_MRG_LB
 #define RQ_MRG_LB 1024
 #endif
-// wall events per branch-free batch of the merged-stream K = 1 sink-bit sweep (C5 with
-// the repeat-stream skip: 4 -> 6 +1.5 %, 8 -3.7 %, profiles/r04_c5_blb.txt)
+// wall events per branch-free batch of the merged-stream K = 1 sink-bit sweep
 #ifndef RQ_MRG_BLB
-#define RQ_MRG_BLB 6
+#define RQ_MRG_BLB 4
 #endif
 #define RQ_MG_B 512         // merge block: one source per thread (the fast general sweep: <= 512)
 
