@@ -115,6 +115,14 @@ def c5():
                            kinds=("Hawkes",), world_rate=0.5, alpha=1.0, beta=2.0)
 
 
+def c5_small():
+    """C5's bursty regime at C5's own horizon, small enough for the reference to run
+    10k replicas (~2 s each): 4 followers, 4 Hawkes broadcasters (l_0 = 0.5, alpha = 1,
+    beta = 2: stationary rate 1, branching ratio 0.5), degree 2, T = 1000, q = 16."""
+    return followers_graph(num_followers=4, num_sources=4, degree=2, end_time=1000.0,
+                           kinds=("Hawkes",), world_rate=0.5, alpha=1.0, beta=2.0)
+
+
 def g120():
     """A > 64-source world (the general sweep's instances, like C5) small enough for the
     reference to run thousands of replicas: 60 followers, 120 broadcasters (Poisson2

@@ -27,6 +27,10 @@ installed and there is no network) and records, as plain data:
   dist_c3.npz      (--c3-dist N) N-replica RedQueen ensemble on the C3 bench network
   dist_g120.npz    (--g120-dist N) N-replica RedQueen ensemble on graphs.g120 (> 64
                    sources: the general sweep's instances)
+  dist_c5s.npz     (--c5s-dist N) RedQueen ensemble on graphs.c5_small: C5's bursty
+                   Hawkes (l_0 0.5, alpha 1, beta 2) at T = 1000 on 4 followers
+  dist_hawkes0.npz (--hawkes-seed0) the 10k-replica Hawkes world draw at seed0 0 that
+                   round 1 replaced by dist_world's 30k draw (kept to state its z)
   dist_sig.npz     (--sig-dist N) N-replica OptPWSignificance ensemble (K3 network,
                    24-segment follower significance, randomized worlds)
   realdata.npz     all-RealData worlds (create_manager_with_times): the reference's whole
@@ -746,6 +750,42 @@ def gen_c4_dist(n, start=0, procs=0):
     os.replace(tmp, path)
 
 
+C5S_SEED_STRIDE = 1000     # > 99 x the 4 broadcasters: no shared streams
+C5S_OPT_SEED_OFFSET = 900  # the controller's RandomState differs from every wall source's
+
+
+def _c5s_worker(r):
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from redqueen_amd import graphs as G
+    so = SimOpts(**G.c5_small())
+    u = C5S_SEED_STRIDE * r
+    m = so.randomize_other_sources(u).create_manager_with_opt(seed=u + C5S_OPT_SEED_OFFSET)
+    m.run_dynamic()
+    df = m.state.get_dataframe()
+    met, own, world = metrics(df, so)
+    return np.concatenate([[own, world, m.state.get_num_events()], met])
+
+
+def gen_c5s_dist(n, start=0, procs=0):
+    """graphs.c5_small (C5's Hawkes l_0 0.5 / alpha 1 / beta 2 at T = 1000 on 4 followers)
+    through the reference itself: replica r runs world randomize_other_sources(1000 r) and
+    RedQueen seed 1000 r + 900.  start > 0 appends to dist_c5s.npz (which must hold exactly
+    start rows)."""
+    path = os.path.join(HERE, "dist_c5s.npz")
+    with mp.Pool(procs or os.cpu_count()) as pool:
+        res = np.asarray(pool.map(_c5s_worker, range(start, start + n), chunksize=4))
+    if start:
+        old = np.load(path)["data"]
+        assert old.shape[0] == start, (old.shape, start)
+        res = np.concatenate([old, res])
+    cols = ["posts", "world", "events"] + ["top%d" % k for k in KS] + ["avg", "r2"]
+    tmp = path + ".tmp.npz"
+    np.savez_compressed(tmp, data=res, cols=np.asarray(cols),
+                        seed_stride=np.asarray([C5S_SEED_STRIDE]),
+                        opt_seed_offset=np.asarray([C5S_OPT_SEED_OFFSET]))
+    os.replace(tmp, path)
+
+
 G120_SEED_STRIDE = 20000   # > 99 x the broadcaster count: no shared streams
 
 
@@ -841,6 +881,17 @@ def gen_dist(n, worlds=True):
 WORLD_SAMPLES = {"hawkes": (30000, 3_000_000), "pwconst": (10000, 0)}
 
 
+def gen_hawkes_seed0(procs=0):
+    """The 10k-replica Hawkes world draw at seed0 0 that round 1 replaced by the 30k draw
+    at seed0 3e6 (WORLD_SAMPLES): regenerated so the test can state its z under the
+    cluster-robust variance (dist_hawkes0.npz, same columns as dist_world's hawkes)."""
+    with mp.Pool(procs or os.cpu_count()) as pool:
+        res = np.asarray(pool.map(_world_worker, [("hawkes", r) for r in range(10000)],
+                                  chunksize=16)).astype(np.float32)
+    np.savez_compressed(os.path.join(HERE, "dist_hawkes0.npz"), hawkes=res,
+                        hawkes_seed0=np.asarray([0]))
+
+
 def gen_worlds(n=0):
     rec = {}
     for name in WORLDS:
@@ -867,6 +918,10 @@ if __name__ == "__main__":
     ap.add_argument("--g120-dist", type=int, default=0, help="only dist_g120.npz with N replicas")
     ap.add_argument("--c4-dist", type=int, default=0, help="only dist_c4.npz: N more replicas")
     ap.add_argument("--c4-start", type=int, default=0, help="append to dist_c4.npz from here")
+    ap.add_argument("--c5s-dist", type=int, default=0, help="only dist_c5s.npz: N more replicas")
+    ap.add_argument("--c5s-start", type=int, default=0, help="append to dist_c5s.npz from here")
+    ap.add_argument("--hawkes-seed0", action="store_true",
+                    help="only dist_hawkes0.npz: the discarded 10k seed0-0 Hawkes world draw")
     a = ap.parse_args()
     steps = {"npsum": gen_npsum, "draws": gen_draws, "readme": gen_readme, "kats": gen_kats,
              "adv": gen_adversarial, "graphs": gen_graphs, "frac": gen_frac,
@@ -875,6 +930,14 @@ if __name__ == "__main__":
     if a.c4_dist:
         gen_c4_dist(a.c4_dist, a.c4_start, a.procs)
         print("done c4 dist", flush=True)
+        a.worlds = True   # nothing else
+    elif a.c5s_dist:
+        gen_c5s_dist(a.c5s_dist, a.c5s_start, a.procs)
+        print("done c5s dist", flush=True)
+        a.worlds = True   # nothing else
+    elif a.hawkes_seed0:
+        gen_hawkes_seed0(a.procs)
+        print("done hawkes seed0", flush=True)
         a.worlds = True   # nothing else
     elif a.g120_dist:
         gen_g120_dist(a.g120_dist, a.procs)

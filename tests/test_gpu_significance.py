@@ -1,11 +1,10 @@
 """OptPWSignificance on the GPU (controller of every sweep variant) against the CPU
 engine oracle bit for bit, the facade's create_manager_with_significance, the
 batched grid, and the reference's 8k-replica ensemble (99% CI)."""
-import math
-
 import numpy as np
 import pytest
 
+import ensemble as E
 from tests.test_gpu_engine import MODES, _cmp_replica, _ctx, _graph, _mode_kw, _world_with_seeds
 from tests.test_significance_cpu import KAT_BASE, KS
 
@@ -98,10 +97,9 @@ def test_ensemble_vs_reference(golden):
            "events": out.events.values, "avg": out.avg_rank.values, "r2": out.r_2.values}
     for k in KS:
         eng["top%d" % k] = out["top_%d" % k].values
-    for k, v in eng.items():
-        r = ref[k]
-        z = (v.mean() - r.mean()) / math.sqrt(v.var() / len(v) + r.var() / len(r))
-        assert abs(z) < 2.576, (k, r.mean(), v.mean(), z)
+    # replica r: world randomize_other_sources(r), seeds r and r + 99 (clusters r mod 99)
+    ind = E.independent_rows(n, 2)
+    E.compare("gpu_sig", eng, ref, clusters=99, indep_eng=ind, indep_ref=ind, z_bound=2.576)
 
 
 def _err_worlds():

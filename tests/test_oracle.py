@@ -8,6 +8,7 @@ import math
 import numpy as np
 import pytest
 
+import ensemble as E
 from oracle import oracle as O
 from redqueen_amd import graphs
 
@@ -189,10 +190,9 @@ def test_engine_semantics_match_reference_distribution(golden):
     for i, k in enumerate(KS):
         eng["poi_top%d" % k] = out2[:, i]
     eng["poi_avg"], eng["poi_r2"] = out2[:, len(KS)], out2[:, len(KS) + 1]
-    for k, v in eng.items():
-        r = ref[k]
-        z = (v.mean() - r.mean()) / math.sqrt(v.var() / len(v) + r.var() / len(r))
-        assert abs(z) < 2.576, (k, r.mean(), v.mean(), z)
+    # replica r: world randomize_other_sources(r) -> seeds r, r + 99 (clusters r mod 99)
+    ind = E.independent_rows(n, 2)
+    E.compare("oracle_c2", eng, ref, clusters=99, indep_eng=ind, indep_ref=ind, z_bound=2.576)
 
 
 def test_engine_world_distributions(golden):
@@ -212,22 +212,51 @@ def test_engine_world_distributions(golden):
                                        ("Poisson2", {"src_id": 4, "seed": 0, "rate": 2.5})],
                         edge_list=[(2, 1), (3, 2), (4, 1), (4, 2)]),
     }
-    def cvar(x):
-        # cluster-robust variance of the mean: randomize_other_sources(u) gives source k
-        # seed u + 99 k, so replicas r and r + 99 share streams (clusters r mod 99)
-        x = np.asarray(x, np.float64)
-        sums = np.bincount(np.arange(len(x)) % 99, x - x.mean())
-        return float((sums ** 2).sum()) / len(x) ** 2
-
+    # randomize_other_sources(u) gives source k seed u + 99 k, so replicas r and r + 99
+    # share streams: the means use the cluster-robust variance (clusters r mod 99), the
+    # spread / shape tests the rows that share no stream (E.independent_rows)
     for name, so in worlds.items():
         ref = d[name].astype(np.float64)
         ns = len(so["other_sources"])
         out, cnt, _ = O.engine_batch(O.Scenario(so, ("wall",)), 40000, 0, True, KS, 8)
-        r_world = ref[:, :ns].sum(1)
-        for v, r, lab in [(cnt[:, 1], r_world, "world")] + \
-                [(out[:, i], ref[:, ns + i], "m%d" % i) for i in range(len(KS) + 2)]:
-            z = (v.mean() - r.mean()) / math.sqrt(cvar(v) + cvar(r) + 1e-300)
-            assert abs(z) < 2.576, (name, lab, r.mean(), v.mean(), z)
+        eng = {"world": cnt[:, 1]}
+        rr = {"world": ref[:, :ns].sum(1)}
+        for i in range(len(KS) + 2):
+            eng["m%d" % i], rr["m%d" % i] = out[:, i], ref[:, ns + i]
+        E.compare("oracle_world_" + name, eng, rr, clusters=99,
+                  indep_eng=E.independent_rows(len(out), ns),
+                  indep_ref=E.independent_rows(len(ref), ns), z_bound=2.576)
+
+
+def test_discarded_hawkes_draw_under_cluster_variance(golden):
+    """Round 1 replaced the reference's 10k-replica Hawkes world draw at seed0 0 by a 30k
+    draw at seed0 3e6 after its top-5 mean sat ~3 naive sd off the engine's.  That draw
+    (regenerated: dist_hawkes0.npz) shares streams between replicas r and r + 99; under
+    the cluster-robust variance of the mean its worst z is -2.53, inside the 99 % band
+    per statistic, and every spread / shape test passes family-wise.  The two reference
+    draws differ from EACH OTHER by up to |z| 2.65 on the same statistics."""
+    d = golden("dist_hawkes0.npz")
+    ref = d["hawkes"].astype(np.float64)
+    w = golden("dist_world.npz")["hawkes"].astype(np.float64)
+    so = dict(src_id=1, end_time=50.0, s=1.0, q=1.0, sink_ids=[1, 2],
+              other_sources=[("Hawkes", {"src_id": 2, "seed": 0, "l_0": 2.0, "alpha": 1.0,
+                                         "beta": 2.0}),
+                             ("Hawkes", {"src_id": 3, "seed": 0, "l_0": 5.0, "alpha": 2.0,
+                                         "beta": 10.0})],
+              edge_list=[(2, 1), (3, 1), (3, 2)])
+    out, cnt, _ = O.engine_batch(O.Scenario(so, ("wall",)), 40000, 0, True, KS, 8)
+    eng, rr, ww = {"world": cnt[:, 1]}, {"world": ref[:, :2].sum(1)}, {"world": w[:, :2].sum(1)}
+    for i in range(len(KS) + 2):
+        eng["m%d" % i], rr["m%d" % i], ww["m%d" % i] = out[:, i], ref[:, 2 + i], w[:, 2 + i]
+    rec = E.compare("oracle_world_hawkes_seed0", eng, rr, clusters=99, z_bound=2.576,
+                    indep_eng=E.independent_rows(len(out), 2),
+                    indep_ref=E.independent_rows(len(ref), 2))
+    assert 2.4 < rec["max_abs_z"] < 2.576
+    # reference vs reference: the same statistics, the same cluster-robust z
+    rr_ = E.compare("reference_hawkes_seed0_vs_3e6", rr, ww, clusters=99,
+                    indep_eng=E.independent_rows(len(ref), 2),
+                    indep_ref=E.independent_rows(len(w), 2))
+    assert rr_["max_abs_z"] > 2.0
 
 
 def test_engine_is_deterministic_and_seed_sensitive():
@@ -251,10 +280,7 @@ def test_engine_c3_matches_reference_distribution(golden):
                                  seed_stride=int(d["seed_stride"][0]))
     eng = {"posts": cnt[:, 0], "world": cnt[:, 1], "events": cnt[:, 2], "top1": out[:, 0],
            "avg": out[:, 1]}
-    for k, v in eng.items():
-        r = ref[k]
-        z = (v.mean() - r.mean()) / math.sqrt(v.var() / len(v) + r.var() / len(r))
-        assert abs(z) < 2.576, (k, r.mean(), v.mean(), z)
+    E.compare("oracle_c3", eng, ref, z_bound=2.576)
 
 
 def test_engine_g120_matches_reference_distribution(golden):
@@ -270,10 +296,7 @@ def test_engine_g120_matches_reference_distribution(golden):
            "r2": out[:, len(KS) + 1]}
     for i, k in enumerate(KS):
         eng["top%d" % k] = out[:, i]
-    for k, v in eng.items():
-        r = ref[k]
-        z = (v.mean() - r.mean()) / math.sqrt(v.var() / len(v) + r.var() / len(r))
-        assert abs(z) < 2.576, (k, r.mean(), v.mean(), z)
+    E.compare("oracle_g120", eng, ref, z_bound=2.576)
 
 
 def test_realdata_worlds_both_restatements_exact(golden):

@@ -4,11 +4,10 @@ notebook's "Testing out significance" cells (opt_broadcast.ipynb:5469, :5569:
 325 / 323 posts, top-1 29.6750640797 / 30.2860675318); the engine semantics
 (Philox draws, thinning at the per-event bound) match the reference's 8k-replica
 ensemble within 99% CIs."""
-import math
-
 import numpy as np
 import pytest
 
+import ensemble as E
 from oracle import oracle as O
 
 KS = [1, 2, 5, 10]
@@ -61,7 +60,6 @@ def test_engine_matches_reference_distribution(golden):
            "avg": out[:, len(KS)], "r2": out[:, len(KS) + 1]}
     for i, k in enumerate(KS):
         eng["top%d" % k] = out[:, i]
-    for k, v in eng.items():
-        r = ref[k]
-        z = (v.mean() - r.mean()) / math.sqrt(v.var() / len(v) + r.var() / len(r))
-        assert abs(z) < 2.576, (k, r.mean(), v.mean(), z)
+    # replica r: world randomize_other_sources(r), seeds r and r + 99 (clusters r mod 99)
+    ind = E.independent_rows(n, 2)
+    E.compare("oracle_sig", eng, ref, clusters=99, indep_eng=ind, indep_ref=ind, z_bound=2.576)
