@@ -21,9 +21,17 @@ import os
 import sys
 import time
 
-import numpy as np
-import torch
-import torch.distributed as dist
+# The engine pipelines a batch's chunks on two HIP streams (rq_run_batch) and an RCCL
+# group adds its own; with HIP's default of 4 hardware queues per process the engine's two
+# streams then share one queue and the pipeline serialises (C3: 2.93 -> 3.42 ms per step
+# with a world-size-1 group, 2.97 ms with 8 queues; profiles/r05_dist_queues.txt).  Set
+# before HIP initialises; gpurun allows up to 32.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -37,6 +45,10 @@ MERGE_B_PER_WALL_EVENT = 18     # rq_merge_streams: read the arrival (8), write 
 SWEEP_B_PER_ROW = 24            # write t f64 + sumR f64 + nvalid u32 + cnt[K=1] u32
 SCAN_B_PER_ROW = 24             # read the same row back
 GEN_B_PER_WALL_EVENT = 8        # write one arrival time
+
+
+def e2e_gbs(events_per_s):
+    return SWEEP_B_PER_ROW * events_per_s / 1e9
 
 
 def workload(name):
@@ -137,14 +149,15 @@ def pmc_traffic(workload, R, plan):
     return None, None, None
 
 
-def make_step(wl, g, so, R, world, rank, dev, Ks, group=None):
+def make_step(wl, g, so, R, world, rank, dev, Ks, group=None, force=False):
     """The bench step of a workload, on this rank: (step(k) -> (this rank's BatchResult,
     ensemble means), replicas per step over all ranks, plan kwargs).
     c2 / c3 / c5: R replicas per GPU with their own seeds, one all-gather of the
     per-replica metric rows (RCCL over xGMI), the ensemble means.
     c4: the 64 q x 4 s grid with R replicas per grid point per GPU -- rank k runs the
     k-th replica window of EVERY grid point (dist.run_sharded), one all-gather, then
-    per-grid-point means in fixed replica order (dist.grid_means)."""
+    per-grid-point means in fixed replica order (dist.grid_means).
+    force: the all-gather runs through the process group even for one rank (--dist)."""
     from redqueen_amd import dist as D
     if wl == "c4":
         from redqueen_amd import graphs
@@ -157,8 +170,9 @@ def make_step(wl, g, so, R, world, rank, dev, Ks, group=None):
 
         def step(k):
             base = k * n_rep
-            m, c, res = D.run_sharded(g, len(grid), n_rep, world, rank, group, ctrl="opt",
-                                      ctrl_seed=base, world_seed=base, check=False, **kw)
+            m, c, res = D.run_sharded(g, len(grid), n_rep, world, rank, group, force,
+                                      ctrl="opt", ctrl_seed=base, world_seed=base, check=False,
+                                      **kw)
             return res, D.grid_means(m, len(grid), n_rep)
         return step, len(grid) * n_rep, dict(kw, n_rep=n_rep, rep_lo=lo, rep_cnt=hi - lo)
 
@@ -167,9 +181,9 @@ def make_step(wl, g, so, R, world, rank, dev, Ks, group=None):
         res = g.run("opt", q=so["q"], s=so["s"], n_rep=R, ctrl_seed=base, world_seed=base,
                     randomize=True, Ks=Ks, check=False)
         m = res.metrics
-        if world > 1:
-            allm = D.gather_rows(m, world * R, world, rank, group)   # RCCL over xGMI: the only exchange
-            m = allm
+        if world > 1 or force:
+            # RCCL over xGMI: the only exchange
+            m = D.gather_rows(m, world * R, world, rank, group, force=force)
         # ensemble means (redqueen_amd.dist.grid_means): identical on every rank
         return res, D.grid_means(m, 1, m.shape[0])[0]
     return step, R * world, dict(q=so["q"], s=so["s"], n_rep=R, randomize=True, Ks=Ks)
@@ -186,6 +200,9 @@ def main():
     ap.add_argument("--workload", default="c3")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=0)
+    ap.add_argument("--dist", action="store_true",
+                    help="at N = 1 too: a world-size-1 RCCL group, the step's all-gather "
+                         "runs through it")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -196,6 +213,10 @@ def main():
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=dev)
+    elif a.dist:   # one rank, no rendezvous: an in-process store
+        dist.init_process_group("nccl", device_id=dev, store=dist.HashStore(), rank=0,
+                                world_size=1)
+    grouped = dist.is_initialized()
 
     from redqueen_amd import engine
     from redqueen_amd import _lib as L
@@ -208,7 +229,8 @@ def main():
     # replicas/s against 15.8k at 4096 (profiles/r04_c5_ab.txt)
     R = a.replicas or {"c5": 8192, "c4": 1000}.get(a.workload, 10000)
     Ks = (1,)
-    step, rep_step, pkw = make_step(a.workload, g, so, R, world, rank, dev, Ks)
+    step, rep_step, pkw = make_step(a.workload, g, so, R, world, rank, dev, Ks,
+                                    force=grouped)
     plan = g.run("opt", plan_only=True, **pkw)
 
     # capacity check once at full size (overflow -> the engine reruns with doubled
@@ -245,7 +267,7 @@ def main():
     torch.cuda.synchronize()
 
     L.lib().rq_timing(1)
-    if world > 1:
+    if grouped:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -255,7 +277,7 @@ def main():
         accumulate(res, acc)
     csum, status, ties = acc
     torch.cuda.synchronize()
-    if world > 1:
+    if grouped:
         dist.barrier()
     el = time.perf_counter() - t0
     ms = np.zeros(5)
@@ -263,13 +285,13 @@ def main():
     L.lib().rq_timing_read(ms.ctypes.data_as(L._pd), nl.ctypes.data_as(L._pi64))
     L.lib().rq_timing(0)
     t = torch.tensor([el], dtype=torch.float64, device=dev)
-    if world > 1:
+    if grouped:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
 
     rows_l, posts_l = int(csum[3].item()), int(csum[0].item())   # this rank
     tot = csum.clone()
-    if world > 1:   # reporting only, after the timed region
+    if grouped:   # reporting only, after the timed region
         dist.all_reduce(tot)
     local_ev = int(tot[2].item())   # events of all ranks
     replicas = rep_step * a.steps
@@ -363,11 +385,17 @@ def main():
             "scan_gbs": scan_gbs,
             "gen_gbs": gen_gbs,
             "merge_gbs": merge_gbs,
+            # SURVEY 8(d)'s end-to-end figure: 24 B per simulated event (one pivot row
+            # written and read back) at the whole job's event rate
+            "roofline_e2e": {"bytes_per_event": SWEEP_B_PER_ROW, "achieved": e2e_gbs(ev_rate),
+                             "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": e2e_gbs(ev_rate) / HBM_PEAK_GBS / world},
+            "exchange": ("RCCL all-gather (process group of %d)" % world) if grouped else None,
             "cpu_baseline": cpu,
             "cpu_baseline_reference": ref_cpu_baseline(a.workload),
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if grouped:
         dist.destroy_process_group()
 
 

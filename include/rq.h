@@ -63,7 +63,7 @@
 extern "C" {
 #endif
 
-#define RQ_ABI_VERSION 4
+#define RQ_ABI_VERSION 5
 #define RQ_MAX_K 4 /* at most 4 K values (perf_opts.Ks, opt_runs.py:31-38) per run */
 
 typedef enum {
@@ -121,6 +121,11 @@ typedef struct rq_graph* rq_graph_t;
 /* status bits written per replica into rq_outputs.status */
 #define RQ_ST_ROWS_OVERFLOW 1    /* metric-row / event-log capacity exceeded: rerun with larger cap_scale */
 #define RQ_ST_STREAM_OVERFLOW 2  /* a source's arrival stream exceeded its capacity: rerun      */
+/* A replica flagged with either overflow bit ran TRUNCATED: its metrics and counts cover
+   only the events that fit and are not the reference's.  Every other replica of the batch
+   is exact.  The library never reruns by itself: the Python Graph.run(check=True) reruns
+   the batch with doubled cap_scale (and remembers the scale for the graph's later runs);
+   check=False hands the flagged rows back as they are, for the caller to mask or rerun. */
 #define RQ_ST_TIE 4              /* events at equal times shared a pivot row.  Exact (pivot cells
                                     averaged like pandas) in the sequential sweep -- max_events,
                                     sweep_mode 2, or any RealData stream; the fast
@@ -153,7 +158,7 @@ typedef struct rq_batch_desc {
     double cap_scale;            /* >= 1: multiplies every auto-sized capacity                   */
     int64_t chunk;               /* replicas per launch (0 = library default: the batch in an   */
                                  /* even number of chunks of <= 131072, pipelined on two streams */
-                                 /* within a 200 GiB workspace budget)                          */
+                                 /* within the workspace budget, ws_budget below)               */
     int64_t replica0;            /* this call runs global replicas [replica0, replica0+n_local):  */
     int64_t n_local;             /* a shard of the grid (0 = all n_grid*n_rep); outputs are      */
                                  /* indexed locally, seeds and grid point use the global id     */
@@ -200,6 +205,16 @@ typedef struct rq_batch_desc {
        rep_cnt = 0: the whole grid (rep_lo = 0, rep_cnt = n_rep). */
     int64_t rep_lo;
     int64_t rep_cnt;
+    /* Device-memory budget of the workspace (ABI v5), bytes.  With the library's chunking
+       (chunk = 0) the plan takes smaller chunks (an even count when pipelined) until the
+       buffer sets in flight fit it; RQ_ENOMEM when one replica does not.  0: the library's
+       default -- rq_workspace_size / rq_plan_info / rq_event_capacity take 0.9 x the
+       device's free memory (hipMemGetInfo), rq_run_batch the workspace_bytes it is handed
+       (so a workspace sized by rq_workspace_size always fits; the chunking, never the
+       results, may differ).  A caller that frees or reuses memory of its own (a caching
+       allocator) passes its reclaimable total here so both calls plan alike.  The
+       environment variable RQ_WS_BUDGET_GB caps either. */
+    int64_t ws_budget;
 } rq_batch_desc;
 #define RQ_MAX_RD 64
 

@@ -17,7 +17,7 @@ RQ_OK, RQ_EINVAL, RQ_EOVERFLOW, RQ_EHIP, RQ_ENOMEM, RQ_EUNSORTED, RQ_EUNSUPPORTE
 SRC_NONE, SRC_POISSON, SRC_POISSON2, SRC_HAWKES, SRC_PWCONST, SRC_REALDATA, SRC_OPT, SRC_OPTPW = range(8)
 ST_ROWS_OVERFLOW, ST_STREAM_OVERFLOW, ST_TIE, ST_EMPTY = 1, 2, 4, 8
 RUN_EVENT_LOG = 1
-ABI_VERSION = 4
+ABI_VERSION = 5
 REPLAY_LARGE = 1
 REPLAY_CHUNKED = 2
 REPLAY_CHUNK_ROWS = 4096   # RC_L: rows per workgroup of the chunked replay
@@ -55,7 +55,8 @@ class BatchDesc(C.Structure):
                 ("replica0", C.c_int64), ("n_local", C.c_int64), ("sweep_mode", C.c_int32),
                 ("n_seg", C.c_int32), ("period", C.c_double), ("s_pw", _pd),
                 ("n_rd", C.c_int32), ("rd_src_id", _pi64), ("rd_cap", _pi64), ("rd_times", _P),
-                ("rd_off", _P), ("rep_lo", C.c_int64), ("rep_cnt", C.c_int64)]
+                ("rd_off", _P), ("rep_lo", C.c_int64), ("rep_cnt", C.c_int64),
+                ("ws_budget", C.c_int64)]
 
 
 class Outputs(C.Structure):

@@ -265,7 +265,24 @@ double stream_mean_var(const rq_graph* g, int j, int kind, const rq_batch_desc* 
     return m;
 }
 
-int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
+// the buffer layout of one chunk plan (p->chunk, p->nbuf): offsets and p->total
+void plan_layout(const rq_graph* g, const rq_batch_desc* b, Plan* p);
+
+// device-memory budget of a plan's workspace: the caller's (rq_batch_desc.ws_budget),
+// else `fallback` (rq_run_batch: the workspace it was handed) or, with none, 0.9 x the
+// device's free memory; RQ_WS_BUDGET_GB caps it
+double ws_budget(const rq_batch_desc* b, double fallback)
+{
+    double bud = b && b->ws_budget > 0 ? (double)b->ws_budget : fallback;
+    if (!(bud > 0.0)) {
+        size_t fr = 0, tot = 0;
+        bud = hipMemGetInfo(&fr, &tot) == hipSuccess ? 0.9 * (double)fr : 200.0 * (1 << 30);
+    }
+    if (const char* e = getenv("RQ_WS_BUDGET_GB")) bud = std::min(bud, atof(e) * (1 << 30));
+    return bud;
+}
+
+int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p, double budget)
 {
     if (!g || !b) return RQ_EINVAL;
     if (b->nK < 1 || b->nK > RQ_MAX_K || !b->Ks) return RQ_EINVAL;
@@ -402,6 +419,11 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     p->mrg = !p->log && b->sweep_mode != 6;
     p->n_grp = g->n_str > RQ_MG_B ? (g->n_str + RQ_MG_B - 1) / RQ_MG_B : 1;
     if (const char* e = getenv("RQ_MRG")) p->mrg = p->mrg && atoi(e) != 0;   // A/B only
+    // without the merged streams the windowed sweep owns <= 8 sources per lane
+    if (!p->mrg && !p->log && g->n_str > 512) {
+        p->log = true;
+        goto replan;
+    }
 
     // general sweep: pick (ring depth W, waves per block) for the most waves per CU
     {
@@ -584,23 +606,23 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
             nch = std::max<int64_t>(1, std::min(nch, p->R));
             p->chunk = (p->R + nch - 1) / nch;
         }
-        int64_t nch = (p->R + p->chunk - 1) / p->chunk;
+        const int64_t nch = (p->R + p->chunk - 1) / p->chunk;
         p->nbuf = (int)std::min<int64_t>(nb, nch);
-        // device-memory budget of the buffer sets in flight (C5: ~47 MB per replica):
-        // smaller chunks (an even count) until nbuf of them fit
-        if (p->nbuf > 1 && b->chunk <= 0) {
-            double budget = 200.0 * (1 << 30);
-            if (const char* e = getenv("RQ_WS_BUDGET_GB")) budget = atof(e) * (1 << 30);   // tuning only
-            const double rows_b = (double)p->cap_rows * (20.0 + 4.0 * p->nK);
-            const double per_rep = std::max(8.0 * (double)p->capsum, rows_b) + 4.0 * g->n_str +
-                                   10.0 * (double)p->mrg_stride + 16.0 +
-                                   (p->n_grp > 1 ? 10.0 * (double)p->capsum + 512.0 * p->n_grp : 0.0);
-            const int64_t fit = std::max<int64_t>(1, (int64_t)(budget / (p->nbuf * per_rep)));
-            if (p->chunk > fit) {
-                nch = (p->R + fit - 1) / fit;
-                nch = (nch + 1) & ~(int64_t)1;
-                p->chunk = (p->R + nch - 1) / nch;
-            }
+    }
+
+    // the workspace within the device-memory budget (C5: ~20 MB per replica in flight):
+    // with the library's chunking, smaller chunks (an even count when pipelined) until the
+    // nbuf buffer sets in flight fit; a caller-fixed chunk is the caller's business
+    plan_layout(g, b, p);
+    if (b->chunk <= 0 && budget > 0.0) {
+        while ((double)p->total > budget) {
+            if (p->chunk <= 1) return RQ_ENOMEM;
+            int64_t c = (int64_t)((double)p->chunk * budget / (double)p->total * 0.97);
+            c = std::max<int64_t>(1, std::min<int64_t>(c, p->chunk - 1));
+            int64_t nch = (p->R + c - 1) / c;
+            if (p->nbuf > 1) nch = (nch + 1) & ~(int64_t)1;
+            p->chunk = (p->R + nch - 1) / nch;
+            plan_layout(g, b, p);
         }
     }
 
@@ -608,9 +630,18 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     // out (a chunk larger than the resident wave slots): measured neutral on C3 (3.01 vs
     // 3.02 ms per step) and slower on C5 (8192 replicas in one chunk: sweep 424 ms against
     // 400 ms in index order, profiles/r04_c5_ab.txt) -- off unless RQ_ORDER=1 (A/B)
-    if (const char* e = getenv("RQ_ORDER"))
-        p->order = atoi(e) != 0 && p->mrg && !p->log && p->chunk > (int64_t)std::max(1, p->wpc) * rq_cu_count();
+    if (const char* e = getenv("RQ_ORDER")) {
+        p->order = atoi(e) != 0 && p->mrg && !p->log && p->chunk > (int64_t)std::max(1, p->wpc) * rq_cu_count() &&
+                   p->chunk <= 65536;   // rq_order_replicas sorts <= 65536 replicas per launch
+        if (p->order) plan_layout(g, b, p);
+    }
+    return RQ_OK;
+}
 
+void plan_layout(const rq_graph* g, const rq_batch_desc* b, Plan* p)
+{
+    // the sequential sweep's global per-sink slots: no more than the chunk's replicas
+    if (p->gs) p->gs_slots = std::min<int64_t>(p->gs_slots, (int64_t)align_up((size_t)p->chunk, (size_t)p->gwpb));
     const size_t A = 256;
     const int64_t C = p->chunk;
     size_t o = 0;
@@ -669,7 +700,6 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     p->gs_stride = p->gs ? (int64_t)align_up(16 * (size_t)p->n_sinks_pad, A) : 0;
     p->off_gs = o;      o = align_up(o + (size_t)(p->gs ? p->gs_slots : 0) * p->gs_stride, A);
     p->total = o;
-    return RQ_OK;
 }
 
 }  // namespace
@@ -914,7 +944,7 @@ int rq_workspace_size(rq_graph_t g, const rq_batch_desc* b, size_t* bytes)
 {
     if (!bytes) return RQ_EINVAL;
     Plan p;
-    const int rc = make_plan(g, b, &p);
+    const int rc = make_plan(g, b, &p, ws_budget(b, 0.0));
     if (rc) return rc;
     *bytes = p.total;
     return RQ_OK;
@@ -924,7 +954,7 @@ int rq_plan_info(rq_graph_t g, const rq_batch_desc* b, int64_t* info)
 {
     if (!info) return RQ_EINVAL;
     Plan p;
-    const int rc = make_plan(g, b, &p);
+    const int rc = make_plan(g, b, &p, ws_budget(b, 0.0));
     if (rc) return rc;
     info[0] = (p.log ? (p.gs ? 4 : 1) : (p.bits ? 2 : (p.bl ? 3 : 0))) + (p.fwm ? 20 : p.fw ? 10 : 0);
     info[1] = p.mrg ? 0 : p.spl;   // 0: merged streams (lanes own no sources)
@@ -944,7 +974,7 @@ int rq_event_capacity(rq_graph_t g, const rq_batch_desc* b, int64_t* cap)
 {
     if (!cap) return RQ_EINVAL;
     Plan p;
-    const int rc = make_plan(g, b, &p);
+    const int rc = make_plan(g, b, &p, ws_budget(b, 0.0));
     if (rc) return rc;
     *cap = p.cap_rows;
     return RQ_OK;
@@ -954,7 +984,9 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
                  size_t workspace_bytes, void* hip_stream)
 {
     Plan p;
-    int rc = make_plan(g, b, &p);
+    // the same plan as rq_workspace_size gave when the caller fixes the budget; else the
+    // chunks that fit the workspace handed over
+    int rc = make_plan(g, b, &p, ws_budget(b, (double)workspace_bytes));
     if (rc) return rc;
     if (!out || !out->metrics || !out->counts || !out->status || !workspace) return RQ_EINVAL;
     if (workspace_bytes < p.total) return RQ_EINVAL;
@@ -1050,11 +1082,31 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
     // side streams, forked after the tables / status above and joined before returning)
     // with buffer set k % nbuf, so a set is reused only in its own stream's order
     hipStream_t pst[3] = {s, nullptr, nullptr};
+    // the join of the side streams on EVERY exit: an error return inside the chunk loop
+    // must not leave work queued on a side stream that writes the caller's buffers after
+    // the caller's stream has moved on (the caller frees them when the call fails)
+    struct Join {
+        hipStream_t* pst;
+        int n = 1;
+        int done()
+        {
+            int rc = RQ_OK;
+            for (int k = 1; k < n; ++k)
+                if (hipEventRecord(t_pipe.join[k - 1], pst[k]) != hipSuccess ||
+                    hipStreamWaitEvent(pst[0], t_pipe.join[k - 1], 0) != hipSuccess)
+                    rc = RQ_EHIP;
+            n = 1;
+            return rc;
+        }
+        ~Join() { (void)done(); }
+    } join{pst};
     if (p.nbuf > 1) {
         if ((rc = t_pipe.get(p.nbuf - 1, pst + 1)) != RQ_OK) return rc;
         if (hipEventRecord(t_pipe.fork, s) != hipSuccess) return RQ_EHIP;
-        for (int k = 1; k < p.nbuf; ++k)
+        for (int k = 1; k < p.nbuf; ++k) {
             if (hipStreamWaitEvent(pst[k], t_pipe.fork, 0) != hipSuccess) return RQ_EHIP;
+            join.n = k + 1;
+        }
     }
     int64_t ci = 0;
     for (int64_t c0 = 0; c0 < p.R; c0 += p.chunk, ++ci) {
@@ -1295,11 +1347,7 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             if (rq_launch_scan(sc, p.nK, s) != hipSuccess) return RQ_EHIP;
         }
     }
-    for (int k = 1; k < p.nbuf; ++k)   // join: the caller's stream waits for every side stream
-        if (hipEventRecord(t_pipe.join[k - 1], pst[k]) != hipSuccess ||
-            hipStreamWaitEvent(pst[0], t_pipe.join[k - 1], 0) != hipSuccess)
-            return RQ_EHIP;
-    return RQ_OK;
+    return join.done();   // the caller's stream waits for every side stream
 }
 
 int rq_timing(int enable)

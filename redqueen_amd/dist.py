@@ -49,11 +49,13 @@ def _all_gather_padded(local, m, world, group):
     return out
 
 
-def gather_rows(local, n_total, world=None, rank=None, group=None):
+def gather_rows(local, n_total, world=None, rank=None, group=None, force=False):
     """All-gather per-replica rows [n_local, C] of every rank into [n_total, C]
-    in global replica order (ranks own contiguous, possibly unequal, shards)."""
+    in global replica order (ranks own contiguous, possibly unequal, shards).
+    ``force``: run the collective even for a world of one (bench.py --dist, the
+    world-size-1 RCCL test) instead of returning ``local``."""
     world, rank = _world_rank(world, rank, group)
-    if world == 1:
+    if world == 1 and not force:
         return local
     sizes = [shard(n_total, world, r)[1] - shard(n_total, world, r)[0] for r in range(world)]
     m = max(sizes)
@@ -61,12 +63,12 @@ def gather_rows(local, n_total, world=None, rank=None, group=None):
     return torch.cat([out[r * m:r * m + sizes[r]] for r in range(world)], 0).to(local.device)
 
 
-def gather_grid_rows(local, n_grid, n_rep, world=None, rank=None, group=None):
+def gather_grid_rows(local, n_grid, n_rep, world=None, rank=None, group=None, force=False):
     """All-gather per-replica rows of grid_shard()s: rank k holds [n_grid * cnt_k, C]
     (grid point major, its replica window minor); returns [n_grid * n_rep, C] in
-    global replica order i = g * n_rep + r."""
+    global replica order i = g * n_rep + r.  ``force`` as in gather_rows."""
     world, rank = _world_rank(world, rank, group)
-    if world == 1:
+    if world == 1 and not force:
         return local
     wins = [grid_shard(n_rep, world, r) for r in range(world)]
     m = n_grid * max(hi - lo for lo, hi in wins)
@@ -88,10 +90,11 @@ def grid_means(rows, n_grid, n_rep):
     return x.sum(1) / torch.full((), float(n_rep), dtype=torch.float64, device=x.device)
 
 
-def run_sharded(graph, n_grid, n_rep, world=None, rank=None, group=None, **run_kw):
+def run_sharded(graph, n_grid, n_rep, world=None, rank=None, group=None, force=False, **run_kw):
     """Run this rank's shard of an (n_grid x n_rep) batch -- the same replica window
     of every grid point -- and return the gathered per-replica metrics
-    [n_grid*n_rep, nK+2] and counts [n_grid*n_rep, 4] (and this rank's BatchResult)."""
+    [n_grid*n_rep, nK+2] and counts [n_grid*n_rep, 4] (and this rank's BatchResult).
+    ``force``: exchange through the collective even for a world of one."""
     world, rank = _world_rank(world, rank, group)
     lo, hi = grid_shard(n_rep, world, rank)
     if hi > lo:
@@ -103,6 +106,6 @@ def run_sharded(graph, n_grid, n_rep, world=None, rank=None, group=None, **run_k
         dev = torch.device("cuda", torch.cuda.current_device())
         lm = torch.empty((0, nk + 2), dtype=torch.float64, device=dev)
         lc = torch.empty((0, 4), dtype=torch.int64, device=dev)
-    m = gather_grid_rows(lm, n_grid, n_rep, world, rank, group)
-    c = gather_grid_rows(lc, n_grid, n_rep, world, rank, group)
+    m = gather_grid_rows(lm, n_grid, n_rep, world, rank, group, force)
+    c = gather_grid_rows(lc, n_grid, n_rep, world, rank, group, force)
     return m, c, res

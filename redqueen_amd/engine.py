@@ -140,6 +140,7 @@ class Graph:
         if self.n_followers:
             L.lib().rq_graph_followers(h, self.followers.ctypes.data_as(L._pi64))
         self._ws = None
+        self._cap_scale = {}   # (controller kind, max_events) -> cap_scale an overflow needed
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -163,8 +164,9 @@ class Graph:
         """Enqueue one batch on ``stream`` (default: the current torch stream).  Every
         tensor the batch reads or writes is allocated with that stream current, so
         the caching allocator, the library and the status check all agree on it.
-        With a dynamic plugin among the sources, the batch's first replica is checked to
-        be self-driven (_verify_dynamic) before the result is returned."""
+        With a dynamic plugin among the sources, the batch's replicas (all of a batch of
+        <= 64, else a seeded sample of 64) are checked to be self-driven (_verify_dynamic)
+        before the result is returned."""
         use = stream or torch.cuda.current_stream()
         with torch.cuda.stream(use):
             res = self._run(*args, stream=use, **kw)
@@ -268,6 +270,7 @@ class Graph:
             b.s_pw = spw.ctypes.data_as(L._pd)
         lib = L.lib()
         if plan_only:
+            b.ws_budget = self._ws_budget(dev)
             info = (C.c_int64 * 8)()
             L.check("rq_plan_info", lib.rq_plan_info(self._h, C.byref(b), info))
             keys = ("variant", "sources_per_lane", "ring_depth", "waves_per_block",
@@ -278,8 +281,12 @@ class Graph:
 
     def _run_loop(self, lib, b, keep, dev, R, Ks, n_grid, n_rep, ck, event_log, gids,
                   check, use):
+        # start from the capacity scale an earlier overflow rerun of this graph needed
+        key = (ck, b.max_events >= 0)
+        b.cap_scale = max(b.cap_scale, self._cap_scale.get(key, 1.0))
         while True:
             nbytes = C.c_size_t()
+            b.ws_budget = self._ws_budget(dev)
             L.check("rq_workspace_size", lib.rq_workspace_size(self._h, C.byref(b), C.byref(nbytes)))
             if self._ws is None or self._ws.numel() < nbytes.value:
                 self._ws = None
@@ -319,6 +326,18 @@ class Graph:
             if b.cap_scale > 64:
                 raise L.RQError("rq_run_batch", L.RQ_EOVERFLOW)
             b.cap_scale = b.cap_scale * 2.0
+            self._cap_scale[key] = max(self._cap_scale.get(key, 1.0), b.cap_scale)
+
+    def _ws_budget(self, dev):
+        """The workspace's device-memory budget (rq_batch_desc.ws_budget): 0.9 x what this
+        process can get -- the device's free memory, torch's cached (reserved, unallocated)
+        blocks and the graph's own workspace, which the next one replaces."""
+        if not torch.cuda.is_available():
+            return 0   # plan queries without a device: the library's default
+        free, _total = torch.cuda.mem_get_info(dev)
+        cached = torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
+        held = self._ws.numel() if self._ws is not None else 0
+        return int(0.9 * (free + cached + held))
 
     def _plugin_streams(self, b, keep, dev, R_all, gids, world_seed, seed_mod):
         """Per-replica times of the registered static broadcasters of a randomized
@@ -362,35 +381,50 @@ class Graph:
         from .opt_model import source_times
         return source_times(inst, self.start_time, self.sink_ids, self._edges, self.end_time)
 
+    VERIFY_ALL = 64   # dynamic-plugin check: every replica of a batch this small, else a sample
+
     def _verify_dynamic(self, args, kw, res):
         """A dynamic plugin is played from its own schedule: check that it is self-driven
-        on the batch's first replica -- rerun that replica with its event log and feed a
-        fresh copy of each dynamic plugin the whole event sequence in play order
-        (opt_model.verify_dynamic_plugin), which raises when its schedule reacts to
-        another source's event."""
+        -- rerun replicas with their event log and feed a fresh copy of each dynamic plugin
+        the whole event sequence in play order (opt_model.verify_dynamic_plugin), which
+        raises when its schedule reacts to another source's event.  Every replica of a
+        batch of <= 64 (one probe batch), else 64 replicas drawn with a seed fixed by the
+        batch (one probe run each): a plugin that reacts only in some replicas is caught
+        whenever one of them is probed.  Cost: one event-logged run of the probed replicas
+        plus a host replay of their events through the plugin (~10-50 ms per replica)."""
         from .opt_model import verify_dynamic_plugin
-        gids = res.global_ids
-        if not len(gids):
+        gids = np.asarray(res.global_ids, dtype=np.int64)
+        R = len(gids)
+        if not R:
             return
-        kw = dict(kw)
-        kw.update(replica0=int(kw.get("replica0", 0)), n_local=1, event_log=True, check=True)
-        probe = self._run(*args, **kw)
-        t_ev, s_ev = probe.events(0)
-        i = int(gids[0])
-        if kw.get("randomize"):
-            ws = kw.get("world_seed", 0)
-            wseed = ws.to(torch.int64).cpu().numpy() if torch.is_tensor(ws) else None
-            make = lambda: self._plugin_instances(i, wseed, ws, int(kw.get("seed_mod", 0)))  # noqa: E731
+        base = dict(kw)
+        r0 = int(base.get("replica0", 0))
+        base.update(event_log=True, check=True)
+        if R <= self.VERIFY_ALL:
+            probes = [(np.arange(R), self._run(*args, **dict(base, replica0=r0, n_local=R)))]
         else:
-            make = lambda: [cls(**kw_) for _idx, cls, kw_, _sid, _dyn in self.plugins]  # noqa: E731
-        for fresh, gen, p in zip(make(), make(), self.plugins):
-            if not p[4]:
-                continue
-            times = self._plugin_source_times(gen)
-            me = kw.get("max_events")
-            verify_dynamic_plugin(fresh, self.start_time, self.sink_ids, self._edges, self.end_time,
-                                  t_ev, s_ev, times,
-                                  max_events=None if me is None or me == float("inf") else int(me))
+            rng = np.random.default_rng([0x52510000, R, int(gids[0])])
+            pick = np.sort(rng.choice(R, self.VERIFY_ALL, replace=False))
+            probes = [(np.asarray([j]), self._run(*args, **dict(base, replica0=r0 + int(j), n_local=1)))
+                      for j in pick]
+        ws = kw.get("world_seed", 0)
+        wseed = ws.to(torch.int64).cpu().numpy() if torch.is_tensor(ws) else None
+        me = kw.get("max_events")
+        me = None if me is None or me == float("inf") else int(me)
+        for idx, probe in probes:
+            for k, j in enumerate(idx):
+                t_ev, s_ev = probe.events(k)
+                i = int(gids[j])
+                if kw.get("randomize"):
+                    make = lambda: self._plugin_instances(i, wseed, ws, int(kw.get("seed_mod", 0)))  # noqa: E731
+                else:
+                    make = lambda: [cls(**kw_) for _idx, cls, kw_, _sid, _dyn in self.plugins]  # noqa: E731
+                for fresh, gen, p in zip(make(), make(), self.plugins):
+                    if not p[4]:
+                        continue
+                    times = self._plugin_source_times(gen)
+                    verify_dynamic_plugin(fresh, self.start_time, self.sink_ids, self._edges,
+                                          self.end_time, t_ev, s_ev, times, max_events=me)
 
     def _plan_variant(self, lib, b):
         info = (C.c_int64 * 8)()

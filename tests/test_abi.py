@@ -28,7 +28,7 @@ def test_exports_every_declared_symbol():
 
 def test_version_and_errors():
     lib = L.lib()
-    assert lib.rq_abi_version() == L.ABI_VERSION == 4
+    assert lib.rq_abi_version() == L.ABI_VERSION == 5
     assert lib.rq_strerror(L.RQ_EINVAL) == b"invalid argument"
     assert lib.rq_strerror(-99) == b"unknown error"
 

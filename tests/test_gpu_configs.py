@@ -180,3 +180,37 @@ def test_c4_grid_sharded():
         (top, avg, r2, cnt), _ = O.engine_metrics(O.Scenario(_world_with_seeds(dd, u), ("opt", u)), (1,))
         row = full.metrics[gi * n_rep].cpu().numpy()
         assert row[0] == top[0] and row[1] == avg and row[2] == r2
+
+
+def test_c5_workspace_within_free_memory():
+    """The workspace is planned against the device memory this process can get
+    (rq_batch_desc.ws_budget = 0.9 x (free + torch's cached blocks + the graph's own
+    workspace)), not a fixed 200 GiB: with all but 6 GiB of the device held
+    through torch, a C5 batch runs in smaller pipelined chunks inside what is left and
+    gives the unconstrained batch's bits."""
+    torch, engine, graphs, O = _ctx()
+    so = graphs.c5()
+    g = _graph(engine, so)
+    kw = dict(q=so["q"], s=so["s"], n_rep=1024, ctrl_seed=21, world_seed=21, randomize=True,
+              Ks=(1,))
+    free_plan = g.run("opt", plan_only=True, **kw)
+    ref = g.run("opt", **kw)
+    assert int(ref.status.max().item()) == 0
+    ref_m, ref_c = ref.metrics.clone(), ref.counts.clone()
+    big = g._ws.numel()
+    assert big > 12 * 2 ** 30, big   # ~20 MB per replica in flight
+    del ref
+    g._ws = None
+    torch.cuda.empty_cache()
+    free, _ = torch.cuda.mem_get_info()
+    hog = torch.empty(free - 6 * 2 ** 30, dtype=torch.uint8, device="cuda")
+    try:
+        plan = g.run("opt", plan_only=True, **kw)
+        assert plan["chunk"] < free_plan["chunk"], (plan, free_plan)
+        res = g.run("opt", **kw)
+        assert g._ws.numel() <= 6 * 2 ** 30
+        assert torch.equal(res.metrics, ref_m) and torch.equal(res.counts, ref_c)
+    finally:
+        del hog
+        g._ws = None
+        torch.cuda.empty_cache()

@@ -131,3 +131,71 @@ def test_bench_step_two_ranks_equals_one():
         for r in (0, 1):
             assert got[r][wl][0] == n
             assert np.array_equal(got[r][wl][1], means.cpu().numpy()), (wl, r)
+
+
+def _rccl_worker(q):
+    """A fresh process: a world-size-1 nccl (= RCCL) group bound to the device before
+    any other GPU work, then every exchange of redqueen_amd.dist on device tensors
+    through it (force=True skips the world == 1 shortcut)."""
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    import torch.distributed as dist
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", device_id=dev, store=dist.HashStore(), rank=0,
+                            world_size=1)
+    assert dist.get_backend() == "nccl"
+    from redqueen_amd import dist as D
+    import bench
+    out = {}
+    x = torch.arange(7 * 3, dtype=torch.float64, device=dev).reshape(7, 3) / 3.0
+    out["x"] = x.cpu().numpy()
+    pad = D._all_gather_padded(x, 9, 1, None)
+    assert pad.is_cuda
+    out["padded"] = pad.cpu().numpy()
+    rows = D.gather_rows(x, 7, force=True)
+    assert rows.is_cuda
+    out["rows"] = rows.cpu().numpy()
+    gr = D.gather_grid_rows(x[:6], 2, 3, force=True)
+    assert gr.is_cuda
+    out["grid_rows"] = gr.cpu().numpy()
+    for name, so, kw, n_grid, n_rep in _cases():
+        m, c, _ = D.run_sharded(_graph(so), n_grid, n_rep, force=True, **kw)
+        out[name] = (m.cpu().numpy(), c.cpu().numpy())
+    for wl, R in (("c4", 6), ("c3", 48)):
+        so, _ = bench.workload(wl)
+        step, n, _ = bench.make_step(wl, _graph(so), so, R, 1, 0, dev, (1,), force=True)
+        _, means = step(1)
+        out["bench_" + wl] = means.cpu().numpy()
+    torch.cuda.synchronize()
+    dist.destroy_process_group()
+    q.put(out)
+
+
+def test_rccl_world_one_exchanges_on_device():
+    """RCCL executes: a child process with a world-size-1 nccl group drives
+    _all_gather_padded, gather_rows, gather_grid_rows, run_sharded and bench's own step
+    through the collective on device tensors; every result equals its input (the
+    exchange of one rank is the identity) and the engine's direct run, bit for bit."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import bench
+    ctx = mp.get_context("spawn")
+    qu = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(qu,))
+    p.start()
+    got = qu.get(timeout=300)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    x = got["x"]
+    assert np.array_equal(got["padded"][:7], x) and not got["padded"][7:].any()
+    assert np.array_equal(got["rows"], x)
+    assert np.array_equal(got["grid_rows"], x[:6])
+    for name, so, kw, n_grid, n_rep in _cases():
+        res = _graph(so).run(n_rep=n_rep, **kw)
+        assert np.array_equal(got[name][0], res.metrics.cpu().numpy()), name
+        assert np.array_equal(got[name][1], res.counts.cpu().numpy()), name
+    dev = torch.device("cuda", 0)
+    for wl, R in (("c4", 6), ("c3", 48)):
+        so, _ = bench.workload(wl)
+        step, n, _ = bench.make_step(wl, _graph(so), so, R, 1, 0, dev, (1,))
+        _, means = step(1)
+        assert np.array_equal(got["bench_" + wl], means.cpu().numpy()), wl

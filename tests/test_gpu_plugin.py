@@ -143,3 +143,47 @@ def test_reactive_dynamic_plugin_refused(golden):
                      w2["end_time"], ctrl_a=ctrl)
     with pytest.raises(NotImplementedError):
         g.run("times", n_rep=4, world_seed=0, randomize=True, Ks=KS)
+
+
+def _rarely_reactive():
+    """Renewal (self-driven) except in the replicas whose seed is listed: there, like
+    KnockedOff, another source's event moves its schedule."""
+    from realdata_worlds import RenewalMixin
+    from redqueen_amd.opt_model import Broadcaster
+
+    class RarelyReactive(RenewalMixin, Broadcaster):
+        REACT = set()
+
+        def __init__(self, src_id, seed, scale=0.6):
+            super().__init__(src_id, seed, scale)
+            self._react = seed in self.REACT
+
+        def get_next_interval(self, event):
+            if self._react and event is not None and event.src_id != self.src_id:
+                return self.get_current_time(event) - self.last_self_event_time + 0.01
+            return super().get_next_interval(event)
+    return RarelyReactive
+
+
+@pytest.mark.parametrize("n_rep,react", [(16, {5}), (640, set(range(7, 640, 10)))])
+def test_dynamic_plugin_verified_beyond_replica_zero(n_rep, react):
+    """A dynamic plugin that reacts to other sources only in a few replicas, none of them
+    replica 0: every replica of a batch of <= 64 is verified, a seeded
+    sample of 64 above that, so the batch raises NotImplementedError instead of
+    returning those replicas played as if self-driven.  The same plugin in a batch of
+    its self-driven replicas only runs."""
+    engine, SimOpts, (w, ctrl, us) = _dyn_setup()
+    RR = _rarely_reactive()
+    RR.REACT = set(react)
+    SimOpts.registerSource("RarelyReactive", RR)
+    w2 = dict(w, other_sources=[("RarelyReactive", {"src_id": 2, "seed": 21, "scale": 0.6})] +
+              w["other_sources"][1:])
+    g = engine.Graph(w2["src_id"], w2["other_sources"], w2["sink_ids"], w2["edge_list"],
+                     w2["end_time"], ctrl_a=ctrl)
+    assert 0 not in react
+    with pytest.raises(NotImplementedError):
+        g.run("times", n_rep=n_rep, world_seed=0, randomize=True, Ks=KS)
+    # replicas 0..4 (seeds 0..4: randomize_other_sources gives source idx 0 seed u) are
+    # self-driven: that shard runs
+    res = g.run("times", n_rep=n_rep, world_seed=0, randomize=True, Ks=KS, replica0=0, n_local=5)
+    assert int((res.status & 3).max().item()) == 0   # no overflow (ties are exact here: RealData)
