@@ -4,7 +4,11 @@
 (:109-126) and ``worker_oracle`` (:129-155) keep their parameter tuples and
 result dicts; each simulation is one GPU run (librq.so) and every metric one
 ``rq_metrics_replay`` pass.  For many seeds at once use ``redqueen_amd.batch``
-(one launch for the whole grid) instead of a process pool.
+(one launch for the whole grid) instead of a process pool.  ``run_inference`` /
+``run_inference_queue`` (:350-440, :560-646) batch the q x seed grid on the GPU; the
+multiple-follower helpers (``make_edge_list``, ``create_phased_pwconst_broadcaster``,
+``trim_sim_opts``, ``prepare_multiple_followers_sim_opts``, :651-795) are host-side
+network builders with the reference's draw order.
 """
 import logging
 
@@ -28,6 +32,25 @@ class _Options:
         d = self._get_dict()
         d.update(kw)
         return _Options(**d)
+
+
+def _optioned(fn):
+    """decorated_options' @optioned('opts'): arguments not passed explicitly are taken
+    from the ``opts`` bundle's fields."""
+    import functools
+    import inspect
+    sig = inspect.signature(fn)
+
+    @functools.wraps(fn)
+    def wrapper(*args, **kwargs):
+        opts = kwargs.pop("opts", None)
+        if opts is not None:
+            bound = sig.bind_partial(*args, **kwargs)
+            for name in sig.parameters:
+                if name not in bound.arguments and hasattr(opts, name):
+                    kwargs[name] = getattr(opts, name)
+        return fn(*args, **kwargs)
+    return wrapper
 
 
 Ks = [1]
@@ -216,6 +239,16 @@ def _opt_poisson_batches(worlds, qs, seeds, num_segments):
     return out
 
 
+def run_inference(N=None, T=None, num_segments=None, sim_opts_gen=None, log_q_high=None,
+                  log_q_low=None, opts=None):
+    """opt_runs.run_inference (opt_runs.py:350-440): the q x seed sweep with, after every
+    RedQueen replica, Poisson and the Oracle at its capacity -- run_inference_queue's
+    legs (the q x seed grid as GPU batches) without its Karimi follow-up, which
+    run_inference has commented out.  Returns Options(df, raw_results, capacities)."""
+    return _run_inference(N, T, num_segments, sim_opts_gen, log_q_high, log_q_low, opts,
+                          kdd=False)
+
+
 def run_inference_queue(N=None, T=None, num_segments=None, sim_opts_gen=None, log_q_high=None,
                         log_q_low=None, num_procs=None, opts=None):
     """opt_runs.run_inference_queue (opt_runs.py:560-646): for every q in
@@ -236,6 +269,11 @@ def run_inference_queue(N=None, T=None, num_segments=None, sim_opts_gen=None, lo
     task that raises (worker_oracle's KeyError when q = 1 already meets the
     capacity, utils.py:271-276) is logged and dropped as the reference's queue does.
     Returns Options(df, raw_results, capacities) with the same fields."""
+    return _run_inference(N, T, num_segments, sim_opts_gen, log_q_high, log_q_low, opts,
+                          kdd=True)
+
+
+def _run_inference(N, T, num_segments, sim_opts_gen, log_q_high, log_q_low, opts, kdd):
     import pandas as pd
     if opts is not None:   # @optioned(option_arg='opts'): explicit arguments win
         d = opts._get_dict() if hasattr(opts, "_get_dict") else dict(opts)
@@ -291,9 +329,10 @@ def run_inference_queue(N=None, T=None, num_segments=None, sim_opts_gen=None, lo
         else:
             raw_results.append(orc)
             results.append(extract_perf_fields(orc))
-        logging.error("Exception while handling: %r", {
-            "type": "Exception", "broadcaster_type": "kdd",
-            "error": NameError("broadcast.opt.optimizer (Karimi et al.) is not vendored")})
+        if kdd:
+            logging.error("Exception while handling: %r", {
+                "type": "Exception", "broadcaster_type": "kdd",
+                "error": NameError("broadcast.opt.optimizer (Karimi et al.) is not vendored")})
     return _Options(df=pd.DataFrame.from_records(results), raw_results=raw_results,
                     capacities=capacities)
 
@@ -342,3 +381,101 @@ def _std_hawkes_gen(seed):
 poisson_inf_opts = simulation_opts.set_new(sim_opts_gen=_std_poisson_gen)
 piecewise_inf_opts = piecewise_sim_opt_factory(opts=simulation_opts)
 hawkes_inf_opts = simulation_opts.set_new(sim_opts_gen=_std_hawkes_gen)
+
+
+# ---------------------------------------------------------------- multiple followers
+# opt_runs.py:651-795: the networks of the multiple-follower experiments (C3 / C5's
+# construction, graphs.followers_graph), built on the host with the reference's draws.
+
+def make_piecewise_const(num_segments):
+    """A piecewise-constant semi-sinusoid of num_segments segments (opt_runs.py:653-657)."""
+    import pandas as pd
+    true_values = np.sin(np.arange(0, np.pi, step=0.001))
+    seg_idx = np.arange(true_values.shape[0]) // (true_values.shape[0] / num_segments)
+    return pd.Series(true_values).groupby(seg_idx).mean().tolist()
+
+
+mk_edge_list_opts = _Options(num_followers=100, num_broadcasters=100, degree=5, seed=42,
+                             follower_id_offset=1000, broadcaster_id_offset=5000)
+
+
+@_optioned
+def make_edge_list(num_followers, num_broadcasters, degree, seed, follower_id_offset=0,
+                   broadcaster_id_offset=0, preferential_attachment=False):
+    """Each follower follows ``degree`` distinct broadcasters drawn by RandomState(seed)
+    (opt_runs.py:663-686; graphs.make_edge_list, pinned by tests/golden/graphs.npz)."""
+    from .graphs import make_edge_list as _mk
+    return _mk(num_followers, num_broadcasters, degree, seed, follower_id_offset,
+               broadcaster_id_offset, preferential_attachment)
+
+
+def create_phased_pwconst_broadcaster(src_id, seed, rel_rates, avg_rate, end_time, phase_shift):
+    """A PiecewiseConst source over num_segments equal segments of [0, end_time), its
+    relative rates rotated by ``phase_shift`` and scaled to average ``avg_rate``
+    (opt_runs.py:689-702)."""
+    num_segments = len(rel_rates)
+    assert int(phase_shift) == phase_shift, "The phase shift cannot be fractional."
+    phase_shift %= num_segments
+    change_times = np.arange(num_segments) * (end_time / num_segments)
+    shifted_rates = np.asarray(rel_rates[phase_shift:] + rel_rates[:phase_shift])
+    actual_rates = shifted_rates * (avg_rate * num_segments) / np.sum(shifted_rates)
+    return ('PiecewiseConst', {'src_id': src_id, 'seed': seed, 'change_times': change_times,
+                               'rates': actual_rates})
+
+
+def trim_sim_opts(sim_opts):
+    """Only the controlled source's followers and the broadcasters reaching them stay;
+    q = (#followers)^2 (opt_runs.py:705-718)."""
+    intended = set(t for s_, t in sim_opts.edge_list if s_ == sim_opts.src_id)
+    new_edges = [(s_, t) for s_, t in sim_opts.edge_list if t in intended]
+    reach = set(s_ for s_, _ in new_edges)
+    return sim_opts.update({
+        'sink_ids': sorted(intended),
+        'edge_list': new_edges,
+        'other_sources': [x for x in sim_opts.other_sources if x[1]['src_id'] in reach],
+        'q': 1.0 * (len(intended) ** 2),
+    })
+
+
+multiple_follower_opts = _Options(seed=42, world_alpha=1.0, world_beta=10.0, world_rate=100.0,
+                                  kind='PiecewiseConst', num_other_broadcasters=1000,
+                                  max_num_followers=500, follower_other_degree=1)
+
+
+@_optioned
+def prepare_multiple_followers_sim_opts(num_followers, num_other_broadcasters, max_num_followers,
+                                        seed, world_rate, world_alpha, world_beta,
+                                        follower_other_degree, kind):
+    """The multiple-follower world (opt_runs.py:725-795): a fixed network over
+    max_num_followers (seed 1024), num_other_broadcasters of one kind (seed + src_id
+    each), the controlled source 1 following num_followers of them drawn by
+    RandomState(seed), trimmed to those followers (trim_sim_opts).  T = 100."""
+    from .opt_model import SimOpts
+    assert num_other_broadcasters >= follower_other_degree, (
+        "There should be more other broadcasters than followers per node.")
+    end_time = 100.0
+    rs = np.random.RandomState(seed)
+    follower_ids = 1000 + np.arange(max_num_followers)
+    b_ids = 5000 + np.arange(num_other_broadcasters)
+    network = make_edge_list(num_followers=max_num_followers, num_broadcasters=num_other_broadcasters,
+                             degree=follower_other_degree, seed=1024, follower_id_offset=1000,
+                             broadcaster_id_offset=5000, opts=mk_edge_list_opts)
+    if kind == 'PiecewiseConst':
+        pcw = make_piecewise_const(24)
+        others = [create_phased_pwconst_broadcaster(src_id=x, seed=seed + x, rel_rates=pcw,
+                                                    avg_rate=world_rate, end_time=end_time,
+                                                    phase_shift=x) for x in b_ids]
+    elif kind == 'Hawkes':
+        others = [('Hawkes', {'src_id': x, 'seed': seed + x, 'l_0': world_rate,
+                              'alpha': world_alpha, 'beta': world_beta}) for x in b_ids]
+    elif kind == 'Poisson2':
+        logging.warning('The rates are being randomised for Poisson2')
+        others = [('Poisson2', {'src_id': x, 'seed': seed + x,
+                                'rate': world_rate * np.abs(rs.randn() + 1.0)}) for x in b_ids]
+    else:
+        raise ValueError('Cannot create broadcasters of kind "{}"'.format(kind))
+    network.extend([(1, x) for x in rs.choice(follower_ids, num_followers, replace=False)])
+    so = SimOpts(src_id=1, end_time=end_time, s=np.asarray([1.0] * num_followers),
+                 sink_ids=follower_ids, other_sources=others, edge_list=network,
+                 q=1.0 * (num_followers ** 2))
+    return trim_sim_opts(so)

@@ -280,6 +280,20 @@ def gen_graphs():
     rec["mf_sinks"] = np.asarray(so.sink_ids, dtype=np.int64)
     rec["mf_q"] = np.asarray([so.q])
     rec["mf_src"] = np.asarray([x[1]["src_id"] for x in so.other_sources], dtype=np.int64)
+    # the PiecewiseConst (phased semi-sinusoids) and Poisson2 (randomised rates) kinds
+    for kind in ("PiecewiseConst", "Poisson2"):
+        so = R.prepare_multiple_followers_sim_opts(num_followers=10, opts=R.multiple_follower_opts.set_new(
+            kind=kind, num_other_broadcasters=6, max_num_followers=20, follower_other_degree=2))
+        k = "mf_" + kind.lower()
+        rec[k + "_edges"] = np.asarray(so.edge_list, dtype=np.int64)
+        rec[k + "_src"] = np.asarray([x[1]["src_id"] for x in so.other_sources], dtype=np.int64)
+        rec[k + "_seed"] = np.asarray([x[1]["seed"] for x in so.other_sources], dtype=np.int64)
+        if kind == "PiecewiseConst":
+            rec[k + "_rates"] = np.asarray([x[1]["rates"] for x in so.other_sources])
+            rec[k + "_times"] = np.asarray([x[1]["change_times"] for x in so.other_sources])
+        else:
+            rec[k + "_rates"] = np.asarray([x[1]["rate"] for x in so.other_sources])
+    rec["pwc24"] = np.asarray(R.make_piecewise_const(24))
     np.savez_compressed(os.path.join(HERE, "graphs.npz"), **rec)
 
 

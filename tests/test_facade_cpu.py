@@ -117,3 +117,41 @@ def test_inference_queue_helpers():
     op = {"seed": 1, "q": 2.0, "type": "Opt", "top_1": 0.5, "avg_rank": 1.0, "r_2": 2.0,
           "num_events": 3, "world_events": 4, "capacity": 3.0}
     assert list(R.extract_perf_fields(op)) == R.perf_opts.performance_fields
+
+
+def test_opt_runs_multiple_follower_names_are_drop_in(golden):
+    """redqueen_amd.opt_runs exports the reference's multiple-follower helpers with its
+    signatures (opt_runs.py:651-795) -- called exactly as tests/golden/gen_golden.py called
+    the reference's, they give its networks, sources and rates bit for bit."""
+    from redqueen_amd import opt_runs as R
+    g = golden("graphs.npz")
+    for name, (nf, nb, deg, seed) in {"c3": (1000, 50, 5, 1024), "small": (20, 7, 3, 5)}.items():
+        e = R.make_edge_list(num_followers=nf, num_broadcasters=nb, degree=deg, seed=seed,
+                             follower_id_offset=1000, broadcaster_id_offset=5000,
+                             opts=R.mk_edge_list_opts)
+        assert np.array_equal(np.asarray(e, dtype=np.int64), g[name]), name
+    so = R.prepare_multiple_followers_sim_opts(num_followers=50, opts=R.multiple_follower_opts.set_new(
+        kind="Hawkes", num_other_broadcasters=20, max_num_followers=80))
+    assert np.array_equal(np.asarray(so.edge_list), g["mf_edges"])
+    assert np.array_equal(np.asarray(so.sink_ids), g["mf_sinks"]) and so.q == g["mf_q"][0]
+    assert np.array_equal([x[1]["src_id"] for x in so.other_sources], g["mf_src"])
+    for kind in ("PiecewiseConst", "Poisson2"):
+        so = R.prepare_multiple_followers_sim_opts(num_followers=10, opts=R.multiple_follower_opts.set_new(
+            kind=kind, num_other_broadcasters=6, max_num_followers=20, follower_other_degree=2))
+        k = "mf_" + kind.lower()
+        assert np.array_equal(np.asarray(so.edge_list), g[k + "_edges"]), kind
+        assert np.array_equal([x[1]["src_id"] for x in so.other_sources], g[k + "_src"])
+        assert np.array_equal([x[1]["seed"] for x in so.other_sources], g[k + "_seed"])
+        if kind == "PiecewiseConst":
+            assert np.array_equal(np.asarray([x[1]["rates"] for x in so.other_sources]), g[k + "_rates"])
+            assert np.array_equal(np.asarray([x[1]["change_times"] for x in so.other_sources]),
+                                  g[k + "_times"])
+        else:
+            assert np.array_equal([x[1]["rate"] for x in so.other_sources], g[k + "_rates"])
+    assert R.make_piecewise_const(24) == list(g["pwc24"])
+    src = R.create_phased_pwconst_broadcaster(7, 3, [1.0, 2.0, 3.0], 2.0, 30.0, 4)
+    assert src[0] == "PiecewiseConst" and list(src[1]["change_times"]) == [0.0, 10.0, 20.0]
+    assert np.allclose(src[1]["rates"], np.asarray([2.0, 3.0, 1.0]) * 6.0 / 6.0)
+    t = R.trim_sim_opts(so)
+    assert t.q == so.q and list(t.sink_ids) == list(so.sink_ids)
+    assert callable(R.run_inference) and callable(R.run_inference_queue)

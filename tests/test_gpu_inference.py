@@ -77,6 +77,22 @@ def test_run_inference_queue_batched():
     assert len(out.df) == len(opt) + len(poi) + len(orc)
 
 
+def test_run_inference_equals_queue_legs(caplog):
+    """opt_runs.run_inference (opt_runs.py:350-440): the Opt / Poisson / Oracle legs of the
+    q x seed sweep -- the same records as run_inference_queue, without the Karimi leg the
+    reference's run_inference has commented out."""
+    import logging
+    O, R, SimOpts = _ctx()
+    gen = _gen(SimOpts)
+    a = R.run_inference_queue(N=2, T=20.0, num_segments=4, sim_opts_gen=gen, log_q_high=3, log_q_low=-1)
+    caplog.clear()
+    with caplog.at_level(logging.ERROR):
+        b = R.run_inference(N=2, T=20.0, num_segments=4, sim_opts_gen=gen, log_q_high=3, log_q_low=-1)
+    assert a.df.equals(b.df) and set(a.capacities) == set(b.capacities)
+    assert not any("kdd" in r.getMessage() for r in caplog.records)
+    _check_against_oracle(O, R, b, gen, 2, 20.0)
+
+
 def test_batched_equals_per_replica_workers(monkeypatch):
     """The two-batch Opt/Poisson legs == one worker_opt / worker_poisson per replica."""
     O, R, SimOpts = _ctx()
