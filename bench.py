@@ -200,6 +200,10 @@ def main():
     ap.add_argument("--workload", default="c3")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=0)
+    ap.add_argument("--streams", type=int, default=2,
+                    help="caller streams the steps alternate over (the engine keeps a "
+                         "workspace and side stream per caller stream, so step k's tail "
+                         "overlaps step k+1's generation and merge); 1 = one stream")
     ap.add_argument("--dist", action="store_true",
                     help="at N = 1 too: a world-size-1 RCCL group, the step's all-gather "
                          "runs through it")
@@ -257,13 +261,30 @@ def main():
                 torch.zeros((), dtype=torch.int32, device=dev),
                 torch.zeros((), dtype=torch.int64, device=dev)]
 
-    # the warmup runs the exact timed body: HIP loads a kernel's code object on its first
-    # launch (tens of ms for torch's), which must not land in the timed region
+    # steps alternate over caller streams: step k's batch, exchange, means and tallies are
+    # ordered on stream k % S, so the next step's generation and merge (another stream,
+    # its own workspace and side stream) fill the wave slots this step's sweep tail and
+    # scan leave; every step still runs all of its work inside the timed region, which
+    # ends with a device-wide synchronize
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream(device=dev)
+                                                for _ in range(max(1, a.streams) - 1)]
+
+    def run_steps(ks):
+        accs = []
+        for st in streams:
+            with torch.cuda.stream(st):
+                accs.append(new_acc())
+        for k in ks:
+            with torch.cuda.stream(streams[k % len(streams)]):
+                res, means = step(k)
+                accumulate(res, accs[k % len(streams)])
+        return accs
+
+    # the warmup runs the exact timed body (every stream, its workspace and side stream):
+    # HIP loads a kernel's code object on its first launch (tens of ms for torch's), which
+    # must not land in the timed region
     L.lib().rq_timing(1)
-    acc = new_acc()
-    for k in range(max(1, a.warmup)):
-        res, means = step(k + 10_000)
-        accumulate(res, acc)
+    run_steps([k + 10_000 for k in range(max(len(streams), a.warmup))])
     torch.cuda.synchronize()
 
     L.lib().rq_timing(1)
@@ -271,15 +292,14 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    acc = new_acc()
-    for k in range(a.steps):
-        res, means = step(k)
-        accumulate(res, acc)
-    csum, status, ties = acc
+    accs = run_steps(range(a.steps))
     torch.cuda.synchronize()
     if grouped:
         dist.barrier()
     el = time.perf_counter() - t0
+    csum = sum(x[0] for x in accs)
+    status = torch.stack([x[1] for x in accs]).max()
+    ties = sum(x[2] for x in accs)
     ms = np.zeros(5)
     nl = np.zeros(5, dtype=np.int64)
     L.lib().rq_timing_read(ms.ctypes.data_as(L._pd), nl.ctypes.data_as(L._pi64))

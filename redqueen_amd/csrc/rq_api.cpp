@@ -76,12 +76,16 @@ struct TimedLaunch {
     }
 };
 
-// Side streams of the pipelined chunk loop (rq_run_batch): per host thread, created on
-// first use on the caller's current device, with the fork / join events.  Work on them
-// is always bracketed by a wait on the caller's stream (fork) and a wait of the caller's
-// stream on them (join), so the call stays stream-ordered for the caller.
+// Side streams of the pipelined chunk loop (rq_run_batch): per host thread AND per
+// caller stream, created on first use on the caller's current device, with the fork /
+// join events.  Work on them is always bracketed by a wait on the caller's stream (fork)
+// and a wait of the caller's stream on them (join), so the call stays stream-ordered for
+// the caller; batches issued on different caller streams get different side streams and
+// so overlap (a caller alternating two streams overlaps one batch's tail with the next
+// batch's generation and merge).
 struct SidePipe {
     int dev = -1;
+    hipStream_t caller = nullptr;
     hipStream_t s[2] = {nullptr, nullptr};
     hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};
     int get(int n, hipStream_t* out)
@@ -102,7 +106,24 @@ struct SidePipe {
         return RQ_OK;
     }
 };
-thread_local SidePipe t_pipe;
+// a few caller streams per thread (the engine's users run on one or two); past kPipes
+// the least recently added entry is reused
+constexpr int kPipes = 4;
+struct SidePipes {
+    SidePipe p[kPipes];
+    int next = 0, used = 0;
+    SidePipe& of(hipStream_t caller)
+    {
+        for (int k = 0; k < used; ++k)
+            if (p[k].caller == caller) return p[k];
+        SidePipe& x = p[next];
+        next = (next + 1) % kPipes;
+        used = used < kPipes ? used + 1 : kPipes;
+        x.caller = caller;   // its streams and events are kept: only the owner changes
+        return x;
+    }
+};
+thread_local SidePipes t_pipes;
 
 }  // namespace
 
@@ -1082,24 +1103,26 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
     // side streams, forked after the tables / status above and joined before returning)
     // with buffer set k % nbuf, so a set is reused only in its own stream's order
     hipStream_t pst[3] = {s, nullptr, nullptr};
+    SidePipe& t_pipe = t_pipes.of(s);
     // the join of the side streams on EVERY exit: an error return inside the chunk loop
     // must not leave work queued on a side stream that writes the caller's buffers after
     // the caller's stream has moved on (the caller frees them when the call fails)
     struct Join {
         hipStream_t* pst;
+        SidePipe& sp;
         int n = 1;
         int done()
         {
             int rc = RQ_OK;
             for (int k = 1; k < n; ++k)
-                if (hipEventRecord(t_pipe.join[k - 1], pst[k]) != hipSuccess ||
-                    hipStreamWaitEvent(pst[0], t_pipe.join[k - 1], 0) != hipSuccess)
+                if (hipEventRecord(sp.join[k - 1], pst[k]) != hipSuccess ||
+                    hipStreamWaitEvent(pst[0], sp.join[k - 1], 0) != hipSuccess)
                     rc = RQ_EHIP;
             n = 1;
             return rc;
         }
         ~Join() { (void)done(); }
-    } join{pst};
+    } join{pst, t_pipe};
     if (p.nbuf > 1) {
         if ((rc = t_pipe.get(p.nbuf - 1, pst + 1)) != RQ_OK) return rc;
         if (hipEventRecord(t_pipe.fork, s) != hipSuccess) return RQ_EHIP;

@@ -139,7 +139,9 @@ class Graph:
         self.followers = np.zeros(max(1, self.n_followers), dtype=np.int64)[:self.n_followers]
         if self.n_followers:
             L.lib().rq_graph_followers(h, self.followers.ctypes.data_as(L._pi64))
-        self._ws = None
+        # one workspace per caller stream: batches enqueued on different streams may run
+        # at the same time and must not share buffers
+        self._wss = {}
         self._cap_scale = {}   # (controller kind, max_events) -> cap_scale an overflow needed
 
     def __del__(self):
@@ -149,6 +151,16 @@ class Graph:
                 L.lib().rq_graph_free(h)
             except Exception:
                 pass
+
+    def workspace_bytes(self, stream=None):
+        """Bytes of the workspace held for ``stream`` (default: the current stream)."""
+        use = stream or torch.cuda.current_stream()
+        ws = self._wss.get(use.cuda_stream)
+        return 0 if ws is None else ws.numel()
+
+    def release_workspaces(self):
+        """Drop every stream's workspace (the caching allocator keeps the blocks)."""
+        self._wss.clear()
 
     # ------------------------------------------------------------------
     def s_matrix(self, s, n_grid=1):
@@ -284,13 +296,15 @@ class Graph:
         # start from the capacity scale an earlier overflow rerun of this graph needed
         key = (ck, b.max_events >= 0)
         b.cap_scale = max(b.cap_scale, self._cap_scale.get(key, 1.0))
+        sk = use.cuda_stream
         while True:
             nbytes = C.c_size_t()
-            b.ws_budget = self._ws_budget(dev)
+            b.ws_budget = self._ws_budget(dev, sk)
             L.check("rq_workspace_size", lib.rq_workspace_size(self._h, C.byref(b), C.byref(nbytes)))
-            if self._ws is None or self._ws.numel() < nbytes.value:
-                self._ws = None
-                self._ws = torch.empty(max(256, nbytes.value), dtype=torch.uint8, device=dev)
+            ws = self._wss.get(sk)
+            if ws is None or ws.numel() < nbytes.value:
+                self._wss[sk] = ws = None
+                ws = self._wss[sk] = torch.empty(max(256, nbytes.value), dtype=torch.uint8, device=dev)
             metrics = torch.empty((R, Ks.size + 2), dtype=torch.float64, device=dev)
             counts = torch.empty((R, 4), dtype=torch.int64, device=dev)
             status = torch.empty(R, dtype=torch.int32, device=dev)
@@ -305,7 +319,7 @@ class Graph:
                 out.ev_t, out.ev_src, out.ev_cap = ev_t.data_ptr(), ev_src.data_ptr(), cap.value
             st = use.cuda_stream
             L.check("rq_run_batch", lib.rq_run_batch(self._h, C.byref(b), C.byref(out),
-                                                     self._ws.data_ptr(), self._ws.numel(), st))
+                                                     ws.data_ptr(), ws.numel(), st))
             res = BatchResult(self, metrics, counts, status, ev_t, ev_src, Ks, n_grid, int(n_rep))
             res.replica0 = int(gids[0]) if len(gids) else 0
             res.global_ids = gids
@@ -328,15 +342,16 @@ class Graph:
             b.cap_scale = b.cap_scale * 2.0
             self._cap_scale[key] = max(self._cap_scale.get(key, 1.0), b.cap_scale)
 
-    def _ws_budget(self, dev):
+    def _ws_budget(self, dev, sk=None):
         """The workspace's device-memory budget (rq_batch_desc.ws_budget): 0.9 x what this
         process can get -- the device's free memory, torch's cached (reserved, unallocated)
-        blocks and the graph's own workspace, which the next one replaces."""
+        blocks and the stream's own workspace, which the next one replaces."""
         if not torch.cuda.is_available():
             return 0   # plan queries without a device: the library's default
         free, _total = torch.cuda.mem_get_info(dev)
         cached = torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
-        held = self._ws.numel() if self._ws is not None else 0
+        ws = self._wss.get(sk if sk is not None else torch.cuda.current_stream().cuda_stream)
+        held = ws.numel() if ws is not None else 0
         return int(0.9 * (free + cached + held))
 
     def _plugin_streams(self, b, keep, dev, R_all, gids, world_seed, seed_mod):

@@ -197,10 +197,10 @@ def test_c5_workspace_within_free_memory():
     ref = g.run("opt", **kw)
     assert int(ref.status.max().item()) == 0
     ref_m, ref_c = ref.metrics.clone(), ref.counts.clone()
-    big = g._ws.numel()
+    big = g.workspace_bytes()
     assert big > 12 * 2 ** 30, big   # ~20 MB per replica in flight
     del ref
-    g._ws = None
+    g.release_workspaces()
     torch.cuda.empty_cache()
     free, _ = torch.cuda.mem_get_info()
     hog = torch.empty(free - 6 * 2 ** 30, dtype=torch.uint8, device="cuda")
@@ -208,9 +208,9 @@ def test_c5_workspace_within_free_memory():
         plan = g.run("opt", plan_only=True, **kw)
         assert plan["chunk"] < free_plan["chunk"], (plan, free_plan)
         res = g.run("opt", **kw)
-        assert g._ws.numel() <= 6 * 2 ** 30
+        assert g.workspace_bytes() <= 6 * 2 ** 30
         assert torch.equal(res.metrics, ref_m) and torch.equal(res.counts, ref_c)
     finally:
         del hog
-        g._ws = None
+        g.release_workspaces()
         torch.cuda.empty_cache()
