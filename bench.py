@@ -145,6 +145,8 @@ def pmc_traffic(workload, R, plan):
                     cyc = c["GRBM_GUI_ACTIVE"] / 8.0
                     issue["valu_insts"] = c["SQ_INSTS_VALU"]
                     issue["issue_frac"] = c["SQ_INSTS_VALU"] / (N_CU * 4 * cyc / 2.0)
+                if v.get("serial_avg_ns"):
+                    issue["serial_avg_ms"] = v["serial_avg_ns"] * 1e-6
                 return v["hbm_read_bytes"] + v["hbm_write_bytes"], os.path.relpath(path, ROOT), issue
     return None, None, None
 
@@ -399,6 +401,12 @@ def main():
                          "issue": issue,
                          "issue_frac": issue.get("issue_frac") if issue else None,
                          "wave_slot_occupancy": issue.get("wave_slot_occupancy") if issue else None,
+                         # the same algorithmic bytes over the launch's duration with every
+                         # kernel serialised (stamped PMC summary, AMD_SERIALIZE_KERNEL=3
+                         # trace): in the timed run the two streams' kernels share the chip,
+                         # which stretches each launch's HIP-event time
+                         "frac_serialized": (sweep_bytes / (issue["serial_avg_ms"] * 1e-3) / 1e9 /
+                                             HBM_PEAK_GBS) if issue and issue.get("serial_avg_ms") else None,
                          "note": "sweep is latency/issue-bound (serial event chain per replica); "
                                  "algorithmic bytes = 24 B/pivot row written%s" %
                                  ("" if fused else " + %d B/wall event read" % b_wall)},

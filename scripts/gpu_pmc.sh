@@ -22,6 +22,9 @@ print(g.run('opt', q=so['q'], s=so['s'], n_rep=$R, randomize=True, plan_only=Tru
 P="--output-format csv"
 timeout -k 10 -s KILL 200 rocprofv3 --kernel-trace --stats $P -d "$OUT/kt" -o kt -- python3 $B > "$OUT/kt.log" 2>&1 || { echo kt failed; tail -5 "$OUT/kt.log"; exit 1; }
 echo "kt ok"
+# every kernel alone on the chip (the serialised durations of pmc_summary.py's serial_avg_ns)
+AMD_SERIALIZE_KERNEL=3 timeout -k 10 -s KILL 200 rocprofv3 --kernel-trace --stats $P -d "$OUT/kts" -o kts -- python3 $B > "$OUT/kts.log" 2>&1 || { echo kts failed; tail -5 "$OUT/kts.log"; exit 1; }
+echo "kts ok"
 timeout -k 10 -s KILL 120 rocprofv3 --pmc FETCH_SIZE $P -d "$OUT/p3" -o p3 -- python3 $B > "$OUT/p3.log" 2>&1 || { echo p3 failed; tail -5 "$OUT/p3.log"; exit 1; }
 echo "fetch ok"
 timeout -k 10 -s KILL 120 rocprofv3 --pmc WRITE_SIZE $P -d "$OUT/p4" -o p4 -- python3 $B > "$OUT/p4.log" 2>&1 || { echo p4 failed; tail -5 "$OUT/p4.log"; exit 1; }

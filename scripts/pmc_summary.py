@@ -58,6 +58,15 @@ for k, rs in rows.items():
         if d.get("SQ_WAVES", 0) > 0 and d.get("GRBM_GUI_ACTIVE", 0) > 0:
             info["wave_slot_occupancy"] = wc * 4.0 / (d["SQ_WAVES"] * d["GRBM_GUI_ACTIVE"] / 8.0)
     out[k] = info
+# per-kernel average duration with every kernel serialised (AMD_SERIALIZE_KERNEL=3 kernel
+# trace, scripts/gpu_pmc.sh "kts" pass): the launch alone on the chip, the time a
+# serialised roofline figure divides by
+for f in glob.glob(root + "/kts/**/*kernel_stats.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        k = r["Name"].split("(")[0].replace("void ", "")
+        if k in out:
+            out[k]["serial_avg_ns"] = float(r["AverageNs"])
+            out[k]["serial_min_ns"] = float(r["MinNs"])
 meta = {}
 for kv in sys.argv[2:]:
     k, v = kv.split("=", 1)
