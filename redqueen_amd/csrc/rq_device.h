@@ -76,6 +76,18 @@ struct PhiloxStream {
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
+// set bits of a 64-bit wave mask in the lanes below this one (v_mbcnt_lo / _hi): no
+// per-lane 64-bit "below" constant that the compiler hoists out of a loop and spills
+__device__ __forceinline__ int mbcnt64(uint64_t m)
+{
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+// ... at or below this lane
+__device__ __forceinline__ int mbcnt64_incl(uint64_t m)
+{
+    return mbcnt64(m) + (int)((m >> lane_id()) & 1ull);
+}
+
 __device__ __forceinline__ double wave_min(double v)
 {
 #pragma unroll

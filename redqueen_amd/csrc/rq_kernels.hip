@@ -603,8 +603,7 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
             const bool own_b = act && ((ownm >> lane) & 1ull);     // controller post before #lane
             if (a.ev_t) {
                 // event log (t, stream): lane q's post (if any) then its arrival, in tile order
-                const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-                const int64_t pp = n_events + lane + __popcll(ownm & below);
+                const int64_t pp = n_events + lane + mbcnt64(ownm);
                 const int64_t pw = pp + (own_b ? 1 : 0);
                 double* Et = a.ev_t + o * a.ev_cap;
                 int32_t* Es = a.ev_src + o * a.ev_cap;
@@ -709,9 +708,7 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
                 uint64_t needm = ~0ull;
                 if (MRG && sk_stamp) {
                     const uint64_t sownm = __ballot(strm_own);
-                    const uint64_t incl = lane == 63 ? ~0ull : ((2ull << lane) - 1);
-                    const uint64_t excl = lane ? (~0ull >> (64 - lane)) : 0ull;
-                    const int seg = __popcll(ownm & incl) + __popcll(sownm & excl);
+                    const int seg = mbcnt64_incl(ownm) + mbcnt64(sownm);
                     const int nres = __popcll(ownm) + __popcll(sownm);
                     const bool wl = act && !strm_own && degl > 0;
                     bool rep = false;
@@ -862,7 +859,7 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
                     // (sumF); a post or own-stream arrival drops sumF from sumR (AggL)
                     const bool rst = own_b || strm_own;
                     const uint64_t rm = __ballot(rst);
-                    const bool hasr = (rm & (~0ull >> (63 - lane))) != 0;   // reset at or before #lane
+                    const bool hasr = mbcnt64_incl(rm) != 0;   // reset at or before #lane
                     const bool wl = act && !strm_own;
                     const int deg = wl ? e1 - e0 : 0;
                     const int odv = wl ? od : 0;

@@ -505,18 +505,18 @@ __device__ __forceinline__ bool place_rows(RowStage<NK>& rs, uint64_t ma, bool h
 {
     const int lane = lane_id();
     const uint64_t mo = __ballot(has_o), mw = __ballot(has_w);
-    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-    const uint64_t above = ma & ~below & ~(1ull << lane);
+    // the next row-holding lane above this one (per-lane shifts, no hoisted lane masks)
+    const uint64_t above = lane < 63 ? ma >> (lane + 1) : 0ull;
     const bool nxt = above != 0;
     const double ft = has_o ? ot : tt;
-    const double nft = __shfl(ft, nxt ? __ffsll((unsigned long long)above) - 1 : lane, 64);
+    const double nft = __shfl(ft, nxt ? lane + __ffsll((unsigned long long)above) : lane, 64);
     const bool keep_o = has_o && !(has_w ? ot == tt : (nxt && ot == nft));
     const bool keep_w = has_w && !(nxt && tt == nft);
     const bool tie0 = rs.nrow > 0 && bcast_d(ft, __ffsll((unsigned long long)ma) - 1) == rs.last_t;
     const uint64_t ko = __ballot(keep_o), kw = __ballot(keep_w);
     if (tie0 || ko != mo || kw != mw) status |= RQ_ST_TIE;
     const int64_t r0 = rs.nrow - (tie0 ? 1 : 0);
-    const int64_t po = r0 + __popcll(ko & below) + __popcll(kw & below);
+    const int64_t po = r0 + mbcnt64(ko) + mbcnt64(kw);
     const int64_t pw = po + (keep_o ? 1 : 0);
     if (keep_o && po < rs.cap) {
         rs.Rt[po] = ot;

@@ -311,8 +311,7 @@ __device__ __forceinline__ void sweep_fw_body(SweepArgs a)
         const bool own_b = act && ((ownm >> lane) & 1ull);       // controller post before #lane
         if (a.ev_t) {
             // event log (t, stream): lane q's post (if any) then its arrival, in tile order
-            const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-            const int64_t pp = n_events + lane + __popcll(ownm & below);
+            const int64_t pp = n_events + lane + mbcnt64(ownm);
             const int64_t pw = pp + (own_b ? 1 : 0);
             double* Et = a.ev_t + o * a.ev_cap;
             int32_t* Es = a.ev_src + o * a.ev_cap;
@@ -340,7 +339,7 @@ __device__ __forceinline__ void sweep_fw_body(SweepArgs a)
             // segments of the tile start at its own events (posts / own-stream arrivals)
             const bool rst = own_b || strm_own;
             const uint64_t rm = __ballot(rst);
-            const bool hasr = (rm & (~0ull >> (63 - lane))) != 0;   // own event at or before #lane
+            const bool hasr = mbcnt64_incl(rm) != 0;   // own event at or before #lane
             const bool wl = act && !strm_own;                        // a wall event
             const int deg = wl ? e1 - e0 : 0;
             const int odv = wl ? od : 0;
