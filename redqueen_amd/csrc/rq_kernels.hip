@@ -265,16 +265,20 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
         for (int q = 0; q < SPL; ++q) load_win(q);
     }
     // MRG: the replica's merged sequence; lane l holds entry mpos + l of the next tile
-    const double* mt = MRG ? a.mrg_t + rl * a.mrg_stride : nullptr;
-    const uint16_t* mj = MRG ? a.mrg_j + rl * a.mrg_stride : nullptr;
+    // (entry index of the replica's first entry; opaque at each tile's loads, so no
+    // per-lane 64-bit sequence pointers are hoisted out of the tile loop and spilled)
+    const int64_t mb = MRG ? rl * a.mrg_stride : 0;
+    auto mload = [&](int64_t e, double& t_, int& j_) __attribute__((always_inline)) {
+        int64_t x = mb;
+        __asm__ volatile("" : "+v"(x));
+        t_ = a.mrg_t[x + e];
+        j_ = a.mrg_j[x + e];
+    };
     const int mlen = MRG ? a.mrg_len[rl] : 0;
     int mpos = 0;
     double nxt_t = RQ_INF;
     int nxt_j = 0;
-    if (MRG && lane < mlen) {
-        nxt_t = mt[lane];
-        nxt_j = mj[lane];
-    }
+    if (MRG && lane < mlen) mload(lane, nxt_t, nxt_j);
     double span = -1.0;   // fast sweep: adaptive tile width in time (< 0: not estimated yet)
     double* st_t = reinterpret_cast<double*>(win);   // fast sweep: tile staging (64 t + 64 j)
     int* st_j = reinterpret_cast<int*>(st_t + 64);
@@ -296,8 +300,7 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
     if (BITS) agb.init(msk, a.nw, a.mstride, a.ctrl_idx, lane);
     RowStage<NK> rs;
     const int64_t rbase = rl * a.cap_rows;
-    rs.init(a.rows_t + rbase, a.rows_sum + rbase, a.rows_valid + rbase, a.rows_cnt + rbase * NK,
-            a.cap_rows);
+    rs.init(a.rows_t, a.rows_sum, a.rows_valid, a.rows_cnt, rbase, a.cap_rows);
     EvStage es;
     if (LOG && a.ev_t) es.init(a.ev_t + o * a.ev_cap, a.ev_src + o * a.ev_cap, a.ev_cap);
 
@@ -381,10 +384,7 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
             // the next tile's loads stay in flight through phases B and C
             nxt_t = RQ_INF;
             nxt_j = 0;
-            if (mpos + lane < mlen) {
-                nxt_t = mt[mpos + lane];
-                nxt_j = mj[mpos + lane];
-            }
+            if (mpos + lane < mlen) mload(mpos + lane, nxt_t, nxt_j);
         } else if constexpr (!LOG) {
             // windowed: every arrival before a cut tau, tau < the W-th pending arrival of
             // every source that has more (so the tile is complete) and tuned so the tile
@@ -997,11 +997,7 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
                     rs.last_t = opt_next;
                 }
                 if (rr >= 0 && lane == 0) {
-                    rs.Rt[rr] = opt_next;
-                    rs.Rs[rr] = (double)ag.sumR;
-                    rs.Rv[rr] = (uint32_t)ag.nvalid;
-#pragma unroll
-                    for (int kq = 0; kq < NK; ++kq) rs.Rc[rr * NK + kq] = (uint32_t)ag.cnt[kq];
+                    rs.write(rr, opt_next, (double)ag.sumR, ag.nvalid, ag.cnt);
                 }
             }
         }

@@ -357,11 +357,17 @@ struct RowStage {
     int r_cnt[NK];
     int64_t nrow, s0, cap;
     double last_t;
-    double* Rt;
-    double* Rs;
-    uint32_t* Rv;
-    uint32_t* Rc;
-    __device__ __forceinline__ void init(double* t, double* s, uint32_t* v, uint32_t* c, int64_t cap_)
+    // the replica's rows start at row rb of the kernel's row arrays (wave-uniform bases);
+    // a row's address is rebuilt at each store from rb, which an empty asm makes opaque,
+    // so the compiler cannot hoist four per-lane 64-bit row pointers out of the tile
+    // loop and spill them (they were reloaded from scratch every tile)
+    double* Rt0;
+    double* Rs0;
+    uint32_t* Rv0;
+    uint32_t* Rc0;
+    int64_t rb;
+    __device__ __forceinline__ void init(double* t, double* s, uint32_t* v, uint32_t* c, int64_t rb_,
+                                         int64_t cap_)
     {
         r_t = 0.0;
         r_sum = 0.0;
@@ -372,10 +378,23 @@ struct RowStage {
         s0 = 0;
         cap = cap_;
         last_t = -RQ_INF;
-        Rt = t;
-        Rs = s;
-        Rv = v;
-        Rc = c;
+        Rt0 = t;
+        Rs0 = s;
+        Rv0 = v;
+        Rc0 = c;
+        rb = rb_;
+    }
+    // row rr of this replica <- (t, sum, valid, cnt)
+    __device__ __forceinline__ void write(int64_t rr, double t, double sum, int valid, const int* cnt)
+    {
+        int64_t b = rb;
+        __asm__ volatile("" : "+v"(b));
+        const int64_t r = b + rr;
+        Rt0[r] = t;
+        Rs0[r] = sum;
+        Rv0[r] = (uint32_t)valid;
+#pragma unroll
+        for (int q = 0; q < NK; ++q) Rc0[r * NK + q] = (uint32_t)cnt[q];
     }
     // one whole row (no tie merge: the caller closes equal-time groups itself)
     __device__ __forceinline__ bool put(double t, double sum, int valid, const int* cnt, int lane,
@@ -401,14 +420,7 @@ struct RowStage {
         }
         return true;
     }
-    __device__ __forceinline__ void store(int64_t rr)
-    {
-        Rt[rr] = r_t;
-        Rs[rr] = r_sum;
-        Rv[rr] = (uint32_t)r_valid;
-#pragma unroll
-        for (int q = 0; q < NK; ++q) Rc[rr * NK + q] = (uint32_t)r_cnt[q];
-    }
+    __device__ __forceinline__ void store(int64_t rr) { write(rr, r_t, r_sum, r_valid, r_cnt); }
     __device__ __forceinline__ void flush(int lane)
     {
         const int rem = (int)(nrow - s0);
@@ -518,20 +530,8 @@ __device__ __forceinline__ bool place_rows(RowStage<NK>& rs, uint64_t ma, bool h
     const int64_t r0 = rs.nrow - (tie0 ? 1 : 0);
     const int64_t po = r0 + mbcnt64(ko) + mbcnt64(kw);
     const int64_t pw = po + (keep_o ? 1 : 0);
-    if (keep_o && po < rs.cap) {
-        rs.Rt[po] = ot;
-        rs.Rs[po] = (double)osum;
-        rs.Rv[po] = (uint32_t)oval;
-#pragma unroll
-        for (int kq = 0; kq < NK; ++kq) rs.Rc[po * NK + kq] = (uint32_t)ocnt[kq];
-    }
-    if (keep_w && pw < rs.cap) {
-        rs.Rt[pw] = tt;
-        rs.Rs[pw] = (double)wsum;
-        rs.Rv[pw] = (uint32_t)wval;
-#pragma unroll
-        for (int kq = 0; kq < NK; ++kq) rs.Rc[pw * NK + kq] = (uint32_t)wcnt[kq];
-    }
+    if (keep_o && po < rs.cap) rs.write(po, ot, (double)osum, oval, ocnt);
+    if (keep_w && pw < rs.cap) rs.write(pw, tt, (double)wsum, wval, wcnt);
     rs.last_t = bcast_d(has_w ? tt : ot, 63 - __builtin_clzll(ma));   // always kept
     rs.nrow = r0 + __popcll(ko) + __popcll(kw);
     rs.s0 = rs.nrow;

@@ -116,16 +116,20 @@ __device__ __forceinline__ void sweep_fw_body(SweepArgs a)
     else gen.none();
     int pos = 0, fil = 0;   // arrivals consumed / generated by this lane's source
     // MRG: the replica's merged sequence; lane l holds entry mpos + l of the next tile
-    const double* mt = MRG ? a.mrg_t + rl * a.mrg_stride : nullptr;
-    const uint16_t* mj = MRG ? a.mrg_j + rl * a.mrg_stride : nullptr;
+    // (entry index of the replica's first entry; opaque at each tile's loads, so no
+    // per-lane 64-bit sequence pointers are hoisted out of the tile loop and spilled)
+    const int64_t mb = MRG ? rl * a.mrg_stride : 0;
+    auto mload = [&](int64_t e, double& t_, int& j_) __attribute__((always_inline)) {
+        int64_t x = mb;
+        __asm__ volatile("" : "+v"(x));
+        t_ = a.mrg_t[x + e];
+        j_ = a.mrg_j[x + e];
+    };
     const int mlen = MRG ? a.mrg_len[rl] : 0;
     int mpos = 0;
     double nxt_t = RQ_INF;
     int nxt_j = 0;
-    if (MRG && lane < mlen) {
-        nxt_t = mt[lane];
-        nxt_j = mj[lane];
-    }
+    if (MRG && lane < mlen) mload(lane, nxt_t, nxt_j);
 
     const bool opt = a.ctrl_kind == RQ_SRC_OPT || a.ctrl_kind == RQ_SRC_OPTPW;
     // OptPWSignificance only in the PW instances: the thinning loop's registers stay out
@@ -149,8 +153,7 @@ __device__ __forceinline__ void sweep_fw_body(SweepArgs a)
     }
     RowStage<NK> rs;
     const int64_t rbase = rl * a.cap_rows;
-    rs.init(a.rows_t + rbase, a.rows_sum + rbase, a.rows_valid + rbase, a.rows_cnt + rbase * NK,
-            a.cap_rows);
+    rs.init(a.rows_t, a.rows_sum, a.rows_valid, a.rows_cnt, rbase, a.cap_rows);
 
     int64_t n_events = 0, posts = 0, world = 0;
     int status = 0;
@@ -190,10 +193,7 @@ __device__ __forceinline__ void sweep_fw_body(SweepArgs a)
             // the next tile's loads stay in flight through phases B and C
             nxt_t = RQ_INF;
             nxt_j = 0;
-            if (mpos + lane < mlen) {
-                nxt_t = mt[mpos + lane];
-                nxt_j = mj[mpos + lane];
-            }
+            if (mpos + lane < mlen) mload(mpos + lane, nxt_t, nxt_j);
             RQ_CLK(2);
         } else {
         // ---- A1: opportunistic passes while >= thr rings are below W; if some unfinished
@@ -483,11 +483,7 @@ __device__ __forceinline__ void sweep_fw_body(SweepArgs a)
                 rs.last_t = opt_next;
             }
             if (rr >= 0 && lane == 0) {
-                rs.Rt[rr] = opt_next;
-                rs.Rs[rr] = (double)ag.sumR;
-                rs.Rv[rr] = (uint32_t)ag.nvalid;
-#pragma unroll
-                for (int kq = 0; kq < NK; ++kq) rs.Rc[rr * NK + kq] = (uint32_t)ag.cnt[kq];
+                rs.write(rr, opt_next, (double)ag.sumR, ag.nvalid, ag.cnt);
             }
         }
     }
