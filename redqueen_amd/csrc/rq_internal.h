@@ -161,9 +161,11 @@ struct MergeArgs {
 #ifndef RQ_MRG_LB
 #define RQ_MRG_LB 1024
 #endif
-// wall events per branch-free batch of the merged-stream K = 1 sink-bit sweep
+// wall events per branch-free batch of the merged-stream K = 1 sink-bit sweep: C5 sweep
+// per 4096 replicas on one stream (same box, round 5) 4: 139.0, 5: 136.1, 6: 135.0 ms;
+// the pipelined 8192-replica step 382.6 / 372.0 / 374.5 ms (gpurun_out/abc5)
 #ifndef RQ_MRG_BLB
-#define RQ_MRG_BLB 4
+#define RQ_MRG_BLB 5
 #endif
 #define RQ_MG_B 512         // merge block: one source per thread (the fast general sweep: <= 512)
 

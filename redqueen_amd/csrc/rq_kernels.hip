@@ -780,7 +780,7 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
                         continue;
                     }
                     // the next <= BLB needed events from q, all before the next break (8; the
-                    // merged-stream instances 4 -- RQ_MRG_BLB -- so the batch fits their 128
+                    // merged-stream instances RQ_MRG_BLB (5) so the batch fits their 128
                     // VGPRs); without skipping, events q .. q+m-1
                     const uint64_t nb = q < 63 ? brk & (~0ull << (q + 1)) : 0ull;
                     uint64_t cand = needm & (nb ? (nb & (0ull - nb)) - 1 : ~0ull) & (~0ull << q);
