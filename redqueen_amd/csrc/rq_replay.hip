@@ -76,7 +76,11 @@ constexpr int RP_SMALL_NK = 1;
 #define RQ_RP_RFEW 3
 #endif
 constexpr int RP_RFEW = RQ_RP_RFEW;   // the small table's rows per thread, one workgroup per CU
-static_assert(RP_RFEW * RP_B < 4096 && RP_B * 2 < 4096, "bucket counts are 12-bit");
+// the bucket word of a sink: rows of it in this batch (low RP_BB bits), list offset (next)
+constexpr int RP_BB = RP_RFEW * RP_B < 4096 ? 12 : 13;
+constexpr int RP_BM = (1 << RP_BB) - 1;
+static_assert(RP_RFEW * RP_B < (1 << RP_BB) && RP_B * 2 < (1 << RP_BB) && 2 * RP_BB <= 30,
+              "bucket fields");
 constexpr uint64_t RP_EMPTY_KEY = 0x8000000000000000ull;   // INT64_MIN: gets its own slot
 
 struct alignas(16) RpSlot {
@@ -439,8 +443,8 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
             RpSlot* sl = tst + slot_c[r];
             st0[r] = valid[r] ? *sl : RpSlot{0, 0, -1, 0};
             // (low bits: the ticket-0 row may already have added the list offset)
-            m[r] = valid[r] ? ((GLOBAL ? bk_read(sl) : st0[r].bucket) & 0xFFF) : 0;
-            if (valid[r] && m[r] > 1 && ticket[r] == 0) bk_write(sl, (atomicAdd(&misc[8], m[r]) << 12) | m[r]);
+            m[r] = valid[r] ? ((GLOBAL ? bk_read(sl) : st0[r].bucket) & RP_BM) : 0;
+            if (valid[r] && m[r] > 1 && ticket[r] == 0) bk_write(sl, (atomicAdd(&misc[8], m[r]) << RP_BB) | m[r]);
         }
         __syncthreads();
 
@@ -450,7 +454,7 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
         for (int r = 0; r < R; ++r) {
             boff[r] = 0;
             if (valid[r] && m[r] > 1) {
-                boff[r] = bk_read(tst + slot_c[r]) >> 12;
+                boff[r] = bk_read(tst + slot_c[r]) >> RP_BB;
                 lst[boff[r] + ticket[r]] = tid * R + r;
             }
         }
