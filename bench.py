@@ -202,10 +202,13 @@ def main():
     ap.add_argument("--workload", default="c3")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=0)
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=0,
                     help="caller streams the steps alternate over (the engine keeps a "
                          "workspace and side stream per caller stream, so step k's tail "
-                         "overlaps step k+1's generation and merge); 1 = one stream")
+                         "overlaps step k+1's generation and merge); 1 = one stream; "
+                         "0 = 2, except C5, whose 164 GB step workspace does not fit twice "
+                         "in HBM (the second stream would plan smaller chunks: same mean "
+                         "rate, mixed launch sizes; gpurun_out/r05m)")
     ap.add_argument("--dist", action="store_true",
                     help="at N = 1 too: a world-size-1 RCCL group, the step's all-gather "
                          "runs through it")
@@ -268,8 +271,9 @@ def main():
     # its own workspace and side stream) fill the wave slots this step's sweep tail and
     # scan leave; every step still runs all of its work inside the timed region, which
     # ends with a device-wide synchronize
+    n_streams = a.streams or (1 if a.workload == "c5" else 2)
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream(device=dev)
-                                                for _ in range(max(1, a.streams) - 1)]
+                                                for _ in range(n_streams - 1)]
 
     def run_steps(ks):
         accs = []
@@ -391,6 +395,7 @@ def main():
             "kernels_ms_per_launch": {"gen_streams": gen_ms, "merge_streams": merge_ms, "sweep": sweep_ms,
                                       "scan": scan_ms},
             "launches_per_step": lps,
+            "caller_streams": len(streams),
             "sweep_plan": plan,
             "roofline": {"bound": "hbm", "kernel": "rq_sweep", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
