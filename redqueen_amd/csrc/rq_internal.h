@@ -164,6 +164,11 @@ struct MergeArgs {
 // wall events per branch-free batch of the merged-stream K = 1 sink-bit sweep: C5 sweep
 // per 4096 replicas on one stream (same box, round 5) 4: 139.0, 5: 136.1, 6: 135.0 ms;
 // the pipelined 8192-replica step 382.6 / 372.0 / 374.5 ms (gpurun_out/abc5)
+// merged-stream sweeps: a tile's rows are stored at the top of the next tile, ahead of
+// its prefetch loads (RowStage::flush_pend); 0 = at the end of their own tile (A/B)
+#ifndef RQ_MRG_DEFER
+#define RQ_MRG_DEFER 1
+#endif
 #ifndef RQ_MRG_BLB
 #define RQ_MRG_BLB 5
 #endif

@@ -366,9 +366,18 @@ struct RowStage {
     uint32_t* Rv0;
     uint32_t* Rc0;
     int64_t rb;
+    // merged-stream sweep (place_rows<NK, true>): this lane's rows of the last tile, kept
+    // in registers and stored by flush_pend() at the top of the next tile, ahead of that
+    // tile's prefetch loads.  vmcnt retires in issue order, so rows stored at the end of
+    // a tile made the loop-latch wait on the prefetched tile wait on the fresh stores too.
+    uint32_t p_o, p_w;   // the rows' indices in the replica (~0u: none)
+    double p_ot, p_os, p_wt, p_ws;
+    int p_ov, p_wv;
+    int p_oc[NK], p_wc[NK];
     __device__ __forceinline__ void init(double* t, double* s, uint32_t* v, uint32_t* c, int64_t rb_,
                                          int64_t cap_)
     {
+        p_o = p_w = ~0u;
         r_t = 0.0;
         r_sum = 0.0;
         r_valid = 0;
@@ -421,6 +430,12 @@ struct RowStage {
         return true;
     }
     __device__ __forceinline__ void store(int64_t rr) { write(rr, r_t, r_sum, r_valid, r_cnt); }
+    __device__ __forceinline__ void flush_pend()
+    {
+        if (p_o != ~0u) write(p_o, p_ot, p_os, p_ov, p_oc);
+        if (p_w != ~0u) write(p_w, p_wt, p_ws, p_wv, p_wc);
+        p_o = p_w = ~0u;
+    }
     __device__ __forceinline__ void flush(int lane)
     {
         const int rem = (int)(nrow - s0);
@@ -510,7 +525,9 @@ __device__ __forceinline__ void controller_tile(int n, bool act, double tt, int 
 //  (the last): a row is dropped when the next row has the same time; a first row
 //  equal to the previous tile's last row overwrites it.  ma = ballot(has_o|has_w),
 //  nonzero.  Returns true when the row capacity overflowed (stop the replica).
-template <int NK>
+//  DEFER: the rows go to rs's pending slots (empty on entry: flush_pend() ran since the
+//  last call); rows per replica stay below 2^32 (rows <= 2 x merged entries + 1, int).
+template <int NK, bool DEFER = false>
 __device__ __forceinline__ bool place_rows(RowStage<NK>& rs, uint64_t ma, bool has_o, bool has_w, double ot,
                                            double tt, int64_t osum, int oval, const int* ocnt,
                                            int64_t wsum, int wval, const int* wcnt, int& status)
@@ -530,8 +547,24 @@ __device__ __forceinline__ bool place_rows(RowStage<NK>& rs, uint64_t ma, bool h
     const int64_t r0 = rs.nrow - (tie0 ? 1 : 0);
     const int64_t po = r0 + mbcnt64(ko) + mbcnt64(kw);
     const int64_t pw = po + (keep_o ? 1 : 0);
-    if (keep_o && po < rs.cap) rs.write(po, ot, (double)osum, oval, ocnt);
-    if (keep_w && pw < rs.cap) rs.write(pw, tt, (double)wsum, wval, wcnt);
+    if constexpr (DEFER) {
+        rs.p_o = keep_o && po < rs.cap ? (uint32_t)po : ~0u;
+        rs.p_w = keep_w && pw < rs.cap ? (uint32_t)pw : ~0u;
+        rs.p_ot = ot;
+        rs.p_os = (double)osum;
+        rs.p_ov = oval;
+        rs.p_wt = tt;
+        rs.p_ws = (double)wsum;
+        rs.p_wv = wval;
+#pragma unroll
+        for (int q = 0; q < NK; ++q) {
+            rs.p_oc[q] = ocnt[q];
+            rs.p_wc[q] = wcnt[q];
+        }
+    } else {
+        if (keep_o && po < rs.cap) rs.write(po, ot, (double)osum, oval, ocnt);
+        if (keep_w && pw < rs.cap) rs.write(pw, tt, (double)wsum, wval, wcnt);
+    }
     rs.last_t = bcast_d(has_w ? tt : ot, 63 - __builtin_clzll(ma));   // always kept
     rs.nrow = r0 + __popcll(ko) + __popcll(kw);
     rs.s0 = rs.nrow;

@@ -111,6 +111,7 @@ __device__ __forceinline__ void sweep_fw_body(SweepArgs a)
     do {          \
     } while (0)
 #endif
+    constexpr bool DEFER = MRG && RQ_MRG_DEFER;   // rows stored one tile late (RowStage::flush_pend)
     SrcGen gen;
     if (lane < a.n_str && !MRG) gen.init(a.gen, lane, i, etab);
     else gen.none();
@@ -190,6 +191,7 @@ __device__ __forceinline__ void sweep_fw_body(SweepArgs a)
             tj = act ? nxt_j : 0;
             mpos += n;
             fin = mpos >= mlen;
+            if constexpr (DEFER) rs.flush_pend();   // the last tile's rows, ahead of the loads
             // the next tile's loads stay in flight through phases B and C
             nxt_t = RQ_INF;
             nxt_j = 0;
@@ -438,11 +440,12 @@ __device__ __forceinline__ void sweep_fw_body(SweepArgs a)
         n_events += n + __popcll(ownm);
         posts += __popcll(mo) + __popcll(__ballot(has_w && strm_own));
         world += __popcll(__ballot(has_w && !strm_own));
-        if (ma && place_rows<NK>(rs, ma, has_o, has_w, ot, tt, osum, oval, ocnt, wsum, wval, wcnt, status))
+        if (ma && place_rows<NK, DEFER>(rs, ma, has_o, has_w, ot, tt, osum, oval, ocnt, wsum, wval, wcnt, status))
             stop = true;
         RQ_CLK(5);   // rows
         if (stop || fin) break;
     }
+    if constexpr (DEFER) rs.flush_pend();
 #ifdef RQ_PHASE_CLOCK
     if (lane == 0 && a.clk)
         for (int q = 0; q < 8; ++q) atomicAdd(&a.clk[q], ck[q]);
