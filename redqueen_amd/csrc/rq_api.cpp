@@ -1478,6 +1478,9 @@ int rp_run(const double* t, const int64_t* src, const int64_t* sink, const int64
     a.end = end_time;
     a.nK = nK;
     for (int q = 0; q < RQ_MAX_K; ++q) a.Ks[q] = q < nK ? Ks[q] : 1;
+#ifdef RQ_PHASE_CLOCK
+    if (getenv("RQ_CLK_REPLAY")) a.clk = phase_clk();
+#endif
     a.info = (RpInfo*)(ws + p.off_info);
     a.rows_dt = (double*)(ws + p.off_dt);
     a.rows_sum = (double*)(ws + p.off_sum);

@@ -298,6 +298,7 @@ struct RpArgs {
     int64_t* gbase;           // [chunk] t-groups started before the chunk (within its df)
     RcCarry* carry;
     RcState* state;
+    unsigned long long* clk;  // RQ_PHASE_CLOCK builds only: rq_rp_fast per-phase s_memtime sums [8]
 };
 hipError_t rq_launch_rp(const RpArgs& a, int phase, hipStream_t s);
 

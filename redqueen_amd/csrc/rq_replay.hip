@@ -244,8 +244,7 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
     double* tb = reinterpret_cast<double*>(carve(8 * (BR + 2)));         // [0] prev, [1+i], [BR+1] next
     int64_t* eb = reinterpret_cast<int64_t*>(carve(8 * (BR + 1)));       // [0] prev eid, [1+i]
     int* gb = reinterpret_cast<int*>(carve(4 * BR));                      // t-group of row i
-    unsigned char* ob = carve(BR);                                        // own flag of row i
-    int* lst = reinterpret_cast<int*>(carve(4 * BR));                     // sink buckets: rows
+    int* lst = reinterpret_cast<int*>(carve(4 * BR));                     // sink buckets: 2 row + own
     int64_t* wsum = reinterpret_cast<int64_t*>(carve(8 * 16));            // wave totals (int64)
     int* ws32 = reinterpret_cast<int*>(carve(4 * 16 * (NK + 6)));         // wave totals (int)
     int* misc = reinterpret_cast<int*>(carve(4 * 16));                    // flags, counters
@@ -296,6 +295,21 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
     for (int q = 0; q < NK; ++q) km1[q] = a.Ks[q] - 1;
     const bool has_eid = a.eid != nullptr;
 
+#ifdef RQ_PHASE_CLOCK
+    // diagnostic builds: per-wave s_memtime per phase of the batch loop (RQ_CLK_REPLAY)
+    unsigned long long ck[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long tk = __builtin_amdgcn_s_memtime();
+#define RP_CLK(q)                                                   \
+    do {                                                            \
+        const unsigned long long t2 = __builtin_amdgcn_s_memtime(); \
+        ck[q] += t2 - tk;                                           \
+        tk = t2;                                                    \
+    } while (0)
+#else
+#define RP_CLK(q) \
+    do {          \
+    } while (0)
+#endif
     // carries across batches
     int64_t Gc = 0;        // t-groups started so far
     RpAcc<NK> carry;
@@ -374,6 +388,7 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
 
         // ---- A: neighbours of every row; its ticket in its sink's bucket ----
         __syncthreads();
+        RP_CLK(0);   // loop top, next batch's load issue, barrier 1
         const int last = (int)((r1 - b0) < BR ? (r1 - b0) : BR);
         const double t_last = tb[last];
         const int64_t e_last = has_eid ? eb[last] : 0;
@@ -393,7 +408,6 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
             start[r] = valid[r] && (first_row || ti[r] != t_prev);
             endg[r] = valid[r] && (i == r1 - 1 || tnx[r] != ti[r]);
             ticket[r] = valid[r] ? bk_add(tst + slot_c[r]) : 0;   // rows of this sink before me: unordered
-            ob[row] = own_c[r] ? 1 : 0;
             if (valid[r] && !first_row && ti[r] < t_prev) misc[3] = 1;
             if (has_eid && valid[r]) {
                 const int64_t ei = eb[1 + row], e_prev = eb[row];
@@ -420,7 +434,9 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
             ws32[16 + w] = nbo;
             ws32[32 + w] = nbw;
         }
+        RP_CLK(2);   // A: neighbours, tickets, group-start scan
         __syncthreads();
+        RP_CLK(3);   // barrier 2
         if (aborted) break;
         int st_pre, st_tot, n_ev_own, n_ev_world, dummy;
         totals_add(ws32, w, st_pre, st_tot);
@@ -438,14 +454,28 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
         }
         RpSlot st0[R];   // state before this batch
         int m[R];        // rows of the row's sink in this batch
+        int need = 0;    // list space of this thread's ticket-0 rows of sinks with > 1 row
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             RpSlot* sl = tst + slot_c[r];
             st0[r] = valid[r] ? *sl : RpSlot{0, 0, -1, 0};
             // (low bits: the ticket-0 row may already have added the list offset)
             m[r] = valid[r] ? ((GLOBAL ? bk_read(sl) : st0[r].bucket) & RP_BM) : 0;
-            if (valid[r] && m[r] > 1 && ticket[r] == 0) bk_write(sl, (atomicAdd(&misc[8], m[r]) << RP_BB) | m[r]);
+            need += (valid[r] && m[r] > 1 && ticket[r] == 0) ? m[r] : 0;
         }
+        {   // one allocator atomic per wave (a wave-wide scan places the lists)
+            const int incl = scan_add_i32(need);
+            int wb = 0;
+            if (lane == 63 && incl > 0) wb = atomicAdd(&misc[8], incl);
+            int off = __builtin_amdgcn_readlane(wb, 63) + incl - need;
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (valid[r] && m[r] > 1 && ticket[r] == 0) {
+                    bk_write(tst + slot_c[r], (off << RP_BB) | m[r]);
+                    off += m[r];
+                }
+        }
+        RP_CLK(4);   // B: totals, groups, states, list space
         __syncthreads();
 
         // ---- C: each row's place among its sink's rows in this batch ----
@@ -455,34 +485,59 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
             boff[r] = 0;
             if (valid[r] && m[r] > 1) {
                 boff[r] = bk_read(tst + slot_c[r]) >> RP_BB;
-                lst[boff[r] + ticket[r]] = tid * R + r;
+                lst[boff[r] + ticket[r]] = 2 * (tid * R + r) + (own_c[r] ? 1 : 0);   // row, own flag
             }
         }
         __syncthreads();
+        RP_CLK(3);   // barrier 3, list placement, barrier 4 (with barrier 2)
         int xs[R], xv[R], xc[R][NK];
+        // j: my sink's rows before me; pred: the last of them; own_le / own_lt: its latest
+        // own row at or before / before me (rows in batch order).  The R rows' lists are
+        // walked side by side, so each step has R independent LDS reads in flight.
+        int jj[R], pred_[R], ole[R], olt[R], mm[R];
+        int mmax = 0;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const int row = tid * R + r;
-            // j: my sink's rows before me; pred: the last of them; own_le / own_lt: its
-            // latest own row at or before / before me (rows in batch order)
-            int j = 0, pred = -1, own_le = own_c[r] ? row : -1, own_lt = -1;
-            if (valid[r] && m[r] > 1) {
-                for (int k = 0; k < m[r]; ++k) {
-                    const int y = lst[boff[r] + k];
-                    if (y < row) {
-                        ++j;
-                        pred = pred > y ? pred : y;
-                        if (ob[y]) {
-                            own_lt = own_lt > y ? own_lt : y;
-                            own_le = own_le > y ? own_le : y;
-                        }
-                    }
+            jj[r] = 0;
+            pred_[r] = -1;
+            ole[r] = own_c[r] ? tid * R + r : -1;
+            olt[r] = -1;
+            mm[r] = valid[r] && m[r] > 1 ? m[r] : 0;
+            mmax = mmax > mm[r] ? mmax : mm[r];
+        }
+        auto visit = [&](int r, int v) __attribute__((always_inline)) {
+            const int y = v >> 1;
+            if (y < tid * R + r) {
+                ++jj[r];
+                pred_[r] = pred_[r] > y ? pred_[r] : y;
+                if (v & 1) {
+                    olt[r] = olt[r] > y ? olt[r] : y;
+                    ole[r] = ole[r] > y ? ole[r] : y;
                 }
             }
+        };
+        // one row per thread: two entries of its list per LDS wait (1024 C3 dataframes
+        // 8.82 -> 8.35 ms); R rows: their R reads already share each wait
+        constexpr int KU = R == 1 ? 2 : 1;
+        for (int k = 0; k < mmax; k += KU) {
+            int v[KU][R];
+#pragma unroll
+            for (int u = 0; u < KU; ++u)
+#pragma unroll
+                for (int r = 0; r < R; ++r) v[u][r] = k + u < mm[r] ? lst[boff[r] + k + u] : 0x7FFFFFFF;
+#pragma unroll
+            for (int u = 0; u < KU; ++u)
+#pragma unroll
+                for (int r = 0; r < R; ++r) visit(r, v[u][r]);
+        }
+        RP_CLK(1);   // C1: the list walk
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int j = jj[r], pred = pred_[r], own_le = ole[r], own_lt = olt[r];
             int j_le = 0, j_lt = 0;   // positions of own_le / own_lt among the bucket
-            if (valid[r] && m[r] > 1 && (own_le >= 0 || own_lt >= 0)) {
-                for (int k = 0; k < m[r]; ++k) {
-                    const int y = lst[boff[r] + k];
+            if (mm[r] > 0 && (own_le >= 0 || own_lt >= 0)) {
+                for (int k = 0; k < mm[r]; ++k) {
+                    const int y = lst[boff[r] + k] >> 1;
                     j_le += y < own_le;
                     j_lt += y < own_lt;
                 }
@@ -525,7 +580,9 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
 
         // the next batch's rows (their loads have landed by now) into LDS, sinks hashed
         // (tb / eb were last read in A, two barriers ago)
+        RP_CLK(5);   // C2: own-row positions, ranks, carried states
         if (has_next) prep(b0 + BR, tn, sn, kn, en, tnn, t_last, e_last);
+        RP_CLK(6);   // next batch into LDS + its hash inserts
 
         // ---- D: running totals in row order; the last row of a t-group emits its pivot row ----
         // this thread's rows: inclusive prefixes in registers; the threads' totals are
@@ -593,8 +650,14 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
             misc[6] += n_ev_world;
             misc[8] = 0;   // bucket allocator (read in B, two barriers ago)
         }
+        RP_CLK(7);   // D: running totals, barrier 5, pivot-row stores
         if (misc[3]) break;   // unsorted (set in A, read after barriers): the df is rejected
     }
+#ifdef RQ_PHASE_CLOCK
+    if (lane == 0 && a.clk)
+        for (int q = 0; q < 8; ++q) atomicAdd(&a.clk[q], ck[q]);
+#endif
+#undef RP_CLK
 
     __syncthreads();
     if (aborted) {
@@ -1637,8 +1700,8 @@ size_t rp_fast_lds(int nK, int R)
 {
     auto al = [](size_t b) { return (b + 15) & ~(size_t)15; };
     const size_t br = (size_t)R * RP_B;
-    size_t s = al(8 * (br + 2)) + al(8 * (br + 1)) + al(4 * br) + al(br) + al(4 * br) +
-               al(8 * 16) + al(4 * 16 * (nK + 6)) + al(4 * 16);
+    size_t s = al(8 * (br + 2)) + al(8 * (br + 1)) + al(4 * br) + al(4 * br) + al(8 * 16) +
+               al(4 * 16 * (nK + 6)) + al(4 * 16);
     const size_t h = TIER == 0 ? RP_HS : RP_H;
     if (TIER < 2) s += al(8 * (h + 1)) + al(sizeof(RpSlot) * (h + 1));
     return s;
