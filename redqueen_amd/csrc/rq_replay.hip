@@ -1378,7 +1378,6 @@ __global__ __launch_bounds__(RP_B) void rq_rc_apply(RpArgs a)
     };
     double* tb = reinterpret_cast<double*>(carve(8 * (RP_B + 2)));       // [0] prev, [1+i], [RP_B+1] next
     int* gb = reinterpret_cast<int*>(carve(4 * RP_B));                    // t-group of row i
-    unsigned char* ob = carve(RP_B);                                      // own flag of row i
     int* lst = reinterpret_cast<int*>(carve(4 * RP_B));                   // sink buckets: rows
     int64_t* wsum = reinterpret_cast<int64_t*>(carve(8 * 16));            // wave totals (int64)
     int* ws32 = reinterpret_cast<int*>(carve(4 * 16 * (NK + 6)));         // wave totals (int)
@@ -1492,7 +1491,6 @@ __global__ __launch_bounds__(RP_B) void rq_rc_apply(RpArgs a)
         const bool own = own_c;
         RpSlot* sl = tst + slot_c;
         const int ticket = valid ? atomicAdd(&sl->bucket, 1) : 0;
-        ob[tid] = own ? 1 : 0;
 
         // ---- B: t-group of every row (block scan of group starts); list space ----
         const int st_incl = scan_add_i32((int)start);
@@ -1504,34 +1502,46 @@ __global__ __launch_bounds__(RP_B) void rq_rc_apply(RpArgs a)
         gb[tid] = (int)G;
         const RpSlot st0 = valid ? *sl : RpSlot{0, 0, -1, 0};
         const int m = valid ? (st0.bucket & 0xFFF) : 0;
-        if (valid && m > 1 && ticket == 0) sl->bucket = (atomicAdd(&misc[8], m) << 12) | m;
+        {   // list space: one allocator atomic per wave (rp_fast_body)
+            const int need = valid && m > 1 && ticket == 0 ? m : 0;
+            const int incl = scan_add_i32(need);
+            int wb = 0;
+            if (lane == 63 && incl > 0) wb = atomicAdd(&misc[8], incl);
+            if (need) sl->bucket = ((__builtin_amdgcn_readlane(wb, 63) + incl - need) << 12) | m;
+        }
         __syncthreads();
 
         // ---- C: my place among my sink's rows in this batch ----
         int boff = 0;
         if (valid && m > 1) {
             boff = sl->bucket >> 12;
-            lst[boff + ticket] = tid;
+            lst[boff + ticket] = 2 * tid + (own ? 1 : 0);   // row, own flag
         }
         __syncthreads();
         int j = 0, pred = -1, own_le = own ? tid : -1, own_lt = -1;
-        if (valid && m > 1) {
-            for (int k = 0; k < m; ++k) {
-                const int y = lst[boff + k];
-                if (y < tid) {
-                    ++j;
-                    pred = pred > y ? pred : y;
-                    if (ob[y]) {
-                        own_lt = own_lt > y ? own_lt : y;
-                        own_le = own_le > y ? own_le : y;
-                    }
+        auto visit = [&](int v) __attribute__((always_inline)) {
+            const int y = v >> 1;
+            if (y < tid) {
+                ++j;
+                pred = pred > y ? pred : y;
+                if (v & 1) {
+                    own_lt = own_lt > y ? own_lt : y;
+                    own_le = own_le > y ? own_le : y;
                 }
+            }
+        };
+        if (valid && m > 1) {
+            for (int k = 0; k < m; k += 2) {   // two entries per LDS wait
+                const int v0 = lst[boff + k];
+                const int v1 = k + 1 < m ? lst[boff + k + 1] : 0x7FFFFFFF;
+                visit(v0);
+                visit(v1);
             }
         }
         int j_le = 0, j_lt = 0;
         if (valid && m > 1 && (own_le >= 0 || own_lt >= 0)) {
             for (int k = 0; k < m; ++k) {
-                const int y = lst[boff + k];
+                const int y = lst[boff + k] >> 1;
                 j_le += y < own_le;
                 j_lt += y < own_lt;
             }
@@ -1710,7 +1720,7 @@ size_t rp_fast_lds(int nK, int R)
 size_t rc_apply_lds(int nK)
 {
     auto al = [](size_t b) { return (b + 15) & ~(size_t)15; };
-    return al(8 * (RP_B + 2)) + al(4 * RP_B) + al(RP_B) + al(4 * RP_B) + al(8 * 16) + al(4 * 16 * (nK + 6)) +
+    return al(8 * (RP_B + 2)) + al(4 * RP_B) + al(4 * RP_B) + al(8 * 16) + al(4 * 16 * (nK + 6)) +
            al(4 * 16) + al(sizeof(RpSlot) * RC_S);
 }
 

@@ -5,8 +5,6 @@ O=gpurun_out/r05p; mkdir -p $O
 timeout -k 10 400 python3 -u -m pytest tests/test_gpu_replay.py tests/test_gpu_replay_batch.py tests/test_gpu_replay_chunked.py tests/test_gpu_realdata.py tests/test_gpu_analysis.py -x -q --timeout 200 --timeout-method thread > $O/tests.txt 2>&1 || { tail -30 $O/tests.txt; exit 1; }
 tail -2 $O/tests.txt
 for L in librq_base.so librq.so librq_base.so librq.so; do
-  RQ_SO_PATH=$PWD/redqueen_amd/$L timeout -k 10 300 python3 scripts/bench_paths.py --only replay_batch,replay_batch_1024 > $O/bp.json 2> $O/bp.err || { tail -5 $O/bp.err; exit 1; }
-  python3 -c "
-import json; d=json.loads(open('$O/bp.json').read().strip().splitlines()[-1]); d=d.get('sections', d)
-print('$L', {k: (round(v['ms_fast'],3), round(v['GBps'])) for k,v in d.items() if isinstance(v, dict) and 'ms_fast' in v})"
+  RQ_SO_PATH=$PWD/redqueen_amd/$L timeout -k 10 300 python3 scripts/bench_paths.py --only replay_batch,replay_batch_1024,replay_batch_eid_chunked,replay_one_df,replay_one_df_one_workgroup > $O/bp.json 2> $O/bp.err || { tail -5 $O/bp.err; exit 1; }
+  python3 scripts/dev/bp_summary.py $O/bp.json $L
 done
