@@ -329,17 +329,17 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
     uint32_t slot_c[R];  // ... their sinks' slots
     auto load = [&](int64_t nb0, double (&t_)[R], int64_t (&s_)[R], int64_t (&k_)[R],
                     int64_t (&e_)[R]) __attribute__((always_inline)) {
+        // unconditional loads at a clamped row (prep masks the rows past r1): no
+        // exec-masked zeroing of the destinations, whose write-after-write wait on the
+        // previous batch's loads stalled the loop top
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int64_t ii = nb0 + tid * R + r;
-            t_[r] = 0.0;
-            s_[r] = k_[r] = e_[r] = 0;
-            if (ii < r1) {
-                t_[r] = a.t[ii];
-                s_[r] = a.src[ii];
-                k_[r] = a.sink[ii];
-                if (has_eid) e_[r] = a.eid[ii];
-            }
+            const int64_t ic = ii < r1 ? ii : r1 - 1;   // nd > 0 (the caller checks)
+            t_[r] = a.t[ic];
+            s_[r] = a.src[ic];
+            k_[r] = a.sink[ic];
+            e_[r] = has_eid ? a.eid[ic] : 0;
         }
     };
     auto prep = [&](int64_t nb0, const double (&t_)[R], const int64_t (&s_)[R], const int64_t (&k_)[R],
@@ -368,7 +368,7 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
             }
         }
     };
-    {
+    if (nd > 0) {
         double t0[R];
         int64_t s0[R], k0[R], e0[R];
         load(r0, t0, s0, k0, e0);
@@ -436,7 +436,6 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
         }
         RP_CLK(2);   // A: neighbours, tickets, group-start scan
         __syncthreads();
-        RP_CLK(3);   // barrier 2
         if (aborted) break;
         int st_pre, st_tot, n_ev_own, n_ev_world, dummy;
         totals_add(ws32, w, st_pre, st_tot);
@@ -475,7 +474,7 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
                     off += m[r];
                 }
         }
-        RP_CLK(4);   // B: totals, groups, states, list space
+        RP_CLK(3);   // barrier 2, B: totals, groups, states, list space
         __syncthreads();
 
         // ---- C: each row's place among its sink's rows in this batch ----
@@ -489,7 +488,7 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
             }
         }
         __syncthreads();
-        RP_CLK(3);   // barrier 3, list placement, barrier 4 (with barrier 2)
+        RP_CLK(3);   // barrier 3, list placement, barrier 4
         int xs[R], xv[R], xc[R][NK];
         // j: my sink's rows before me; pred: the last of them; own_le / own_lt: its latest
         // own row at or before / before me (rows in batch order).  The R rows' lists are
@@ -581,7 +580,10 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
         // the next batch's rows (their loads have landed by now) into LDS, sinks hashed
         // (tb / eb were last read in A, two barriers ago)
         RP_CLK(5);   // C2: own-row positions, ranks, carried states
-        if (has_next) prep(b0 + BR, tn, sn, kn, en, tnn, t_last, e_last);
+        // (unconditional: after the last batch it only writes LDS nobody reads; a skipped
+        // prep left the loads' registers pending on the back edge, and the loop top
+        // waited on them -- vmcnt(0) between each row's loads)
+        prep(b0 + BR, tn, sn, kn, en, tnn, t_last, e_last);
         RP_CLK(6);   // next batch into LDS + its hash inserts
 
         // ---- D: running totals in row order; the last row of a t-group emits its pivot row ----
@@ -616,6 +618,7 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
 #pragma unroll
             for (int q = 0; q < NK; ++q) ws32[96 + 16 * q + w] = x.c[q];
         }
+        RP_CLK(4);   // D1: running-total scans
         __syncthreads();
         RpAcc<NK> pre, tot;
         totals_add(wsum, w, pre.s, tot.s);
@@ -630,7 +633,11 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
         for (int q = 0; q < NK; ++q) bc[q] = carry.c[q] + pre.c[q] + (x.c[q] - lc[q]);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
+#ifdef RQ_RP_NOSTORE   // diagnostic only: the stores stay in the code but never run
+            if (endg[r] && a.n_df < 0) {
+#else
             if (endg[r]) {
+#endif
                 const int64_t i = b0 + tid * R + r;
                 const int64_t row = r0 + G[r];
                 a.rows_dt[row] = (i == r1 - 1 ? a.end : tnx[r]) - ti[r];
@@ -650,7 +657,7 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
             misc[6] += n_ev_world;
             misc[8] = 0;   // bucket allocator (read in B, two barriers ago)
         }
-        RP_CLK(7);   // D: running totals, barrier 5, pivot-row stores
+        RP_CLK(7);   // D2: barrier 5, block totals, pivot-row stores
         if (misc[3]) break;   // unsorted (set in A, read after barriers): the df is rejected
     }
 #ifdef RQ_PHASE_CLOCK
