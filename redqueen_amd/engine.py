@@ -177,19 +177,24 @@ class Graph:
         tensor the batch reads or writes is allocated with that stream current, so
         the caching allocator, the library and the status check all agree on it.
         With a dynamic plugin among the sources, the batch's replicas (all of a batch of
-        <= 64, else a seeded sample of 64) are checked to be self-driven (_verify_dynamic)
-        before the result is returned."""
+        <= 64, else a seeded sample of 64) are checked to be self-driven (_verify_dynamic);
+        when one reacts to other sources' events the whole batch is replayed to the
+        reactive fixed point (_run_reactive) before the result is returned."""
+        from .opt_model import PluginReacts
         use = stream or torch.cuda.current_stream()
         with torch.cuda.stream(use):
             res = self._run(*args, stream=use, **kw)
             if any(p[4] for p in self.plugins) and not kw.get("plan_only"):
-                self._verify_dynamic(args, dict(kw, stream=use), res)
+                try:
+                    self._verify_dynamic(args, dict(kw, stream=use), res)
+                except PluginReacts:
+                    res = self._run_reactive(args, dict(kw, stream=use), res)
             return res
 
     def _run(self, ctrl="opt", q=1.0, s=None, n_rep=1, ctrl_seed=0, world_seed=0,
             randomize=False, seed_mod=0, ctrl_rate=None, Ks=(1,), max_events=None,
             event_log=False, cap_scale=1.0, chunk=0, stream=None, check=True, sweep_mode=0, replica0=0, n_local=0,
-            plan_only=False, s_pw=None, period=None, rep_lo=0, rep_cnt=0):
+            plan_only=False, s_pw=None, period=None, rep_lo=0, rep_cnt=0, rd_override=None):
         """Enqueue one batch.  ``q``: scalar or [n_grid]; ``s``: per grid point
         row(s) over the sorted followers ([n_grid, F]) or anything ``s_matrix``
         takes.  Seeds: int base (seed + replica id) or a device uint32 tensor.
@@ -253,8 +258,8 @@ class Graph:
         else:
             b.world_seed0 = int(world_seed) & 0xFFFFFFFF
         b.seed_mod = int(seed_mod)
-        if self.plugins and randomize:
-            self._plugin_streams(b, keep, dev, R_all, gids, world_seed, int(seed_mod))
+        if self.plugins and (randomize or rd_override is not None):
+            self._plugin_streams(b, keep, dev, R_all, gids, world_seed, int(seed_mod), rd_override)
         if ck == L.SRC_POISSON2:
             if ctrl_rate is None:
                 raise ValueError("ctrl_rate required for a Poisson controlled source")
@@ -354,11 +359,13 @@ class Graph:
         held = ws.numel() if ws is not None else 0
         return int(0.9 * (free + cached + held))
 
-    def _plugin_streams(self, b, keep, dev, R_all, gids, world_seed, seed_mod):
-        """Per-replica times of the registered static broadcasters of a randomized
+    def _plugin_streams(self, b, keep, dev, R_all, gids, world_seed, seed_mod, override=None):
+        """Per-replica times of the registered plugin broadcasters of a randomized
         batch: replica i's instance gets seed u_i + 99 idx (randomize_other_sources,
-        opt_model.py:795-804) and the host runs its initialize() / get_all_times();
-        the times reach the kernels as per-replica RealData streams (rq_batch_desc.rd_*)."""
+        opt_model.py:795-804) and the host runs its initialize() / get_all_times() (or a
+        self-driven dynamic plugin's schedule); ``override``: {global id: [times per
+        plugin]} instead (the reactive fixed point).  The times reach the kernels as
+        per-replica RealData streams (rq_batch_desc.rd_*)."""
         wseed = world_seed.to(torch.int64).cpu().numpy() if torch.is_tensor(world_seed) else None
         nrd = len(self.plugins)
         if nrd > L.MAX_RD:
@@ -367,8 +374,11 @@ class Graph:
         chunks = []
         for i in gids:   # increasing: rd_off is a prefix over the global ids
             i = int(i)
-            for c, inst in enumerate(self._plugin_instances(i, wseed, world_seed, seed_mod)):
-                t = self._plugin_source_times(inst)
+            ts = override[i] if override is not None else \
+                [self._plugin_source_times(inst)
+                 for inst in self._plugin_instances(i, wseed, world_seed, seed_mod)]
+            for c, t in enumerate(ts):
+                t = np.asarray(t, dtype=np.float64)
                 counts[i, c] = t.size
                 chunks.append(t)
         off = np.concatenate([[0], np.cumsum(counts.ravel())]).astype(np.int64)
@@ -440,6 +450,57 @@ class Graph:
                     times = self._plugin_source_times(gen)
                     verify_dynamic_plugin(fresh, self.start_time, self.sink_ids, self._edges,
                                           self.end_time, t_ev, s_ev, times, max_events=me)
+
+    def _run_reactive(self, args, kw, res):
+        """A batch whose dynamic plugins react to other sources' events, played to the
+        fixed point of run_dynamic's loop: every replica's plugin times are recomputed
+        from its run's other events (opt_model.reactive_plugin_times, a fresh plugin
+        instance per replica) and the replicas whose times moved are replayed with them
+        (per-replica RealData streams), until no replica's times move; events before a
+        plugin event whose time changed never change (every source sees only earlier
+        events), so each rerun fixes at least one more plugin event of every replica still
+        moving.  At most REACTIVE_MAX_ITERATIONS reruns, else NotImplementedError.  Cost:
+        one event-logged run and a host pass over every moving replica's events per rerun."""
+        from .opt_model import REACTIVE_MAX_ITERATIONS, reactive_plugin_times
+        gids = np.asarray(res.global_ids, dtype=np.int64)
+        ws = kw.get("world_seed", 0)
+        wseed = ws.to(torch.int64).cpu().numpy() if torch.is_tensor(ws) else None
+        rand = bool(kw.get("randomize"))
+        sm = int(kw.get("seed_mod", 0))
+        me = kw.get("max_events")
+        me = None if me is None or me == float("inf") else int(me)
+
+        def make(i):
+            if rand:
+                return self._plugin_instances(i, wseed, ws, sm)
+            return [cls(**kw_) for _idx, cls, kw_, _sid, _dyn in self.plugins]
+        times = {int(i): [self._plugin_source_times(inst) for inst in make(int(i))] for i in gids}
+        probe_kw = dict(kw, event_log=True, check=True)
+        moving = range(len(gids))
+        for it in range(REACTIVE_MAX_ITERATIONS + 1):
+            probe = self._run(*args, **dict(probe_kw, rd_override=times))
+            nxt = []
+            for k in moving:
+                i = int(gids[k])
+                t_ev, s_ev = probe.events(k)
+                insts, cur = make(i), times[i]
+                new = list(cur)
+                for c, p in enumerate(self.plugins):
+                    if p[4]:
+                        new[c] = reactive_plugin_times(insts[c], self.start_time, self.sink_ids,
+                                                       self._edges, self.end_time, t_ev, s_ev,
+                                                       max_events=me)
+                if any(not np.array_equal(a, b) for a, b in zip(new, cur)):
+                    times[i] = new
+                    nxt.append(k)
+            if not nxt:
+                break
+            if it == REACTIVE_MAX_ITERATIONS:
+                raise NotImplementedError("reactive dynamic broadcasters: no fixed point after %d "
+                                          "reruns" % REACTIVE_MAX_ITERATIONS)
+            moving = nxt
+        self.reactive_reruns = it
+        return self._run(*args, **dict(kw, rd_override=times))
 
     def _plan_variant(self, lib, b):
         info = (C.c_int64 * 8)()

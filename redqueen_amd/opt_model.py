@@ -227,14 +227,20 @@ def dynamic_plugin_times(obj, start_time, sink_ids, edge_list, end_time):
     return np.asarray(t, dtype=np.float64)
 
 
+class PluginReacts(NotImplementedError):
+    """A dynamic plugin's schedule moved on another source's event (verify_dynamic_plugin):
+    Graph.run then plays the batch through the reactive fixed point (Graph._run_reactive)."""
+
+
 def verify_dynamic_plugin(fresh, start_time, sink_ids, edge_list, end_time, ev_t, ev_src,
                           times, max_events=None):
     """Feed a fresh copy of a dynamic plugin every event of a run in play order
     (ev_t / ev_src: the engine's event log), as run_dynamic does (opt_model.py:271-311:
     get_next_event_time(last_event) for every event, event ids from 100, time_delta on
     the accumulated State.time); its schedule must put each of its own events where the
-    engine played them (`times`).  Raises NotImplementedError otherwise: the plugin's
-    schedule depends on other sources' events, which the engine cannot play."""
+    engine played them (`times`).  Raises PluginReacts otherwise: the plugin's schedule
+    depends on other sources' events, and the batch is replayed to the reactive fixed
+    point (engine.Graph._run_reactive)."""
     sinks = {}
     for a_, b_ in edge_list:
         sinks.setdefault(a_, []).append(b_)
@@ -263,11 +269,59 @@ def verify_dynamic_plugin(fresh, start_time, sink_ids, edge_list, end_time, ev_t
             if next(own, None) is not None or sched <= end_time:
                 bad = (n, None, sched)
     if bad is not None:
-        raise NotImplementedError(
+        raise PluginReacts(
             "dynamic broadcaster %s (src_id %r) is not self-driven: its schedule reacts to "
-            "other sources' events (at event %d: played %r, its schedule %r); the GPU engine "
-            "plays dynamic plugins whose schedule moves only on their own events "
-            "(RQ_EUNSUPPORTED)" % (type(fresh).__name__, fresh.src_id, bad[0], bad[1], bad[2]))
+            "other sources' events (at event %d: played %r, its schedule %r)"
+            % (type(fresh).__name__, fresh.src_id, bad[0], bad[1], bad[2]))
+
+
+REACTIVE_MAX_ITERATIONS = 1000
+
+
+def reactive_plugin_times(fresh, start_time, sink_ids, edge_list, end_time, ev_t, ev_src,
+                          max_events=None):
+    """Own event times of a dynamic plugin whose schedule may react to other sources'
+    events, given the OTHER sources' events of a run (ev_t / ev_src in play order; the
+    plugin's own entries in the log are dropped): run_dynamic's loop (opt_model.py:271-311)
+    with this plugin beside that fixed sequence.  After every event -- its own and the
+    others', event ids from 100, time_delta on the accumulated State.time -- the plugin's
+    get_next_event_time(event) gives its delay r, and its next event comes at
+    State.time + r unless another event comes first (equal times: the lower src_id first).
+    Exact when the other events do not depend on the plugin's; Graph.run / Manager.run_dynamic
+    rerun with these times until the run reproduces them (the fixed point)."""
+    sinks = {}
+    for a_, b_ in edge_list:
+        sinks.setdefault(a_, []).append(b_)
+    me = fresh.src_id
+    fresh.init_state(start_time, list(sink_ids), sinks.get(me, []), end_time)
+    r = fresh.get_next_event_time(None)
+    ev_t = np.asarray(ev_t, dtype=np.float64)
+    ev_src = np.asarray(ev_src)
+    keep = ev_src != me
+    ot, osrc = ev_t[keep], ev_src[keep]
+    out = []
+    state_time = float(start_time)
+    j, k, n_o = 0, 0, len(ot)
+    while max_events is None or k < max_events:
+        cand = state_time + r
+        if j < n_o and (float(ot[j]) < cand or (float(ot[j]) == cand and int(osrc[j]) < me)):
+            t, src = float(ot[j]), int(osrc[j])
+            j += 1
+        else:
+            if not cand <= end_time:
+                break   # every other event played (they are <= end_time)
+            if len(out) >= DYNAMIC_PLUGIN_MAX_EVENTS:
+                raise ValueError("broadcaster %s (src_id %r) posted more than %d events"
+                                 % (type(fresh).__name__, me, DYNAMIC_PLUGIN_MAX_EVENTS))
+            t, src = cand, me
+            out.append(cand)
+        ev = Event(100 + k, t - state_time, t, src, list(sinks.get(src, [])))
+        state_time += ev.time_delta
+        k += 1
+        if max_events is not None and k >= max_events:
+            break   # run_dynamic stops before it hands the last event over
+        r = fresh.get_next_event_time(ev)
+    return np.asarray(out, dtype=np.float64)
 
 
 def source_times(obj, start_time, sink_ids, edge_list, end_time):
@@ -511,7 +565,8 @@ class Manager:
         else:
             ctrl_id = ctrl.src_id
         # registered plugin broadcasters: their own initialize() / get_all_times(), or a
-        # self-driven dynamic plugin's own schedule (verified against the run below)
+        # dynamic plugin's own schedule (self-driven: reproduced by the run at once;
+        # reactive: recomputed from the run's other events until the run reproduces it)
         import copy
         probes = []
         other_desc = []
@@ -523,7 +578,7 @@ class Manager:
             t = source_times(s, self.start_time, self.sink_ids, self.edge_list, self.end_time)
             other_desc.append(("RealData", {"src_id": s.src_id, "times": t}))
             if fresh is not None:
-                probes.append((fresh, t))
+                probes.append((fresh, t, len(other_desc) - 1))
         if isinstance(ctrl, (Opt, OptPWSignificance)):
             fl = [e[1] for e in self.edge_list if e[0] == ctrl.src_id]
             if len(set(fl)) != len(fl):
@@ -537,36 +592,52 @@ class Manager:
             ctrl_a, ctrl_b = ctrl.change_times, ctrl.rates
         elif isinstance(ctrl, RealData):
             ctrl_a = ctrl.times
-        g = Graph(ctrl_id, other_desc, self.sink_ids, self.edge_list, self.end_time,
-                  start_time=self.start_time, ctrl_a=ctrl_a, ctrl_b=ctrl_b)
         maxev = None if max_events == float('inf') else int(max_events)
         seed = 0 if ctrl is None else int(ctrl.seed) & 0xFFFFFFFF
-        if isinstance(ctrl, Opt):
-            if isinstance(ctrl.s, dict):
-                s = ctrl.s
-            else:
-                s = np.ones(g.n_followers) * np.asarray(ctrl.s, dtype=float)
-            res = g.run("opt", q=ctrl.q, s=s, ctrl_seed=seed, max_events=maxev, event_log=True)
-        elif isinstance(ctrl, OptPWSignificance):
-            s_pw = ctrl._s_pw_for(g.n_followers)
-            res = g.run("sig", q=ctrl.q, s_pw=s_pw, period=float(ctrl.time_period), ctrl_seed=seed,
-                        max_events=maxev, event_log=True)
-            _sig_reach_check(g, self.edge_list, s_pw, ctrl.q, res.events(0)[1], max_events=maxev)
-        elif isinstance(ctrl, Poisson2):
-            res = g.run("poisson", ctrl_seed=seed, ctrl_rate=[float(ctrl.rate)], max_events=maxev,
-                        event_log=True)
-        elif isinstance(ctrl, PiecewiseConst):
-            res = g.run("pwconst", ctrl_seed=seed, max_events=maxev, event_log=True)
-        elif isinstance(ctrl, RealData):
-            res = g.run("times", max_events=maxev, event_log=True)
-        else:
-            res = g.run("wall", max_events=maxev, event_log=True)
+
+        def play(desc):
+            g = Graph(ctrl_id, desc, self.sink_ids, self.edge_list, self.end_time,
+                      start_time=self.start_time, ctrl_a=ctrl_a, ctrl_b=ctrl_b)
+            if isinstance(ctrl, Opt):
+                if isinstance(ctrl.s, dict):
+                    s = ctrl.s
+                else:
+                    s = np.ones(g.n_followers) * np.asarray(ctrl.s, dtype=float)
+                return g.run("opt", q=ctrl.q, s=s, ctrl_seed=seed, max_events=maxev, event_log=True)
+            if isinstance(ctrl, OptPWSignificance):
+                s_pw = ctrl._s_pw_for(g.n_followers)
+                res = g.run("sig", q=ctrl.q, s_pw=s_pw, period=float(ctrl.time_period),
+                            ctrl_seed=seed, max_events=maxev, event_log=True)
+                _sig_reach_check(g, self.edge_list, s_pw, ctrl.q, res.events(0)[1], max_events=maxev)
+                return res
+            if isinstance(ctrl, Poisson2):
+                return g.run("poisson", ctrl_seed=seed, ctrl_rate=[float(ctrl.rate)],
+                             max_events=maxev, event_log=True)
+            if isinstance(ctrl, PiecewiseConst):
+                return g.run("pwconst", ctrl_seed=seed, max_events=maxev, event_log=True)
+            if isinstance(ctrl, RealData):
+                return g.run("times", max_events=maxev, event_log=True)
+            return g.run("wall", max_events=maxev, event_log=True)
+
+        res = play(other_desc)
+        t, src = res.events(0)
+        for it in range(REACTIVE_MAX_ITERATIONS + 1):
+            new = [reactive_plugin_times(copy.deepcopy(fresh), self.start_time, self.sink_ids,
+                                         self.edge_list, self.end_time, t, src, max_events=maxev)
+                   for fresh, _times, _pos in probes]
+            if all(np.array_equal(a, times) for a, (_f, times, _p) in zip(new, probes)):
+                break
+            if it == REACTIVE_MAX_ITERATIONS:
+                raise NotImplementedError(
+                    "reactive dynamic broadcasters did not reach a fixed point in %d reruns"
+                    % REACTIVE_MAX_ITERATIONS)
+            probes = [(fresh, nt, pos) for (fresh, _t, pos), nt in zip(probes, new)]
+            for _f, nt, pos in probes:
+                other_desc[pos] = ("RealData", {"src_id": other_desc[pos][1]["src_id"], "times": nt})
+            res = play(other_desc)
+            t, src = res.events(0)
         for s in self.sources:
             s.used = True
-        t, src = res.events(0)
-        for fresh, times in probes:
-            verify_dynamic_plugin(fresh, self.start_time, self.sink_ids, self.edge_list,
-                                  self.end_time, t, src, times, max_events=maxev)
         self.state._set_log(t, src, self.edge_list, res)
         self.result = res
         return self

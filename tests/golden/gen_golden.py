@@ -38,7 +38,9 @@ installed and there is no network) and records, as plain data:
   plugin.npz       a registered static broadcaster (registerSource): df + metrics of the
                    seeded world and of randomize_other_sources(u), u = 0..15
   dynplugin.npz    a registered DYNAMIC self-driven broadcaster (Renewal) beside a static
-                   one: df + metrics of the seeded world and of randomize_other_sources(u)
+                   one: df + metrics of the seeded world and of randomize_other_sources(u);
+                   the same for a REACTIVE one (KnockedOff, knock_*)
+  dist_knock.npz   (--knock-dist N) the reactive plugin beside RedQueen: N reference runs
   errors.npz       reference behaviour on a scalar-s u_int_opt and on OptPWSignificance
                    events that reach no follower with positive significance
   sig_runs.npz     OptPWSignificance runs (notebook "Testing out significance",
@@ -607,10 +609,65 @@ def gen_dynplugin():
         cnts.append([own, world, m.state.get_num_events()])
     rec["rand_met"], rec["rand_cnt"], rec["rand_u"] = np.asarray(mets), np.asarray(cnts), np.asarray(us)
     w2 = dict(w, other_sources=[("KnockedOff", {"src_id": 2, "seed": 21, "rate": 1.0})] + w["other_sources"][1:])
-    m = SimOpts(**w2).create_manager_with_times(np.asarray(ctrl))
+    so2 = SimOpts(**w2)
+    m = so2.create_manager_with_times(np.asarray(ctrl))
     m.run_dynamic()
     rec["knocked_events"] = np.asarray([m.state.get_num_events()])
+    # the reactive plugin's run: df + metrics, and randomize_other_sources(u) for u in us
+    df = m.state.get_dataframe()
+    _df_cols(rec, "knock", df)
+    met, own, world = metrics(df, so2)
+    rec["knock_met"], rec["knock_cnt"] = met, np.asarray([own, world, m.state.get_num_events()])
+    mets, cnts = [], []
+    for u in us:
+        m = so2.randomize_other_sources(u).create_manager_with_times(np.asarray(ctrl))
+        m.run_dynamic()
+        df = m.state.get_dataframe()
+        met, own, world = metrics(df, so2)
+        mets.append(met)
+        cnts.append([own, world, m.state.get_num_events()])
+    rec["knock_rand_met"], rec["knock_rand_cnt"] = np.asarray(mets), np.asarray(cnts)
     np.savez_compressed(os.path.join(HERE, "dynplugin.npz"), **rec)
+
+
+KNOCK_SEED_STRIDE = 1000   # > 99 x the broadcaster count: no shared streams
+KNOCK_OPT_SEED_OFFSET = 500
+
+
+def _knock_worker(r):
+    from realdata_worlds import BurstyMixin, KnockedOffMixin, dyn_plugin_world
+    from redqueen.opt_model import Broadcaster
+
+    class Bursty(BurstyMixin, Broadcaster):
+        pass
+
+    class KnockedOff(KnockedOffMixin, Broadcaster):
+        pass
+    SimOpts.registerSource("Bursty", Bursty)
+    SimOpts.registerSource("KnockedOff", KnockedOff)
+    w, _ctrl, _us = dyn_plugin_world()
+    w2 = dict(w, other_sources=[("KnockedOff", {"src_id": 2, "seed": 21, "rate": 1.0})] +
+              w["other_sources"][1:])
+    so = SimOpts(**w2)
+    u = KNOCK_SEED_STRIDE * r
+    m = so.randomize_other_sources(u).create_manager_with_opt(seed=u + KNOCK_OPT_SEED_OFFSET)
+    m.run_dynamic()
+    df = m.state.get_dataframe()
+    met, own, world = metrics(df, so)
+    return np.concatenate([[own, world, m.state.get_num_events()], met])
+
+
+def gen_knock_dist(n, procs=0):
+    """The reactive plugin (KnockedOff: it reschedules when another source's event reaches
+    its followers) beside the RedQueen broadcaster, whose posts react to the plugin's
+    events in turn: replica r runs world randomize_other_sources(1000 r), RedQueen seed
+    1000 r + 500, through the reference itself."""
+    with mp.Pool(procs or os.cpu_count()) as pool:
+        res = np.asarray(pool.map(_knock_worker, range(n), chunksize=16))
+    cols = ["posts", "world", "events"] + ["top%d" % k for k in KS] + ["avg", "r2"]
+    np.savez_compressed(os.path.join(HERE, "dist_knock.npz"), data=res, cols=np.asarray(cols),
+                        seed_stride=np.asarray([KNOCK_SEED_STRIDE]),
+                        opt_seed_offset=np.asarray([KNOCK_OPT_SEED_OFFSET]))
 
 
 def gen_sig():
@@ -934,6 +991,8 @@ if __name__ == "__main__":
     ap.add_argument("--c4-start", type=int, default=0, help="append to dist_c4.npz from here")
     ap.add_argument("--c5s-dist", type=int, default=0, help="only dist_c5s.npz: N more replicas")
     ap.add_argument("--c5s-start", type=int, default=0, help="append to dist_c5s.npz from here")
+    ap.add_argument("--knock-dist", type=int, default=0,
+                    help="only dist_knock.npz: N reference runs of the reactive plugin beside RedQueen")
     ap.add_argument("--hawkes-seed0", action="store_true",
                     help="only dist_hawkes0.npz: the discarded 10k seed0-0 Hawkes world draw")
     a = ap.parse_args()
@@ -948,6 +1007,10 @@ if __name__ == "__main__":
     elif a.c5s_dist:
         gen_c5s_dist(a.c5s_dist, a.c5s_start, a.procs)
         print("done c5s dist", flush=True)
+        a.worlds = True   # nothing else
+    elif a.knock_dist:
+        gen_knock_dist(a.knock_dist, a.procs)
+        print("done knock dist", flush=True)
         a.worlds = True   # nothing else
     elif a.hawkes_seed0:
         gen_hawkes_seed0(a.procs)

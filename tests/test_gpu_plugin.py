@@ -5,10 +5,12 @@ per run, or once per replica with the seeds randomize_other_sources gives it,
 :795-804) and the engine plays the times as RealData streams -- per-replica ones
 through rq_batch_desc.rd_* (ABI v3).  Expected values: tests/golden/plugin.npz,
 written by gen_golden.py with the same class over the reference's Broadcaster.
-A DYNAMIC plugin runs when it is self-driven (its schedule moves only on its own
-events): its own times come from its get_next_event_time on the host and every run
-verifies it against the run's event sequence; a reactive one raises
-NotImplementedError (RQ_EUNSUPPORTED).  Expected values: tests/golden/dynplugin.npz."""
+A DYNAMIC plugin's own times come from its get_next_event_time on the host: a
+self-driven one (its schedule moves only on its own events) from its own schedule,
+verified against the run's event sequence; a reactive one (its schedule moves on other
+sources' events) from the run's other events, rerun until the run reproduces them
+(opt_model.reactive_plugin_times, Graph._run_reactive).  Expected values:
+tests/golden/dynplugin.npz, dist_knock.npz."""
 import os
 import sys
 
@@ -126,23 +128,93 @@ def test_self_driven_dynamic_plugin_randomized_batch(golden):
     assert np.array_equal(c[:, :3], d["rand_cnt"])
 
 
-def test_reactive_dynamic_plugin_refused(golden):
+def _knock_world(w):
+    return dict(w, other_sources=[("KnockedOff", {"src_id": 2, "seed": 21, "rate": 1.0})] +
+                w["other_sources"][1:])
+
+
+def test_reactive_dynamic_plugin_single_run(golden):
     """A dynamic plugin whose schedule reacts to other sources' events (KnockedOff, the
-    reference's SmartPoisson idea): the reference runs it (dynplugin.npz knocked_events),
-    the engine cannot play it and raises NotImplementedError (RQ_EUNSUPPORTED) -- for a
-    manager and for a batch -- instead of returning a different run."""
+    reference's SmartPoisson idea): the manager's run_dynamic plays it to the fixed point
+    and its df equals the reference's run_dynamic df bit for bit."""
+    engine, SimOpts, (w, ctrl, us) = _dyn_setup()
+    from redqueen_amd import utils as U
+    d = golden("dynplugin.npz")
+    so = SimOpts(**_knock_world(w))
+    m = so.create_manager_with_times(np.asarray(ctrl))
+    m.run_dynamic()
+    df = m.state.get_dataframe()
+    for c in COLS:
+        assert np.array_equal(df[c].values, d["knock_" + c]), c
+    got = U.replay_metrics(df, so.src_id, so.end_time, KS)
+    assert np.array_equal(np.asarray(got["top_k"] + [got["avg_rank"], got["r_2"]]), d["knock_met"])
+
+
+def test_reactive_dynamic_plugin_randomized_batch(golden):
+    """16 replicas in one batch with randomize_other_sources seeds: the probe finds the
+    plugin reactive, the batch is replayed to the fixed point, and every replica's
+    metrics and counts equal the reference's run."""
     engine, SimOpts, (w, ctrl, us) = _dyn_setup()
     d = golden("dynplugin.npz")
-    assert int(d["knocked_events"][0]) > 0
-    w2 = dict(w, other_sources=[("KnockedOff", {"src_id": 2, "seed": 21, "rate": 1.0})] +
-              w["other_sources"][1:])
-    so = SimOpts(**w2)
-    with pytest.raises(NotImplementedError):
-        so.create_manager_with_times(np.asarray(ctrl)).run_dynamic()
+    w2 = _knock_world(w)
     g = engine.Graph(w2["src_id"], w2["other_sources"], w2["sink_ids"], w2["edge_list"],
                      w2["end_time"], ctrl_a=ctrl)
-    with pytest.raises(NotImplementedError):
-        g.run("times", n_rep=4, world_seed=0, randomize=True, Ks=KS)
+    res = g.run("times", n_rep=len(us), world_seed=0, randomize=True, Ks=KS)
+    assert g.reactive_reruns >= 1
+    m = res.metrics.cpu().numpy()
+    c = res.counts.cpu().numpy()
+    assert np.array_equal(m, d["knock_rand_met"]), m - d["knock_rand_met"]
+    assert np.array_equal(c[:, :3], d["knock_rand_cnt"])
+
+
+def _fixed_point(g, res, w, cls, kws, me=None, n=None):
+    """Every replica's (the first n) plugin times reproduce themselves from its run's
+    other events."""
+    from redqueen_amd.opt_model import reactive_plugin_times
+    for k in range(len(res.global_ids) if n is None else n):
+        t, src = res.events(k)
+        got = reactive_plugin_times(cls(**kws(int(res.global_ids[k]))), 0.0, w["sink_ids"],
+                                    w["edge_list"], w["end_time"], t, src, max_events=me)
+        assert np.array_equal(got, t[src == 2]), k
+
+
+def test_reactive_plugin_beside_redqueen(golden):
+    """KnockedOff beside the RedQueen broadcaster, whose posts react to the plugin's
+    events in turn: the batch reaches the fixed point (every replica's plugin times come
+    back unchanged from its own run), and the ensemble matches the reference's own
+    ensemble of the same world (dist_knock.npz) in mean, spread and shape."""
+    import torch
+    import ensemble as E
+    engine, SimOpts, (w, ctrl, us) = _dyn_setup()
+    from realdata_worlds import KnockedOffMixin
+    from redqueen_amd.opt_model import Broadcaster
+
+    class KnockedOff(KnockedOffMixin, Broadcaster):
+        pass
+    d = golden("dist_knock.npz")
+    assert d["data"].shape[0] >= 10000
+    w2 = _knock_world(w)
+    g = engine.Graph(w2["src_id"], w2["other_sources"], w2["sink_ids"], w2["edge_list"],
+                     w2["end_time"])
+    stride = int(d["seed_stride"][0])
+    R = 4000
+    u = torch.arange(R, dtype=torch.int64) * stride + 7
+    res = g.run("opt", q=w2["q"], s=w2["s"], n_rep=R, ctrl_seed=u, world_seed=u, randomize=True,
+                Ks=KS, event_log=True)
+    assert g.reactive_reruns >= 1
+    print("reruns to the fixed point:", g.reactive_reruns)
+    assert int((res.status & 3).max().item()) == 0
+    _fixed_point(g, res, w2, KnockedOff,
+                 lambda i: {"src_id": 2, "seed": (i * stride + 7) & 0xFFFFFFFF, "rate": 1.0}, n=256)
+    cols = [str(c) for c in d["cols"]]
+    ref = {c: d["data"][:, i] for i, c in enumerate(cols)}
+    c = res.counts.double().cpu().numpy()
+    m = res.metrics.cpu().numpy()
+    eng = {"posts": c[:, 0], "world": c[:, 1], "events": c[:, 2], "avg": m[:, len(KS)],
+           "r2": m[:, len(KS) + 1]}
+    for i, k in enumerate(KS):
+        eng["top%d" % k] = m[:, i]
+    E.compare("gpu_knock_opt", eng, ref, z_bound=2.576)
 
 
 def _rarely_reactive():
@@ -169,9 +241,10 @@ def _rarely_reactive():
 def test_dynamic_plugin_verified_beyond_replica_zero(n_rep, react):
     """A dynamic plugin that reacts to other sources only in a few replicas, none of them
     replica 0: every replica of a batch of <= 64 is verified, a seeded
-    sample of 64 above that, so the batch raises NotImplementedError instead of
-    returning those replicas played as if self-driven.  The same plugin in a batch of
-    its self-driven replicas only runs."""
+    sample of 64 above that, so the batch is found reactive and replayed to the fixed
+    point instead of returning those replicas played as if self-driven: every replica's
+    plugin times come back unchanged from its own event log, and the self-driven
+    replicas equal a shard of them run alone."""
     engine, SimOpts, (w, ctrl, us) = _dyn_setup()
     RR = _rarely_reactive()
     RR.REACT = set(react)
@@ -181,9 +254,14 @@ def test_dynamic_plugin_verified_beyond_replica_zero(n_rep, react):
     g = engine.Graph(w2["src_id"], w2["other_sources"], w2["sink_ids"], w2["edge_list"],
                      w2["end_time"], ctrl_a=ctrl)
     assert 0 not in react
-    with pytest.raises(NotImplementedError):
-        g.run("times", n_rep=n_rep, world_seed=0, randomize=True, Ks=KS)
-    # replicas 0..4 (seeds 0..4: randomize_other_sources gives source idx 0 seed u) are
-    # self-driven: that shard runs
-    res = g.run("times", n_rep=n_rep, world_seed=0, randomize=True, Ks=KS, replica0=0, n_local=5)
+    res = g.run("times", n_rep=n_rep, world_seed=0, randomize=True, Ks=KS, event_log=True)
+    assert g.reactive_reruns >= 1
     assert int((res.status & 3).max().item()) == 0   # no overflow (ties are exact here: RealData)
+    _fixed_point(g, res, w2, RR, lambda i: {"src_id": 2, "seed": i, "scale": 0.6})
+    # replicas 0..4 (seeds 0..4: randomize_other_sources gives source idx 0 seed u) are
+    # self-driven: that shard runs without the reactive path and equals the batch's rows
+    g2 = engine.Graph(w2["src_id"], w2["other_sources"], w2["sink_ids"], w2["edge_list"],
+                      w2["end_time"], ctrl_a=ctrl)
+    r5 = g2.run("times", n_rep=n_rep, world_seed=0, randomize=True, Ks=KS, replica0=0, n_local=5)
+    assert not hasattr(g2, "reactive_reruns")
+    assert np.array_equal(r5.metrics.cpu().numpy(), res.metrics.cpu().numpy()[:5])
