@@ -132,6 +132,9 @@ typedef struct rq_graph* rq_graph_t;
                                     tiled sweep keeps the last row, so for a replica flagged
                                     here avg-rank / r^2 may differ: rerun it with sweep_mode 2 */
 #define RQ_ST_EMPTY 8            /* no event reached any sink: the reference's df is empty      */
+#define RQ_ST_UNORDERED 16       /* a sequential run over > 2048 sources (merged streams) met more
+                                    than 2048 arrivals at ONE time (replayed data only): their
+                                    order is not the reference's, the replica is not played    */
 
 #define RQ_RUN_EVENT_LOG 1       /* also write the (t, source) event log (for get_dataframe)    */
 

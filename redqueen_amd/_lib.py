@@ -15,7 +15,7 @@ SO_PATH = os.environ.get("RQ_SO_PATH") or os.path.join(_HERE, "librq.so")   # en
 RQ_OK, RQ_EINVAL, RQ_EOVERFLOW, RQ_EHIP, RQ_ENOMEM, RQ_EUNSORTED, RQ_EUNSUPPORTED = (
     0, -1, -2, -3, -4, -5, -6)
 SRC_NONE, SRC_POISSON, SRC_POISSON2, SRC_HAWKES, SRC_PWCONST, SRC_REALDATA, SRC_OPT, SRC_OPTPW = range(8)
-ST_ROWS_OVERFLOW, ST_STREAM_OVERFLOW, ST_TIE, ST_EMPTY = 1, 2, 4, 8
+ST_ROWS_OVERFLOW, ST_STREAM_OVERFLOW, ST_TIE, ST_EMPTY, ST_UNORDERED = 1, 2, 4, 8, 16
 RUN_EVENT_LOG = 1
 ABI_VERSION = 5
 REPLAY_LARGE = 1

@@ -210,6 +210,9 @@ struct Plan {
     // general fast sweep on merged streams (rq_merge_streams; sweep_mode 6: the windowed
     // per-source merge inside the sweep instead)
     bool mrg = false;
+    // the sequential sweep over > RQ_MAX_STREAMS sources: it plays the merged sequence
+    // too (its own per-lane rings hold <= 32 sources per lane)
+    bool lmrg = false;
     size_t off_mt = 0, off_mj = 0, off_mlen = 0;
     int64_t mrg_stride = 0;   // merged entries per replica (capacity)
     int n_grp = 1;            // > RQ_MG_B sources: groups of the two-level merge
@@ -419,8 +422,9 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p, double budget)
     const int nwl = (g->n_sinks + 31) / 32;
 
   replan:
-    // the sequential sweep owns <= 32 sources per lane
-    if (p->log && g->n_str > RQ_MAX_STREAMS) return RQ_EUNSUPPORTED;
+    // the sequential sweep owns <= 32 sources per lane; past that it plays the merged
+    // (t, stream) sequence of rq_merge_streams like the fast general sweep
+    p->lmrg = p->log && g->n_str > RQ_MAX_STREAMS;
     if (p->log) p->spl = g->n_str <= 64 ? 1 : g->n_str <= 512 ? 8 : g->n_str <= 1024 ? 16 : 32;
     p->mstride = g->nw | 1;   // odd row stride: one LDS bank per stream for a given word
     p->bits = !p->log && p->nK == 1 && b->Ks[0] == 1 && g->nw > 0 && b->sweep_mode != 3 &&
@@ -437,9 +441,9 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p, double budget)
     p->gs = false;
     // the fast general sweep plays the merged (t, stream) sequence: the merge kernel reads
     // every stream line once (one source per thread, <= RQ_MG_B sources)
-    p->mrg = !p->log && b->sweep_mode != 6;
+    p->mrg = (!p->log && b->sweep_mode != 6) || p->lmrg;
     p->n_grp = g->n_str > RQ_MG_B ? (g->n_str + RQ_MG_B - 1) / RQ_MG_B : 1;
-    if (const char* e = getenv("RQ_MRG")) p->mrg = p->mrg && atoi(e) != 0;   // A/B only
+    if (const char* e = getenv("RQ_MRG")) p->mrg = p->lmrg || (p->mrg && atoi(e) != 0);   // A/B only
     // without the merged streams the windowed sweep owns <= 8 sources per lane
     if (!p->mrg && !p->log && g->n_str > 512) {
         p->log = true;
@@ -485,8 +489,8 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p, double budget)
                 const size_t w_off = p->bl ? align_up(r_off + 8 * (size_t)nwl, 16)
                                            : align_up(r_off + rank_b * (size_t)p->n_sinks_pad, 16);
                 // LOG: rings of W arrivals for each real source; fast: the tile's staging
-                size_t stride = p->log ? align_up(w_off + 8 * (size_t)g->n_str * W, 16)
-                                       : align_up(w_off + 64 * 12, 16);
+                size_t stride = p->log && !p->lmrg ? align_up(w_off + 8 * (size_t)g->n_str * W, 16)
+                                                   : align_up(w_off + 64 * 12, 16);
                 // LOG: per-sink gtag/gcnt/gsum (gs: in global memory) + a wave_npsum<1>
                 // scratch (RQ_NPSUM1_LDS doubles)
                 const size_t x_off = stride;
@@ -1198,6 +1202,7 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             ma.out_len = (int*)(wsb + p.off_mlen);
             ma.mrg_stride = p.mrg_stride;
             ma.status = out->status;
+            ma.strict_ties = p.lmrg ? 1 : 0;
 #ifdef RQ_PHASE_CLOCK
             if (getenv("RQ_CLK_MERGE")) ma.clk = phase_clk();   // else the sweep's phases only
 #endif

@@ -144,7 +144,8 @@ struct MergeArgs {
     uint16_t* out_j;        // [C][mrg_stride]
     int* out_len;           // [C]
     int64_t mrg_stride;     // capacity per replica: past it the replica is flagged RQ_ST_STREAM_OVERFLOW
-    int32_t* status;        // RQ_ST_TIE when > RQ_MG_CAP arrivals share one time
+    int32_t* status;        // RQ_ST_TIE (strict_ties: RQ_ST_UNORDERED) when > RQ_MG_CAP arrivals share one time
+    int strict_ties;        // the sequential sweep plays this sequence: no exact rerun behind it
     // two-level merge (> RQ_MG_B sources): the first level merges group g's streams
     // [g RQ_MG_B, (g + 1) RQ_MG_B) of replica rl (grid y = group) into out_* at
     // [(rl n_grp + g) mrg_stride]; the second level (sub-merge) takes those n_grp

@@ -563,7 +563,7 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
                 }
             }
         }
-        const bool fin = LOG ? n < 64 : fin_w;
+        const bool fin = LOG && !MRG ? n < 64 : fin_w;
         const bool act = lane < n;
         int e0 = 0, e1 = 0, od = 0;
         if (act) {
@@ -1157,6 +1157,19 @@ static hipError_t launch_sweep_c(const SweepArgs& a, int nK, int col16, int bits
                  : launch_sweep_k<SPL, int, kGW, false>(a, nK, s);
 }
 
+// the sequential sweep on merged streams (> RQ_MAX_STREAMS sources): one instance per K
+// variant and per-sink state placement (GS)
+template <bool GS>
+static hipError_t launch_sweep_lm(const SweepArgs& a, int nK, hipStream_t s)
+{
+    switch (nK) {
+    case 1: return launch_sweep_t<1, 1, int, 4, true, false, false, GS, true>(a, s);
+    case 2: return launch_sweep_t<1, 2, int, 4, true, false, false, GS, true>(a, s);
+    case 3: return launch_sweep_t<1, 3, int, 4, true, false, false, GS, true>(a, s);
+    default: return launch_sweep_t<1, 4, int, 4, true, false, false, GS, true>(a, s);
+    }
+}
+
 // the fast sweep on merged streams: one instance per (K variant, column type)
 template <int NK, class COL>
 static hipError_t launch_sweep_mk(const SweepArgs& a, hipStream_t s)
@@ -1203,6 +1216,9 @@ hipError_t rq_launch_sweep(const SweepArgs& a, int spl, int nK, int col16, int l
     // W = 8; one source per lane when they fit (the per-lane ring state of eight sources
     // costs ~200 VGPRs and spills; 16 / 32 per lane spill more -- correctness instances
     // for 513..2048 sources, global columns only)
+    // > 2048 sources: the sequential sweep on merged streams (global columns, 4-deep
+    // rings the instance never fills)
+    if (log && spl == 0) return log == 2 ? launch_sweep_lm<true>(a, nK, s) : launch_sweep_lm<false>(a, nK, s);
     if (log == 2)
         switch (spl) {
         case 1: return col16 ? launch_sweep_k<1, uint16_t, 8, true, true>(a, nK, s)
@@ -1261,6 +1277,19 @@ static int occ_c(int nK, int col16, int W, int bits, int wpb, size_t lds)
 }
 int rq_sweep_blocks_per_cu(int spl, int nK, int col16, int W, int log, int bits, int wpb, size_t lds)
 {
+    if (log && spl == 0) {   // the sequential sweep on merged streams (launch_sweep_lm)
+        const bool gs = log == 2;
+        switch (nK) {
+        case 1: return gs ? occ_t<1, 1, int, 4, true, false, false, true, true>(wpb, lds)
+                          : occ_t<1, 1, int, 4, true, false, false, false, true>(wpb, lds);
+        case 2: return gs ? occ_t<1, 2, int, 4, true, false, false, true, true>(wpb, lds)
+                          : occ_t<1, 2, int, 4, true, false, false, false, true>(wpb, lds);
+        case 3: return gs ? occ_t<1, 3, int, 4, true, false, false, true, true>(wpb, lds)
+                          : occ_t<1, 3, int, 4, true, false, false, false, true>(wpb, lds);
+        default: return gs ? occ_t<1, 4, int, 4, true, false, false, true, true>(wpb, lds)
+                           : occ_t<1, 4, int, 4, true, false, false, false, true>(wpb, lds);
+        }
+    }
     if (log == 2)
         switch (spl) {
         case 1: return col16 ? occ_k<1, uint16_t, 8, true, true>(nK, wpb, lds) : occ_k<1, int, 8, true, true>(nK, wpb, lds);

@@ -344,7 +344,7 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
             // more than MG_CAP arrivals at t_lo itself: take the first MG_CAP (any subset
             // of equal times is a time prefix) and flag the replica
             nr = MG_CAP;
-            status |= RQ_ST_TIE;
+            status |= a.strict_ties ? RQ_ST_UNORDERED : RQ_ST_TIE;
         }
         if (outpos + (int64_t)nr > a.mrg_stride) {   // past the merged capacity (uniform)
             status |= RQ_ST_STREAM_OVERFLOW;

@@ -378,7 +378,6 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
     }
 
     for (int64_t b0 = r0; b0 < r1; b0 += BR) {
-        const bool has_next = b0 + BR < r1;
         // next batch (in flight across this batch's barriers)
         double tn[R];
         int64_t sn[R], kn[R], en[R];

@@ -331,6 +331,10 @@ class Graph:
             if not check:
                 return res
             use.synchronize()
+            if int((status & L.ST_UNORDERED).any().item()):
+                raise NotImplementedError(
+                    "more than 2048 arrivals at one time in a sequential run over > 2048 sources "
+                    "(RQ_ST_UNORDERED): their play order is not the reference's")
             ovf = int((status & (L.ST_ROWS_OVERFLOW | L.ST_STREAM_OVERFLOW)).any().item())
             if not ovf:
                 # equal event times in a fast tiled sweep: redo with the exact sequential

@@ -7,7 +7,8 @@ GPU, bit for bit against the engine-semantics oracle (oracle/rq_oracle.c):
   multigraph worlds equal the REFERENCE's own df (tests/test_gpu_realdata.py,
   realdata.npz rdmg*);
 * more than 512 sources (the two-level merge feeding the fast sweep, up to 65535; the
-  sequential sweep at 16 and 32 sources per lane, up to 2048);
+  sequential sweep at 16 and 32 sources per lane up to 2048, on the merged sequence
+  above);
 * the repeat-stream skip of the per-wave sink-bit sweep (a stream's second event
   before the next reset walks no sinks): on and off, bit for bit;
 * 50k sinks (per-wave sink bits for K = 1, int16 ranks for K > 1, and the
@@ -108,19 +109,21 @@ def _many_sources(n_src, n_sinks=120, deg=3, T=6.0, seed=11):
 
 
 @pytest.mark.parametrize("n_src,seq", [(600, False), (1500, False), (3000, False), (6000, False),
-                                       (600, True), (1500, True)])
+                                       (600, True), (1500, True), (3000, True), (6000, True)])
 def test_more_than_512_sources(n_src, seq):
     """> 512 sources: the fast general sweep plays the two-level merged sequence
     (rq_merge_streams over groups of 512 streams, then over the groups' sequences; any
     number of sources up to 65535); the exact sequential sweep (sweep_mode 2) owns 16 / 32
-    sources per lane up to 2048.  Event logs and metrics == the engine oracle."""
+    sources per lane up to 2048 and plays the same merged sequence above that.  Event logs
+    and metrics == the engine oracle."""
     torch, engine, graphs, O = _ctx()
     so = _many_sources(n_src)
     g = _graph(engine, so)
     kw = dict(sweep_mode=2) if seq else {}
     plan = g.run("opt", q=1.0, s=1.0, n_rep=4, plan_only=True, **kw)
     if seq:
-        assert plan["variant"] in (1, 4) and plan["sources_per_lane"] == (16 if n_src <= 1024 else 32)
+        assert plan["variant"] in (1, 4), plan
+        assert plan["sources_per_lane"] == (16 if n_src <= 1024 else 32 if n_src <= 2048 else 0), plan
     else:
         assert plan["variant"] not in (1, 4) and plan["sources_per_lane"] == 0, plan
     Ks = (1, 2)
@@ -136,14 +139,34 @@ def test_more_than_512_sources(n_src, seq):
         _cmp_replica(r1, 3, met_o, t_o, s_o, (1,))
 
 
-def test_more_than_2048_sources_sequential_unsupported():
-    """The exact sequential sweep stops at 2048 sources (32 per lane): a run that needs it
-    (here forced, sweep_mode 2) raises RQ_EUNSUPPORTED; the fast sweep takes the graph."""
+def test_more_than_2048_sources_what_needs_the_sequential_sweep():
+    """Past 2048 sources the runs that need the exact sequential sweep run on the merged
+    sequence (round 4: RQ_EUNSUPPORTED): a RealData source among 3000, max_events, and a
+    multigraph -- each == the engine oracle, and a 3000-source fast run == its sequential
+    twin on a continuous world."""
     torch, engine, graphs, O = _ctx()
-    from redqueen_amd import _lib as L
-    g = _graph(engine, _many_sources(3000))
-    with pytest.raises(L.RQError):
-        g.run("opt", q=1.0, s=1.0, n_rep=2, sweep_mode=2, Ks=(1,))
+    so = _many_sources(3000)
+    # a RealData broadcaster (recorded times, with repeats) and a duplicated edge
+    rd = np.round(np.sort(np.random.RandomState(4).uniform(0, so["end_time"], 25)), 1)
+    so_rd = dict(so, other_sources=so["other_sources"] + [("RealData", {"src_id": 9000, "times": rd})],
+                 edge_list=so["edge_list"] + [(9000, 3), (9000, 7), (1000, so["edge_list"][30][1])])
+    Ks = (1, 3)
+    for world, kw in ((so_rd, {}), (so, dict(max_events=400))):
+        g = _graph(engine, world)
+        plan = g.run("opt", q=1.0, s=1.0, n_rep=3, plan_only=True, **kw)
+        assert plan["variant"] in (1, 4) and plan["sources_per_lane"] == 0, plan
+        res = g.run("opt", q=1.0, s=1.0, n_rep=3, ctrl_seed=5, world_seed=5, randomize=True, Ks=Ks,
+                    event_log=True, **kw)
+        assert int((res.status & 3).max().item()) == 0
+        for r in (0, 2):
+            met_o, t_o, s_o = _oracle(O, _world_with_seeds(world, 5 + r), ("opt", 5 + r), Ks,
+                                      max_events=kw.get("max_events"))
+            _cmp_replica(res, r, met_o, t_o, s_o, Ks)
+    g = _graph(engine, so)
+    a = g.run("opt", q=1.0, s=1.0, n_rep=64, ctrl_seed=1, world_seed=1, randomize=True, Ks=Ks)
+    b = g.run("opt", q=1.0, s=1.0, n_rep=64, ctrl_seed=1, world_seed=1, randomize=True, Ks=Ks,
+              sweep_mode=2)
+    assert torch.equal(a.metrics, b.metrics) and torch.equal(a.counts, b.counts)
 
 
 def _bursty(n_src=200, n_sinks=3000, deg=40, n_fol=900, T=6.0, seed=17):
