@@ -182,7 +182,7 @@ struct rq_graph {
     // controlled-slot arrays (PiecewiseConst / RealData controlled runs)
     int ctrl_arr_off = 0, ctrl_arr_n = 0;
     DevBuf<int64_t> d_src_id;
-    DevBuf<int> d_kind, d_orig, d_arr_off, d_arr_n, d_csr_ptr, d_csr_col, d_outdeg_f, d_fol;
+    DevBuf<int> d_kind, d_orig, d_arr_off, d_arr_n, d_csr_ptr, d_csr_col, d_outdeg_f, d_fol, d_cbf;
     DevBuf<uint32_t> d_seed;
     DevBuf<double> d_p0, d_p1, d_p2, d_arr_a, d_arr_b;
 };
@@ -213,6 +213,10 @@ struct Plan {
     // the sequential sweep over > RQ_MAX_STREAMS sources: it plays the merged sequence
     // too (its own per-lane rings hold <= 32 sources per lane)
     bool lmrg = false;
+    // merged streams with the per-stream tables (CSR starts, follower out-degrees, tie
+    // flags, 1/c_j) in global memory: graphs whose tables do not fit LDS (the GT instances;
+    // the sequential ones on merged streams always)
+    bool gt = false;
     size_t off_mt = 0, off_mj = 0, off_mlen = 0;
     int64_t mrg_stride = 0;   // merged entries per replica (capacity)
     int n_grp = 1;            // > RQ_MG_B sources: groups of the two-level merge
@@ -457,8 +461,12 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p, double budget)
         // global memory as int (the kernel's COL type selects the path at compile time)
         // both placements are scored: LDS columns only win at equal waves per CU
         // LOG: the per-sink state in LDS, or (gs) in global memory for more sinks than fit
+        // GT (merged streams only): the per-stream tables in global memory -- tried when no
+        // layout with them in LDS fits, always for the sequential sweep on merged streams
+        for (int gt = p->lmrg ? 1 : 0; gt <= (p->mrg ? 1 : 0) && best < 0; ++gt)
         for (int gs = 0; gs <= (p->log ? 1 : 0); ++gs)
-        for (int col_lds = g->n_sinks <= 65535 && !(p->log && p->spl >= 16) ? 1 : 0; col_lds >= 0; --col_lds) {
+        for (int col_lds = g->n_sinks <= 65535 && !(p->log && p->spl >= 16) && !gt ? 1 : 0; col_lds >= 0; --col_lds) {
+            if (gt && p->bits) continue;   // the sink-bitset instances keep their tables in LDS
             if (const char* e = getenv("RQ_G_COLLDS"))   // tuning only: force the column placement
                 if (atoi(e) != col_lds) continue;
             const int c16 = col_lds;
@@ -467,12 +475,13 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p, double budget)
                                         : (col_lds ? 2 * g->csr_col.size() : 0);
             size_t sh = 0;
             const size_t o_col = sh;  sh = align_up(sh + colb, 16);
-            const size_t o_ptr = sh;  sh = align_up(sh + 4 * (g->n_str + 1), 16);
-            const size_t o_odf = sh;  sh = align_up(sh + 4 * g->n_str, 16);
-            const size_t o_cbf = sh;  sh = align_up(sh + 4 * g->n_str, 16);
+            const size_t tabn = gt ? 0 : (size_t)g->n_str;
+            const size_t o_ptr = sh;  sh = align_up(sh + 4 * (tabn + (gt ? 0 : 1)), 16);
+            const size_t o_odf = sh;  sh = align_up(sh + 4 * tabn, 16);
+            const size_t o_cbf = sh;  sh = align_up(sh + 4 * tabn, 16);
             const size_t o_fb = sh;   if (p->bl) sh = align_up(sh + 4 * (size_t)nwl, 16);
             // one grid point: the 1/c_j table once per block instead of once per wave
-            const bool inv_sh = b->n_grid == 1;
+            const bool inv_sh = b->n_grid == 1 && !gt;
             const size_t o_inv = sh;  if (inv_sh) sh = align_up(sh + 8 * (size_t)g->n_str, 16);
             const int spl = p->spl;
             int only_w = 0;
@@ -482,9 +491,9 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p, double budget)
             for (int W : {8, 4}) {
                 if ((p->log ? (spl >= 32 ? 4 : 8) : 4) != W) continue;
                 if (only_w && W != only_w) continue;
-                const size_t r_off = inv_sh ? 0 : align_up(8 * (size_t)g->n_str, 16);
+                const size_t r_off = inv_sh || gt ? 0 : align_up(8 * (size_t)g->n_str, 16);
                 const size_t rank_b = p->log ? (gs ? 0 : 4) : (p->bits ? 0 : 2);   // fast: int16 saturating
-            const int spl_i = p->mrg ? 0 : spl;   // the instance: 0 = merged streams
+            const int spl_i = p->mrg ? (gt ? -1 : 0) : spl;   // the instance: 0 = merged streams, -1 with GT
                 // BL: two bits per sink (T, V words) in place of the int16 ranks
                 const size_t w_off = p->bl ? align_up(r_off + 8 * (size_t)nwl, 16)
                                            : align_up(r_off + rank_b * (size_t)p->n_sinks_pad, 16);
@@ -519,7 +528,7 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p, double budget)
                         p->g_col = o_col; p->g_ptr = o_ptr; p->g_odf = o_odf; p->g_cbf = o_cbf;
                         p->g_wave = sh; p->g_wave_stride = stride; p->g_rank_off = r_off;
                         p->g_win_off = w_off; p->g_x_off = x_off; p->g_total = tot; p->g_fb = o_fb;
-                        p->g_inv = o_inv; p->g_inv_sh = inv_sh;
+                        p->g_inv = o_inv; p->g_inv_sh = inv_sh; p->gt = gt;
                     }
                 }
             }
@@ -537,7 +546,7 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p, double budget)
         if (p->bl && p->mrg && !p->gs) {
             const size_t st2 = align_up(p->g_wave_stride + 8 * (size_t)g->n_str, 16);
             const size_t tot2 = p->g_wave + p->gwpb * st2;
-            int blocks = tot2 <= kLdsMax ? rq_sweep_blocks_per_cu(0, p->nK, p->gcol16, p->gwin, 0, 2, p->gwpb, tot2) : 0;
+            int blocks = tot2 <= kLdsMax ? rq_sweep_blocks_per_cu(p->gt ? -1 : 0, p->nK, p->gcol16, p->gwin, 0, 2, p->gwpb, tot2) : 0;
             if (tot2 <= kLdsMax && blocks <= 0) blocks = (int)std::min<size_t>(kLdsMax / tot2, 16 / p->gwpb);
             bool on = blocks * p->gwpb >= p->wpc;
             if (const char* e = getenv("RQ_SKIP")) on = on && atoi(e) != 0;   // A/B only
@@ -914,6 +923,15 @@ int rq_graph_build(const rq_graph_desc* d, rq_graph_t* out)
 
     g->fbits.assign((g->n_sinks + 31) / 32, 0u);
     for (int c : g->fol) g->fbits[c / 32] |= 1u << (c % 32);
+    // the controller posts before a wall event at the same time when that source is static
+    // or has a larger src_id (opt_model.py:279-281, :289-290): the sweeps' per-stream flag,
+    // in global memory for the GT instances (the others build it in LDS)
+    std::vector<int> cbf(g->n_str);
+    for (int j = 0; j < g->n_str; ++j) {
+        const int kj = g->kind[j];
+        cbf[j] = kj == RQ_SRC_POISSON2 || kj == RQ_SRC_PWCONST || kj == RQ_SRC_REALDATA ||
+                 g->ctrl_src_id < g->src_id[j];
+    }
 
     int rc;
     if (g->nw > 0 && (rc = g->d_mask.upload(g->masks))) return rc;
@@ -926,7 +944,7 @@ int rq_graph_build(const rq_graph_desc* d, rq_graph_t* out)
         (rc = g->d_p0.upload(g->p0)) || (rc = g->d_p1.upload(g->p1)) ||
         (rc = g->d_p2.upload(g->p2)) || (rc = g->d_arr_a.upload(g->arr_a)) ||
         (rc = g->d_arr_b.upload(g->arr_b)) || (rc = g->d_sink_ids.upload(g->sink_ids)) ||
-        (rc = g->d_csr_col_el.upload(g->csr_col_el)))
+        (rc = g->d_csr_col_el.upload(g->csr_col_el)) || (rc = g->d_cbf.upload(cbf)))
         return rc;
     if (g->multi && ((rc = g->d_lay_ptr.upload(g->lay_ptr)) || (rc = g->d_lay_end.upload(g->lay_end))))
         return rc;
@@ -987,7 +1005,7 @@ int rq_plan_info(rq_graph_t g, const rq_batch_desc* b, int64_t* info)
     info[3] = p.gwpb;
     info[4] = p.fw ? rq_fw_blocks_per_cu(p.nK, p.gcol16, p.fwm ? 0 : p.gwin, p.bits, p.gwpb, p.g_total,
                                           b->ctrl_kind == RQ_SRC_OPTPW)
-                   : rq_sweep_blocks_per_cu(p.mrg ? 0 : p.spl, p.nK, p.gcol16, p.gwin, p.log ? 1 + p.gs : 0,
+                   : rq_sweep_blocks_per_cu(p.mrg ? (p.gt ? -1 : 0) : p.spl, p.nK, p.gcol16, p.gwin, p.log ? 1 + p.gs : 0,
                                             p.bl ? 2 : p.bits, p.gwpb, p.g_total);
     info[5] = p.gcol_lds;
     info[6] = (int64_t)p.g_total;
@@ -1255,6 +1273,7 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
         sa.csr_ptr = g->d_csr_ptr.p;
         sa.csr_col = g->d_csr_col.p;
         sa.outdeg_f = g->d_outdeg_f.p;
+        sa.cbf_g = g->d_cbf.p;
         sa.fol = g->d_fol.p;
         sa.st_off = (const int64_t*)(ws + p.off_stoff);
         sa.capsum = p.capsum;
@@ -1351,7 +1370,7 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             }
             TimedLaunch tl(K_SWEEP, s);
             const hipError_t e = p.fw ? rq_launch_sweep_fw(sa, p.nK, p.gcol16, p.fwm ? 0 : p.gwin, p.bits, s)
-                                      : rq_launch_sweep(sa, p.mrg ? 0 : p.spl, p.nK, p.gcol16, p.log ? 1 + p.gs : 0,
+                                      : rq_launch_sweep(sa, p.mrg ? (p.gt ? -1 : 0) : p.spl, p.nK, p.gcol16, p.log ? 1 + p.gs : 0,
                                                         p.bl ? 2 : p.bits, s);
             if (e != hipSuccess) return RQ_EHIP;
         }

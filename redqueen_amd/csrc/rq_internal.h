@@ -67,6 +67,7 @@ struct SweepArgs {
     const int* csr_ptr;        // [n_str + 1]
     const int* csr_col;        // sink columns, edge-list order per source
     const int* outdeg_f;       // [n_str] edges into the controlled source's followers
+    const int* cbf_g;          // [n_str] the controller posts first at an equal time (GT instances)
     const int* fol;            // [n_fol] follower columns
     const int64_t* st_off;
     int64_t capsum;

@@ -123,7 +123,11 @@ __global__ __launch_bounds__(256) void rq_gen_streams(GenArgs a)
 // ============================================================================
 //    MRG = the fast sweep on merged streams (rq_merge_streams): a tile is the next 64
 //          entries of the replica's (t, stream) sequence, loaded one tile ahead.
-template <int SPL, int NK, class COL, int W, bool LOG, bool BITS, bool BL, bool GS = false, bool MRG = false>
+//    GT  = (merged streams only) the per-stream tables -- CSR row starts, follower
+//          out-degrees, controller tie flags, 1/c_j -- read from global memory instead of
+//          LDS: graphs of more streams than those tables fit in LDS (up to 65535).
+template <int SPL, int NK, class COL, int W, bool LOG, bool BITS, bool BL, bool GS = false, bool MRG = false,
+          bool GT = false>
 __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 1024))) void rq_sweep(SweepArgs a)
 {
     extern __shared__ double lds_g[];
@@ -147,8 +151,8 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
             const int jj = e / a.mstride, ww = e - jj * a.mstride;
             msk[e] = ww < a.nw ? a.masks[jj * a.nw + ww] : 0u;
         }
-    for (int j = threadIdx.x; j <= a.n_str; j += blockDim.x) cptr[j] = a.csr_ptr[j];
-    for (int j = threadIdx.x; j < a.n_str; j += blockDim.x) {
+    for (int j = threadIdx.x; j <= a.n_str && !GT; j += blockDim.x) cptr[j] = a.csr_ptr[j];
+    for (int j = threadIdx.x; j < a.n_str && !GT; j += blockDim.x) {
         odf[j] = a.outdeg_f[j];
         // the controller (a dynamic source) posts before a wall event at the same time
         // when that source is static (run_dynamic plays a static time only if it is
@@ -165,8 +169,12 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
     // one grid point: the controller's 1/c_j table is the same for every replica, so the
     // block holds one copy (its LDS goes to the sink columns instead of 8 per-wave copies)
     double* invc_sh = reinterpret_cast<double*>(base + a.lds_invc);
-    if (a.invc_shared)
+    if (a.invc_shared && !GT)
         for (int j = threadIdx.x; j < a.n_str; j += blockDim.x) invc_sh[j] = a.inv_c[j];
+    // the tables the sweep reads: LDS, or (GT) global
+    const int* cptr_r = GT ? a.csr_ptr : cptr;
+    const int* odf_r = GT ? a.outdeg_f : odf;
+    const int* cbf_r = GT ? a.cbf_g : cbf;
     __syncthreads();   // block-shared tables ready; no block barrier below this line
     char* wb = base + a.lds_wave + (size_t)w * a.lds_wave_stride;
     double* invc = a.invc_shared ? invc_sh : reinterpret_cast<double*>(wb);
@@ -190,8 +198,9 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
         uint32_t* tb = reinterpret_cast<uint32_t*>(wb + a.lds_rank_off);
         agl.init(tb, tb + a.nwl, fbl, a.nwl, lane, a.n_sinks);
     }
-    if (!a.invc_shared)
+    if (!a.invc_shared && !GT)
         for (int j = lane; j < a.n_str; j += 64) invc[j] = a.inv_c[(int64_t)g * a.n_str + j];
+    const double* invc_r = GT ? a.inv_c + (int64_t)g * a.n_str : invc;
     if (!BITS && !BL)
         for (int c = lane; c < a.n_sinks; c += 64) rank[c] = -1;   // NaN: no row yet
     // BL + MRG: stream stamps (the reset epoch the stream last played in) and the
@@ -291,7 +300,7 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
     const uint32_t oseed = a.ctrl_seed ? a.ctrl_seed[i] : a.ctrl_seed0 + (uint32_t)k;
     uint64_t ndraw = 0;   // wall events seen so far = the controller's draw index
     auto colat = [&](int e) -> int { return col_lds ? (int)col_l[e] : col_g[e]; };
-    const int fol0 = cptr[a.ctrl_idx];
+    const int fol0 = cptr_r[a.ctrl_idx];
     auto folat = [&](int f) -> int { return colat(fol0 + f); };
 
     Agg<NK> ag;
@@ -567,9 +576,9 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
         const bool act = lane < n;
         int e0 = 0, e1 = 0, od = 0;
         if (act) {
-            e0 = cptr[tj];
-            e1 = cptr[tj + 1];
-            od = odf[tj];
+            e0 = cptr_r[tj];
+            e1 = cptr_r[tj + 1];
+            od = odf_r[tj];
         }
         // ---- B: RedQueen controller over the tile (opt_model.py:536-556) ----
         //  candidate after wall event i: c_i = t_i + Exp(1)/c_{j_i}; the post fires
@@ -578,7 +587,7 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
         uint64_t ownm = 0;
         double ot = RQ_INF;
         if (opt && a.dbg != 3)
-            controller_tile<true>(n, act, tt, tj, invc, cbf, oseed, ndraw, opt_next, ownm, ot, pwc, pwm, a.n_seg,
+            controller_tile<true>(n, act, tt, tj, invc_r, cbf_r, oseed, ndraw, opt_next, ownm, ot, pwc, pwm, a.n_seg,
                             a.period);
         ownm = sgpr_u64(ownm);   // wave-uniform: phase C's bookkeeping stays scalar
         // ---- C: apply the tile's events in order ----
@@ -1108,16 +1117,16 @@ int rq_cu_count()
     return n;
 }
 template <int SPL, int NK, class COL, int W, bool LOG, bool BITS = false, bool BL = false, bool GS = false,
-          bool MRG = false>
+          bool MRG = false, bool GT = false>
 static int occ_t(int wpb, size_t lds);
 template <int SPL, int NK, class COL, int W, bool LOG, bool BITS = false, bool BL = false, bool GS = false,
-          bool MRG = false>
+          bool MRG = false, bool GT = false>
 static hipError_t launch_sweep_t(const SweepArgs& a, hipStream_t s)
 {
     unsigned blocks = (unsigned)((a.n_chunk + a.wpb - 1) / a.wpb);
     if (a.wq) {
         // persistent grid: every resident wave slot once, the rest from the queue
-        const int nb_c = occ_t<SPL, NK, COL, W, LOG, BITS, BL, GS, MRG>(a.wpb, a.lds_total);
+        const int nb_c = occ_t<SPL, NK, COL, W, LOG, BITS, BL, GS, MRG, GT>(a.wpb, a.lds_total);
         const unsigned cap = (unsigned)(nb_c > 0 ? nb_c : 1) * (unsigned)rq_cu_count();
         if (cap < blocks) blocks = cap;
     }
@@ -1126,7 +1135,7 @@ static hipError_t launch_sweep_t(const SweepArgs& a, hipStream_t s)
         if (!a.wq || cap < 1) return hipErrorInvalidValue;
         if (cap < blocks) blocks = cap;
     }
-    hipLaunchKernelGGL((rq_sweep<SPL, NK, COL, W, LOG, BITS, BL, GS, MRG>), dim3(blocks), dim3(64 * a.wpb), a.lds_total,
+    hipLaunchKernelGGL((rq_sweep<SPL, NK, COL, W, LOG, BITS, BL, GS, MRG, GT>), dim3(blocks), dim3(64 * a.wpb), a.lds_total,
                        s, a);
     return hipGetLastError();
 }
@@ -1158,15 +1167,15 @@ static hipError_t launch_sweep_c(const SweepArgs& a, int nK, int col16, int bits
 }
 
 // the sequential sweep on merged streams (> RQ_MAX_STREAMS sources): one instance per K
-// variant and per-sink state placement (GS)
+// variant and per-sink state placement (GS); per-stream tables in global memory (GT)
 template <bool GS>
 static hipError_t launch_sweep_lm(const SweepArgs& a, int nK, hipStream_t s)
 {
     switch (nK) {
-    case 1: return launch_sweep_t<1, 1, int, 4, true, false, false, GS, true>(a, s);
-    case 2: return launch_sweep_t<1, 2, int, 4, true, false, false, GS, true>(a, s);
-    case 3: return launch_sweep_t<1, 3, int, 4, true, false, false, GS, true>(a, s);
-    default: return launch_sweep_t<1, 4, int, 4, true, false, false, GS, true>(a, s);
+    case 1: return launch_sweep_t<1, 1, int, 4, true, false, false, GS, true, true>(a, s);
+    case 2: return launch_sweep_t<1, 2, int, 4, true, false, false, GS, true, true>(a, s);
+    case 3: return launch_sweep_t<1, 3, int, 4, true, false, false, GS, true, true>(a, s);
+    default: return launch_sweep_t<1, 4, int, 4, true, false, false, GS, true, true>(a, s);
     }
 }
 
@@ -1175,6 +1184,19 @@ template <int NK, class COL>
 static hipError_t launch_sweep_mk(const SweepArgs& a, hipStream_t s)
 {
     return launch_sweep_t<1, NK, COL, kGW, false, false, false, false, true>(a, s);
+}
+// the same with the per-stream tables in global memory (GT: more streams than the LDS
+// tables take; global columns, no sink bitsets)
+static hipError_t launch_sweep_mg(const SweepArgs& a, int nK, int bits, hipStream_t s)
+{
+    if (bits == 2) return launch_sweep_t<1, 1, int, kGW, false, false, true, false, true, true>(a, s);
+    if (bits) return hipErrorInvalidValue;
+    switch (nK) {
+    case 1: return launch_sweep_t<1, 1, int, kGW, false, false, false, false, true, true>(a, s);
+    case 2: return launch_sweep_t<1, 2, int, kGW, false, false, false, false, true, true>(a, s);
+    case 3: return launch_sweep_t<1, 3, int, kGW, false, false, false, false, true, true>(a, s);
+    default: return launch_sweep_t<1, 4, int, kGW, false, false, false, false, true, true>(a, s);
+    }
 }
 template <class COL>
 static hipError_t launch_sweep_m(const SweepArgs& a, int nK, int bits, hipStream_t s)
@@ -1218,7 +1240,8 @@ hipError_t rq_launch_sweep(const SweepArgs& a, int spl, int nK, int col16, int l
     // for 513..2048 sources, global columns only)
     // > 2048 sources: the sequential sweep on merged streams (global columns, 4-deep
     // rings the instance never fills)
-    if (log && spl == 0) return log == 2 ? launch_sweep_lm<true>(a, nK, s) : launch_sweep_lm<false>(a, nK, s);
+    if (log && spl <= 0) return log == 2 ? launch_sweep_lm<true>(a, nK, s) : launch_sweep_lm<false>(a, nK, s);
+    if (spl < 0) return launch_sweep_mg(a, nK, bits, s);   // merged streams, global tables
     if (log == 2)
         switch (spl) {
         case 1: return col16 ? launch_sweep_k<1, uint16_t, 8, true, true>(a, nK, s)
@@ -1249,10 +1272,10 @@ hipError_t rq_launch_sweep(const SweepArgs& a, int spl, int nK, int col16, int l
 
 // blocks of 64*wpb threads per CU the chosen sweep instance reaches with `lds`
 // bytes of dynamic LDS (VGPR, SGPR and LDS limits all applied by the runtime)
-template <int SPL, int NK, class COL, int W, bool LOG, bool BITS, bool BL, bool GS, bool MRG>
+template <int SPL, int NK, class COL, int W, bool LOG, bool BITS, bool BL, bool GS, bool MRG, bool GT>
 static int occ_t(int wpb, size_t lds)
 {
-    return rq_occupancy(rq_sweep<SPL, NK, COL, W, LOG, BITS, BL, GS, MRG>, 64 * wpb, lds);
+    return rq_occupancy(rq_sweep<SPL, NK, COL, W, LOG, BITS, BL, GS, MRG, GT>, 64 * wpb, lds);
 }
 template <int SPL, class COL, int W, bool LOG, bool GS = false>
 static int occ_k(int nK, int wpb, size_t lds)
@@ -1277,17 +1300,27 @@ static int occ_c(int nK, int col16, int W, int bits, int wpb, size_t lds)
 }
 int rq_sweep_blocks_per_cu(int spl, int nK, int col16, int W, int log, int bits, int wpb, size_t lds)
 {
-    if (log && spl == 0) {   // the sequential sweep on merged streams (launch_sweep_lm)
+    if (spl < 0 && !log) {   // merged streams, global tables (launch_sweep_mg)
+        if (bits == 2) return occ_t<1, 1, int, kGW, false, false, true, false, true, true>(wpb, lds);
+        if (bits) return 0;
+        switch (nK) {
+        case 1: return occ_t<1, 1, int, kGW, false, false, false, false, true, true>(wpb, lds);
+        case 2: return occ_t<1, 2, int, kGW, false, false, false, false, true, true>(wpb, lds);
+        case 3: return occ_t<1, 3, int, kGW, false, false, false, false, true, true>(wpb, lds);
+        default: return occ_t<1, 4, int, kGW, false, false, false, false, true, true>(wpb, lds);
+        }
+    }
+    if (log && spl <= 0) {   // the sequential sweep on merged streams (launch_sweep_lm)
         const bool gs = log == 2;
         switch (nK) {
-        case 1: return gs ? occ_t<1, 1, int, 4, true, false, false, true, true>(wpb, lds)
-                          : occ_t<1, 1, int, 4, true, false, false, false, true>(wpb, lds);
-        case 2: return gs ? occ_t<1, 2, int, 4, true, false, false, true, true>(wpb, lds)
-                          : occ_t<1, 2, int, 4, true, false, false, false, true>(wpb, lds);
-        case 3: return gs ? occ_t<1, 3, int, 4, true, false, false, true, true>(wpb, lds)
-                          : occ_t<1, 3, int, 4, true, false, false, false, true>(wpb, lds);
-        default: return gs ? occ_t<1, 4, int, 4, true, false, false, true, true>(wpb, lds)
-                           : occ_t<1, 4, int, 4, true, false, false, false, true>(wpb, lds);
+        case 1: return gs ? occ_t<1, 1, int, 4, true, false, false, true, true, true>(wpb, lds)
+                          : occ_t<1, 1, int, 4, true, false, false, false, true, true>(wpb, lds);
+        case 2: return gs ? occ_t<1, 2, int, 4, true, false, false, true, true, true>(wpb, lds)
+                          : occ_t<1, 2, int, 4, true, false, false, false, true, true>(wpb, lds);
+        case 3: return gs ? occ_t<1, 3, int, 4, true, false, false, true, true, true>(wpb, lds)
+                          : occ_t<1, 3, int, 4, true, false, false, false, true, true>(wpb, lds);
+        default: return gs ? occ_t<1, 4, int, 4, true, false, false, true, true, true>(wpb, lds)
+                           : occ_t<1, 4, int, 4, true, false, false, false, true, true>(wpb, lds);
         }
     }
     if (log == 2)

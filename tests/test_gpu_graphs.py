@@ -109,13 +109,15 @@ def _many_sources(n_src, n_sinks=120, deg=3, T=6.0, seed=11):
 
 
 @pytest.mark.parametrize("n_src,seq", [(600, False), (1500, False), (3000, False), (6000, False),
-                                       (600, True), (1500, True), (3000, True), (6000, True)])
+                                       (12000, False), (40000, False), (600, True), (1500, True),
+                                       (3000, True), (6000, True), (12000, True)])
 def test_more_than_512_sources(n_src, seq):
     """> 512 sources: the fast general sweep plays the two-level merged sequence
     (rq_merge_streams over groups of 512 streams, then over the groups' sequences; any
     number of sources up to 65535); the exact sequential sweep (sweep_mode 2) owns 16 / 32
-    sources per lane up to 2048 and plays the same merged sequence above that.  Event logs
-    and metrics == the engine oracle."""
+    sources per lane up to 2048 and plays the same merged sequence above that.  Past the
+    per-stream tables LDS takes (~8k streams) both read them from global memory (the GT
+    instances).  Event logs and metrics == the engine oracle."""
     torch, engine, graphs, O = _ctx()
     so = _many_sources(n_src)
     g = _graph(engine, so)
@@ -137,6 +139,25 @@ def test_more_than_512_sources(n_src, seq):
         r1 = g.run("opt", q=1.0, s=1.0, n_rep=4, ctrl_seed=2, world_seed=2, randomize=True, Ks=(1,))
         met_o, t_o, s_o = _oracle(O, _world_with_seeds(so, 2 + 3), ("opt", 2 + 3), (1,))
         _cmp_replica(r1, 3, met_o, t_o, s_o, (1,))
+
+
+def test_65000_sources_fast_equals_sequential():
+    """The largest graph the u16 stream ids take: the fast and the sequential sweep on
+    merged streams with global per-stream tables agree bit for bit (and the plan says so)."""
+    torch, engine, graphs, O = _ctx()
+    so = _many_sources(65000, T=2.0)
+    g = _graph(engine, so)
+    assert g.run("opt", q=1.0, s=1.0, n_rep=4, plan_only=True)["sources_per_lane"] == 0
+    a = g.run("opt", q=1.0, s=1.0, n_rep=4, ctrl_seed=3, world_seed=3, randomize=True, Ks=(1, 2),
+              event_log=True)
+    b = g.run("opt", q=1.0, s=1.0, n_rep=4, ctrl_seed=3, world_seed=3, randomize=True, Ks=(1, 2),
+              event_log=True, sweep_mode=2)
+    assert int(a.status.max().item()) == 0 and int((b.status & 3).max().item()) == 0
+    assert torch.equal(a.metrics, b.metrics) and torch.equal(a.counts, b.counts)
+    for r in range(4):
+        ta, sa = a.events(r)
+        tb, sb = b.events(r)
+        assert np.array_equal(ta, tb) and np.array_equal(sa, sb)
 
 
 def test_more_than_2048_sources_what_needs_the_sequential_sweep():
