@@ -69,11 +69,17 @@ constexpr int RP_LOG_HS = RP_LOG_H - 1;
 constexpr int RP_HMAX_S = RP_HS - RP_B - 1;
 constexpr int RP_SMALL_NK = 1;
 // rq_rp_fast rows per thread: where a workgroup has its CU to itself (no more dataframes
-// than CUs: 3 with the small table, 2 with the full one, whose LDS never shares its CU),
-// else 1 (two small-table workgroups per CU).  256 C3 dataframes: 4.35 ms at 1 row per
-// thread, 3.76 at 2, 3.62 at 3 (scripts/bench_paths.py replay_batch)
+// than CUs: RQ_RP_RFEW with the small table, 2 with the full one, whose LDS never shares
+// its CU), else 1 (two small-table workgroups per CU).  256 C3 dataframes: 4.35 ms at 1
+// row per thread, 3.76 at 2, 3.62 at 3 (scripts/bench_paths.py replay_batch); since the
+// per-wave list allocator (round 5) 2.79 ms at 3, 2.645 at 2
 #ifndef RQ_RP_RFEW
-#define RQ_RP_RFEW 3
+#define RQ_RP_RFEW 2
+#endif
+// the list walk reads two entries of each list per wait up to this many rows per thread
+// (256 C3 dataframes at 2 rows per thread: 2.645 -> 2.62 ms)
+#ifndef RQ_RP_KU2_MAXR
+#define RQ_RP_KU2_MAXR 2
 #endif
 constexpr int RP_RFEW = RQ_RP_RFEW;   // the small table's rows per thread, one workgroup per CU
 // the bucket word of a sink: rows of it in this batch (low RP_BB bits), list offset (next)
@@ -514,9 +520,9 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
                 }
             }
         };
-        // one row per thread: two entries of its list per LDS wait (1024 C3 dataframes
-        // 8.82 -> 8.35 ms); R rows: their R reads already share each wait
-        constexpr int KU = R == 1 ? 2 : 1;
+        // one or two rows per thread: two entries of each list per LDS wait (1024 C3
+        // dataframes 8.82 -> 8.35 ms); three rows: their three reads share each wait
+        constexpr int KU = R <= RQ_RP_KU2_MAXR ? 2 : 1;
         for (int k = 0; k < mmax; k += KU) {
             int v[KU][R];
 #pragma unroll
