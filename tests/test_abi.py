@@ -26,6 +26,14 @@ def test_exports_every_declared_symbol():
     assert set(names) == set(L.EXPORTED)
 
 
+def test_status_bits_match_the_header():
+    """The RQ_ST_* status bits the Python side tests equal include/rq.h's."""
+    src = open(os.path.join(ROOT, "include", "rq.h")).read()
+    bits = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define RQ_ST_(\w+)\s+(\d+)", src)}
+    assert bits == {"ROWS_OVERFLOW": L.ST_ROWS_OVERFLOW, "STREAM_OVERFLOW": L.ST_STREAM_OVERFLOW,
+                    "TIE": L.ST_TIE, "EMPTY": L.ST_EMPTY, "UNORDERED": L.ST_UNORDERED}, bits
+
+
 def test_version_and_errors():
     lib = L.lib()
     assert lib.rq_abi_version() == L.ABI_VERSION == 5
