@@ -16,7 +16,7 @@ lib = L.lib()
 lib.rq_phase_clock.argtypes = [C.POINTER(C.c_ulonglong)]
 names = ["top+load issue+barrier1", "C1 list walk", "A tickets+scan", "barriers 2-4, B, lists",
          "D1 scans", "C2 ranks", "prep next (hash)", "D2 barrier5+totals+stores"]
-nb = (int(ro[-1]) + 3071) // 3072
+nb = (int(ro[-1]) + 2047) // 2048
 for k in range(3):
     out = (C.c_ulonglong * 8)()
     lib.rq_phase_clock(out)   # clear
