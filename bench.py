@@ -194,8 +194,8 @@ def make_step(wl, g, so, R, world, rank, dev, Ks, group=None, force=False):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=3)
     # C5 default: two rounds of the 2048 waves the general sweep keeps resident
     ap.add_argument("--replicas", type=int, default=0,
                     help="replicas per GPU per step (default: C3/C2 10000, C5 4096)")
