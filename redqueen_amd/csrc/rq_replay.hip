@@ -374,6 +374,12 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
             }
         }
     };
+    // the next batch's rows: loaded in the middle of the batch before (after its prep,
+    // before its pivot-row stores, so the loop top issues no loads behind fresh stores --
+    // vmcnt retires in issue order), consumed by this batch's prep
+    double tn[R];
+    int64_t sn[R], kn[R], en[R];
+    double tnn = 0.0;   // the t right after the next batch
     if (nd > 0) {
         double t0[R];
         int64_t s0[R], k0[R], e0[R];
@@ -381,19 +387,15 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
         double ta = 0.0;
         if (tid == 0 && r0 + BR < r1) ta = a.t[r0 + BR];
         prep(r0, t0, s0, k0, e0, ta, 0.0, 0);
+        load(r0 + BR, tn, sn, kn, en);
+        if (tid == 0 && r0 + 2 * BR < r1) tnn = a.t[r0 + 2 * BR];
     }
 
     for (int64_t b0 = r0; b0 < r1; b0 += BR) {
-        // next batch (in flight across this batch's barriers)
-        double tn[R];
-        int64_t sn[R], kn[R], en[R];
-        load(b0 + BR, tn, sn, kn, en);
-        double tnn = 0.0;
-        if (tid == 0 && b0 + 2 * BR < r1) tnn = a.t[b0 + 2 * BR];
 
         // ---- A: neighbours of every row; its ticket in its sink's bucket ----
         __syncthreads();
-        RP_CLK(0);   // loop top, next batch's load issue, barrier 1
+        RP_CLK(0);   // loop top, barrier 1
         const int last = (int)((r1 - b0) < BR ? (r1 - b0) : BR);
         const double t_last = tb[last];
         const int64_t e_last = has_eid ? eb[last] : 0;
@@ -589,7 +591,11 @@ __device__ __forceinline__ void rp_fast_body(RpArgs a)
         // prep left the loads' registers pending on the back edge, and the loop top
         // waited on them -- vmcnt(0) between each row's loads)
         prep(b0 + BR, tn, sn, kn, en, tnn, t_last, e_last);
-        RP_CLK(6);   // next batch into LDS + its hash inserts
+        // the batch after next (in flight across the next batch's barriers)
+        load(b0 + 2 * BR, tn, sn, kn, en);
+        tnn = 0.0;
+        if (tid == 0 && b0 + 3 * BR < r1) tnn = a.t[b0 + 3 * BR];
+        RP_CLK(6);   // next batch into LDS + its hash inserts, the one after issued
 
         // ---- D: running totals in row order; the last row of a t-group emits its pivot row ----
         // this thread's rows: inclusive prefixes in registers; the threads' totals are
