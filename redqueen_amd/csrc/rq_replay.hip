@@ -1482,20 +1482,24 @@ __global__ __launch_bounds__(RP_B) void rq_rc_apply(RpArgs a)
         if (tid == 0 && c0 + RP_B < r1) ta = a.t[c0 + RP_B];
         prep(c0, t0, s0, k0, ta, t_bnd);
     }
+    // the next batch's row: loaded in the middle of the batch before, after its prep and
+    // before its pivot-row stores (rp_fast_body), at a clamped index (prep masks past c1)
+    double tn, tnn = 0.0;
+    int64_t sn, kn;
+    auto load_next = [&](int64_t nb0) __attribute__((always_inline)) {
+        const int64_t in = nb0 + tid;
+        const int64_t ic = in < c1 ? in : c1 - 1;   // c1 > c0: the loop runs
+        tn = a.t[ic];
+        sn = a.src[ic];
+        kn = a.sink[ic];
+        tnn = 0.0;
+        if (tid == 0 && nb0 + RP_B < r1) tnn = a.t[nb0 + RP_B];
+    };
+    if (c1 > c0) load_next(c0 + RP_B);
 
     for (int64_t b0 = c0; b0 < c1; b0 += RP_B) {
         const int64_t i = b0 + tid;
         const bool valid = i < c1;
-        const bool has_next = b0 + RP_B < c1;
-        const int64_t in = i + RP_B;
-        double tn = 0.0, tnn = 0.0;
-        int64_t sn = 0, kn = 0;
-        if (has_next && in < c1) {
-            tn = a.t[in];
-            sn = a.src[in];
-            kn = a.sink[in];
-        }
-        if (tid == 0 && b0 + 2 * RP_B < r1) tnn = a.t[b0 + 2 * RP_B];
 
         // ---- A: neighbours of every row; its ticket in its sink's bucket ----
         __syncthreads();
@@ -1597,7 +1601,8 @@ __global__ __launch_bounds__(RP_B) void rq_rc_apply(RpArgs a)
                 sl->bucket = 0;
             }
         }
-        if (has_next) prep(b0 + RP_B, tn, sn, kn, tnn, t_last);
+        prep(b0 + RP_B, tn, sn, kn, tnn, t_last);
+        load_next(b0 + 2 * RP_B);
 
         // ---- D: running totals in row order; the last row of a t-group emits its pivot row ----
         x.s = scan_add_i64_of_i32((int)x.s);
