@@ -151,6 +151,37 @@ def pmc_traffic(workload, R, plan):
     return None, None, None
 
 
+def serial_probe(L, g, pkw, chunk, steps):
+    """Per-launch kernel times with every kernel alone on the chip, measured live: the
+    timed step's batch (same replicas per launch: the plan's chunk) with the library's
+    pipeline off (RQ_PIPE=1: every chunk's generation, merge, sweep and scan in order
+    on the caller's one stream) and nothing else queued, HIP events around each launch.
+    In the timed region two caller streams' kernels share the chip and stretch each
+    launch's HIP-event time; these are the durations the kernel itself needs (the same
+    figure as a rocprofv3 kernel trace under AMD_SERIALIZE_KERNEL=3).
+    Returns (ms per launch [gen, sweep, scan, -, merge], launches)."""
+    old = os.environ.get("RQ_PIPE")
+    os.environ["RQ_PIPE"] = "1"
+    try:
+        g.run("opt", ctrl_seed=7_000_000, world_seed=7_000_000, check=False, chunk=chunk, **pkw)
+        torch.cuda.synchronize()
+        L.lib().rq_timing(1)
+        for k in range(steps):
+            g.run("opt", ctrl_seed=7_000_001 + k, world_seed=7_000_001 + k, check=False,
+                  chunk=chunk, **pkw)
+        torch.cuda.synchronize()
+        ms = np.zeros(5)
+        nl = np.zeros(5, dtype=np.int64)
+        L.lib().rq_timing_read(ms.ctypes.data_as(L._pd), nl.ctypes.data_as(L._pi64))
+        L.lib().rq_timing(0)
+    finally:
+        if old is None:
+            os.environ.pop("RQ_PIPE", None)
+        else:
+            os.environ["RQ_PIPE"] = old
+    return ms / np.maximum(nl, 1), nl
+
+
 def make_step(wl, g, so, R, world, rank, dev, Ks, group=None, force=False):
     """The bench step of a workload, on this rank: (step(k) -> (this rank's BatchResult,
     ensemble means), replicas per step over all ranks, plan kwargs).
@@ -209,6 +240,9 @@ def main():
                          "0 = 2, except C5, whose 164 GB step workspace does not fit twice "
                          "in HBM (the second stream would plan smaller chunks: same mean "
                          "rate, mixed launch sizes; gpurun_out/r05m)")
+    ap.add_argument("--probe-steps", type=int, default=0,
+                    help="steps of the serialised probe after the timed region (per-launch "
+                         "kernel times with each kernel alone on the chip; default 3, C5 1)")
     ap.add_argument("--dist", action="store_true",
                     help="at N = 1 too: a world-size-1 RCCL group, the step's all-gather "
                          "runs through it")
@@ -324,9 +358,14 @@ def main():
     value = replicas / el
     ev_rate = local_ev / el
 
+    # the kernels alone (outside the timed region): the roofline's launch duration
+    sms, snl = serial_probe(L, g, pkw, plan["chunk"],
+                            a.probe_steps or (1 if a.workload == "c5" else 3))
+
     # roofline of the dominant kernel (the sweep), per launch, this rank
     n_sweep = max(1, int(nl[1]))
     sweep_ms = ms[1] / n_sweep
+    sweep_ms_serial = float(sms[1]) if snl[1] else None
     # per LAUNCH: a step runs one launch of each kernel per replica chunk (the engine's
     # pipelined chunks, rq_run_batch), so the step's bytes are split over its launches
     lps = n_sweep / a.steps
@@ -339,7 +378,10 @@ def main():
     b_wall = MRG_SWEEP_B_PER_WALL_EVENT if merged else SWEEP_B_PER_WALL_EVENT
     sweep_bytes = (0 if fused else b_wall * (ev_rank - posts_step)) + \
         SWEEP_B_PER_ROW * rows_step
-    achieved = sweep_bytes / (sweep_ms * 1e-3) / 1e9
+    achieved_live = sweep_bytes / (sweep_ms * 1e-3) / 1e9
+    # the headline fraction: the kernel's own launch duration (serialised probe); the
+    # overlapped HIP-event time of the timed region is kept as frac_live
+    achieved = sweep_bytes / (sweep_ms_serial * 1e-3) / 1e9 if sweep_ms_serial else achieved_live
     scan_ms = ms[2] / max(1, int(nl[2]))
     gen_ms = ms[0] / max(1, int(nl[0]))
     scan_gbs = SCAN_B_PER_ROW * rows_step / (scan_ms * 1e-3) / 1e9 if scan_ms > 0 else None
@@ -352,8 +394,8 @@ def main():
     traffic, traffic_src, issue = pmc_traffic(a.workload, R, plan)
     if issue and "issue_frac" in issue:
         # the same ceiling over this run's own HIP-event launch time at the PMC run's clock
-        issue["issue_frac_2400mhz_bench_time"] = issue["valu_insts"] / (
-            N_CU * 4 * 2.4e9 / 2.0 * sweep_ms * 1e-3)
+        issue["issue_frac_2400mhz_probe_time"] = issue["valu_insts"] / (
+            N_CU * 4 * 2.4e9 / 2.0 * (sweep_ms_serial or sweep_ms) * 1e-3)
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
@@ -392,13 +434,24 @@ def main():
             "events_per_replica": local_ev / replicas,
             "overflow": int(status.item()),
             "tie_replicas": int(ties.item()),
+            # HIP-event time per launch inside the timed region (two caller streams' kernels
+            # share the chip: each launch's time is stretched by the overlap)
             "kernels_ms_per_launch": {"gen_streams": gen_ms, "merge_streams": merge_ms, "sweep": sweep_ms,
                                       "scan": scan_ms},
+            # the same launches alone on the chip (serial_probe: pipeline off, one stream)
+            "kernels_ms_per_launch_serial": {"gen_streams": float(sms[0]), "merge_streams": float(sms[4]),
+                                             "sweep": sweep_ms_serial, "scan": float(sms[2]),
+                                             "launches": [int(x) for x in snl]},
             "launches_per_step": lps,
             "caller_streams": len(streams),
             "sweep_plan": plan,
             "roofline": {"bound": "hbm", "kernel": "rq_sweep", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "duration_ms": sweep_ms_serial or sweep_ms,
+                         "duration_source": "serial_probe: the launch alone on the chip, HIP events"
+                                            if sweep_ms_serial else "timed region, HIP events",
+                         "bytes_per_launch": sweep_bytes,
+                         "achieved_live": achieved_live, "frac_live": achieved_live / HBM_PEAK_GBS,
                          "traffic": traffic,
                          "traffic_source": traffic_src,
                          # what does bound it: SQ issue / wait shares of the wave cycles and

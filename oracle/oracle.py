@@ -256,17 +256,24 @@ class Scenario:
 
     def expand(self, ev_t, ev_dt, ev_src):
         """Events -> reference df columns (State.get_dataframe, opt_model.py:85-97)."""
-        sinks = {}
-        for e in self.edges:
-            sinks.setdefault(e[0], []).append(e[1])
-        eid, td, src, t, sink = [], [], [], [], []
-        for k in range(len(ev_t)):
-            for y in sinks.get(int(ev_src[k]), []):
-                eid.append(100 + k); td.append(ev_dt[k]); src.append(ev_src[k])
-                t.append(ev_t[k]); sink.append(y)
-        return dict(event_id=np.asarray(eid, dtype=np.int64), time_delta=np.asarray(td),
-                    src_id=np.asarray(src, dtype=np.int64), t=np.asarray(t),
-                    sink_id=np.asarray(sink, dtype=np.int64))
+        # one row per (event, sink): events in play order, each event's sinks in
+        # edge_list order (duplicates kept) -- vectorised as a CSR gather
+        ev_src = np.asarray(ev_src, dtype=np.int64)
+        if self.edge_src.size == 0:
+            ev_src = ev_src[:0]
+        order = np.argsort(self.edge_src, kind="stable")          # edge-list order per source
+        srcs, first, deg = np.unique(self.edge_src[order], return_index=True, return_counts=True)
+        col = self.edge_sink[order]
+        k = np.searchsorted(srcs, ev_src)
+        known = (k < len(srcs)) & (srcs[np.minimum(k, len(srcs) - 1)] == ev_src)
+        d = np.where(known, deg[np.minimum(k, len(srcs) - 1)], 0)
+        beg = np.where(known, first[np.minimum(k, len(srcs) - 1)], 0)
+        ev = np.repeat(np.arange(len(ev_src)), d)
+        within = np.arange(ev.size) - np.repeat(np.cumsum(d) - d, d)
+        return dict(event_id=(100 + ev).astype(np.int64),
+                    time_delta=np.asarray(ev_dt, dtype=np.float64)[ev],
+                    src_id=ev_src[ev], t=np.asarray(ev_t, dtype=np.float64)[ev],
+                    sink_id=col[np.repeat(beg, d) + within].astype(np.int64))
 
 
 def state_time_deltas(t, start=0.0):

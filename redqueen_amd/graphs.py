@@ -123,6 +123,15 @@ def c5_small():
                            kinds=("Hawkes",), world_rate=0.5, alpha=1.0, beta=2.0)
 
 
+def c5_mid():
+    """C5's source side at C5's horizon, small enough for a handful of reference runs
+    (minutes each): 500 bursty Hawkes broadcasters (l_0 = 0.5, alpha = 1, beta = 2), 100
+    followers of degree 5, T = 1000, q = 1e4 (the trim keeps the ~316 broadcasters that
+    reach a follower).  The reference-run replay fixture `scale_logs.npz` uses it."""
+    return followers_graph(num_followers=100, num_sources=500, degree=5, end_time=1000.0,
+                           kinds=("Hawkes",), world_rate=0.5, alpha=1.0, beta=2.0)
+
+
 def g120():
     """A > 64-source world (the general sweep's instances, like C5) small enough for the
     reference to run thousands of replicas: 60 followers, 120 broadcasters (Poisson2

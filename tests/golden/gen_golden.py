@@ -24,6 +24,9 @@ installed and there is no network) and records, as plain data:
   sweepq.npz       utils.sweep_q (sequential) on std_poisson(1, 100): q_init, the
                    returned q and calc_q_capacity_iter per (q, seed);
                    rank_of_src_in_df tables and u_int_opt values
+  scale_logs.npz   (--scale-logs) whole reference runs at the headline scale: 8 C3 runs
+                   and 2 runs of graphs.c5_mid (500 bursty Hawkes sources, T = 1000):
+                   event logs, df shape + column crc32s, utils.py's metrics on the df
   dist_c3.npz      (--c3-dist N) N-replica RedQueen ensemble on the C3 bench network
   dist_g120.npz    (--g120-dist N) N-replica RedQueen ensemble on graphs.g120 (> 64
                    sources: the general sweep's instances)
@@ -768,6 +771,58 @@ def gen_c3_dist(n, start=0, procs=0):
     os.replace(tmp, path)
 
 
+# Reference runs at the headline scale, kept whole: the event log (t, time_delta, src),
+# the df's shape and column checksums, and what utils.py returns on that df.  C3 replica r
+# is dist_c3's replica r (world randomize_other_sources(5000 r), RedQueen seed 5000 r);
+# c5_mid replica r runs world randomize_other_sources(100000 r), RedQueen seed 100000 r + 1.
+SCALE_RUNS = {"c3": (8, C3_SEED_STRIDE, 0), "c5m": (2, 100000, 1)}
+
+
+def _crc(a):
+    import zlib
+    return zlib.crc32(np.ascontiguousarray(a).tobytes())
+
+
+def _scale_worker(args):
+    name, r = args
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from redqueen_amd import graphs as G
+    so = SimOpts(**(G.c3() if name == "c3" else G.c5_mid()))
+    _, stride, off = SCALE_RUNS[name]
+    u = stride * r
+    m = so.randomize_other_sources(u).create_manager_with_opt(seed=u + off)
+    m.run_dynamic()
+    df = m.state.get_dataframe()
+    met, own, world = metrics(df, so)
+    t, dt, src = events_of(df)
+    shape = np.asarray([len(df), own, world, m.state.get_num_events(), df.sink_id.nunique()],
+                       dtype=np.int64)
+    crc = np.asarray([_crc(df.t.values), _crc(df.src_id.values.astype(np.int64)),
+                      _crc(df.sink_id.values.astype(np.int64)),
+                      _crc(df.event_id.values.astype(np.int64))], dtype=np.int64)
+    return name, r, t, dt, src, met, shape, crc
+
+
+def gen_scale_logs(procs=0):
+    """scale_logs.npz: SCALE_RUNS through the reference, every event's (t, src_id) kept (the tests
+    rebuild the df with the reference's row layout, check it against the recorded shape
+    and crc32 of each column, and replay it)."""
+    jobs = [(n, r) for n, (cnt, _, _) in SCALE_RUNS.items() for r in range(cnt)]
+    jobs.sort(key=lambda j: j[0] != "c5m")   # the long runs first
+    rec = {}
+    with mp.Pool(procs or os.cpu_count()) as pool:
+        for name, r, t, dt, src, met, shape, crc in pool.imap_unordered(_scale_worker, jobs):
+            k = "%s_%d" % (name, r)
+            # time_delta is not a metric input: the tests rebuild the df without it
+            rec.update({k + "_t": t, k + "_src": src.astype(np.int32), k + "_met": met,
+                        k + "_shape": shape, k + "_crc": crc})
+            print("scale run", k, shape.tolist(), flush=True)
+    rec["runs"] = np.asarray(sorted("%s_%d" % j for j in jobs))
+    rec["shape_cols"] = np.asarray(["rows", "own", "world", "events", "sinks"])
+    rec["crc_cols"] = np.asarray(["t", "src_id", "sink_id", "event_id"])
+    np.savez_compressed(os.path.join(HERE, "scale_logs.npz"), **rec)
+
+
 # C4 corners: README graph at the extreme q of the reference's grid (opt_runs.py:289-291)
 # x three follower-significance vectors (the notebook's sim_opts_unequal (0.5, 1.5),
 # opt_broadcast.ipynb:5550, and a strongly unequal (1, 0.25)).  Replica r runs world
@@ -995,12 +1050,18 @@ if __name__ == "__main__":
                     help="only dist_knock.npz: N reference runs of the reactive plugin beside RedQueen")
     ap.add_argument("--hawkes-seed0", action="store_true",
                     help="only dist_hawkes0.npz: the discarded 10k seed0-0 Hawkes world draw")
+    ap.add_argument("--scale-logs", action="store_true",
+                    help="only scale_logs.npz: whole reference runs of C3 and c5_mid")
     a = ap.parse_args()
     steps = {"npsum": gen_npsum, "draws": gen_draws, "readme": gen_readme, "kats": gen_kats,
              "adv": gen_adversarial, "graphs": gen_graphs, "frac": gen_frac,
              "oracle": gen_oracle, "sweepq": gen_sweepq, "sig": gen_sig, "realdata": gen_realdata,
              "plugin": gen_plugin, "errors": gen_errors, "dynplugin": gen_dynplugin}
-    if a.c4_dist:
+    if a.scale_logs:
+        gen_scale_logs(a.procs)
+        print("done scale logs", flush=True)
+        a.worlds = True   # nothing else
+    elif a.c4_dist:
         gen_c4_dist(a.c4_dist, a.c4_start, a.procs)
         print("done c4 dist", flush=True)
         a.worlds = True   # nothing else
