@@ -63,7 +63,7 @@
 extern "C" {
 #endif
 
-#define RQ_ABI_VERSION 5
+#define RQ_ABI_VERSION 6
 #define RQ_MAX_K 4 /* at most 4 K values (perf_opts.Ks, opt_runs.py:31-38) per run */
 
 typedef enum {
@@ -93,11 +93,17 @@ typedef struct rq_source_desc {
     int32_t n_arr;       /* PWCONST: #segments; REALDATA: #times                           */
     int64_t src_id;
     uint32_t seed;       /* kwargs['seed'] (RandomState seed, opt_model.py:329)            */
-    uint32_t reserved;
+    uint32_t flags;      /* RQ_SRCF_* (ABI v6; was reserved, 0)                            */
     double p0, p1, p2;   /* POISSON/POISSON2: rate; HAWKES: l_0, alpha, beta               */
     const double* a;     /* host: PWCONST change_times[n_arr]; REALDATA times[n_arr]       */
     const double* b;     /* host: PWCONST rates[n_arr]                                     */
 } rq_source_desc;
+/* rq_source_desc.flags: RQ_SRCF_DYNAMIC on an RQ_SRC_REALDATA source = its times are a
+   DYNAMIC broadcaster's (a registered plugin with is_dynamic, opt_model.py:259-260,
+   replayed from its times): at an equal time it plays before every static source and
+   among the dynamic ones (the controller included) in src_id order
+   (opt_model.py:279-281, :289-290), like the built-in Poisson / Hawkes. */
+#define RQ_SRCF_DYNAMIC 1
 
 typedef struct rq_graph_desc {
     int32_t n_sources;                /* SimOpts.other_sources, in list order          */
@@ -218,6 +224,15 @@ typedef struct rq_batch_desc {
        allocator) passes its reclaimable total here so both calls plan alike.  The
        environment variable RQ_WS_BUDGET_GB caps either. */
     int64_t ws_budget;
+    /* Replica list (ABI v6): host [n_local] global ids (i = g * n_rep + r, each in
+       [0, n_grid * n_rep)); the call runs exactly these replicas, output k = replica
+       rep_idx[k] -- seeds, grid point and per-replica inputs (ctrl_seed, world_seed,
+       ctrl_rate, rd_*) come from the global id as in the full batch, so a replica gives
+       the same bits alone as inside its batch.  Requires replica0 = 0, rep_cnt = 0 and
+       n_local > 0.  The caller reruns only a batch's flagged replicas with it (an
+       RQ_ST_*_OVERFLOW replica at a larger cap_scale, an RQ_ST_TIE one on the exact
+       sequential sweep, sweep_mode 2).  NULL: the replica space above. */
+    const int64_t* rep_idx;
 } rq_batch_desc;
 #define RQ_MAX_RD 64
 

@@ -28,7 +28,7 @@ KIND = {"Poisson": POISSON, "Poisson2": POISSON2, "Hawkes": HAWKES,
 
 class _Source(C.Structure):
     _fields_ = [("kind", C.c_int32), ("n_arr", C.c_int32), ("src_id", C.c_int64),
-                ("seed", C.c_uint32), ("p0", C.c_double), ("p1", C.c_double),
+                ("seed", C.c_uint32), ("flags", C.c_uint32), ("p0", C.c_double), ("p1", C.c_double),
                 ("p2", C.c_double), ("a", C.POINTER(C.c_double)), ("b", C.POINTER(C.c_double))]
 
 
@@ -215,6 +215,7 @@ class Scenario:
                                       b=kw["rates"]))
             elif k == REALDATA:
                 srcs.append(self._src(k, kw["src_id"], 0, a=kw["times"]))
+                srcs[-1].flags = 1 if kw.get("dynamic") else 0
             else:
                 raise ValueError(name)
         self.sources = srcs

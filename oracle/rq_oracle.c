@@ -844,6 +844,15 @@ static double optpw_sample(double tt, const double* row, double smax, int64_t S,
     return INFINITY;
 }
 
+/* 1: source j plays its equal-time events after the dynamic sources' (a static source,
+   opt_model.py:289-290); source 0 with a RedQueen / OptPWSignificance controller is dynamic */
+static int engine_static(const rqo_scenario* sc, int j, int opt)
+{
+    const rqo_source* s = &sc->sources[j];
+    if (j == 0 && opt) return 0;
+    return s->kind == RQO_POISSON2 || s->kind == RQO_PWCONST || (s->kind == RQO_REALDATA && !(s->flags & 1u));
+}
+
 int rqo_engine_run(const rqo_scenario* sc, rqo_events* ev)
 {
     int rc = -4;
@@ -921,14 +930,11 @@ int rqo_engine_run(const rqo_scenario* sc, rqo_events* ev)
                 if (j == 0 && opt) tj = opt_next;
                 else tj = head[j] < st[j].n ? st[j].v[head[j]] : INFINITY;
                 int64_t id = sc->sources[j].src_id;
-                /* ties: the (dynamic) controller before a static wall source, else src_id
-                   (opt_model.py:279-281, :289-290) */
-                int beats = id < bid;
-                if (bj >= 0 && tj == bt && opt && (j == 0 || bj == 0)) {
-                    const int other = j == 0 ? sc->sources[bj].kind : sc->sources[j].kind;
-                    if (other == RQO_POISSON2 || other == RQO_PWCONST || other == RQO_REALDATA)
-                        beats = j == 0;
-                }
+                /* ties (opt_model.py:279-281, :289-290): every dynamic source -- the
+                   RedQueen controller, Poisson, Hawkes, a dynamic broadcaster's replayed
+                   times -- before every static one, src_id order within each class */
+                const int cj = engine_static(sc, j, opt), cb = bj >= 0 ? engine_static(sc, bj, opt) : 0;
+                const int beats = cj != cb ? cj < cb : id < bid;
                 if (tj < bt || (tj == bt && bj >= 0 && beats)) { bt = tj; bj = j; bid = id; }
             }
             if (bj < 0 || !(bt <= sc->end_time)) break;

@@ -53,6 +53,8 @@ typedef struct {
                            OPTPW: #significance segments S */
     int64_t src_id;
     uint32_t seed;
+    uint32_t flags;     /* 1: a REALDATA source that replays a DYNAMIC broadcaster's times
+                           (rq.h RQ_SRCF_DYNAMIC): ties order it as a dynamic source */
     double p0, p1, p2;  /* POISSON*: rate; HAWKES: l_0, alpha, beta; OPT: q; OPTPW: q, period */
     const double* a;    /* PWCONST change_times; REALDATA times; OPT s (sorted followers);
                            OPTPW s_pw [sorted followers][S] */

@@ -17,7 +17,8 @@ RQ_OK, RQ_EINVAL, RQ_EOVERFLOW, RQ_EHIP, RQ_ENOMEM, RQ_EUNSORTED, RQ_EUNSUPPORTE
 SRC_NONE, SRC_POISSON, SRC_POISSON2, SRC_HAWKES, SRC_PWCONST, SRC_REALDATA, SRC_OPT, SRC_OPTPW = range(8)
 ST_ROWS_OVERFLOW, ST_STREAM_OVERFLOW, ST_TIE, ST_EMPTY, ST_UNORDERED = 1, 2, 4, 8, 16
 RUN_EVENT_LOG = 1
-ABI_VERSION = 5
+ABI_VERSION = 6
+SRCF_DYNAMIC = 1   # rq_source_desc.flags: a RealData source that is a dynamic broadcaster's times
 REPLAY_LARGE = 1
 REPLAY_CHUNKED = 2
 REPLAY_CHUNK_ROWS = 4096   # RC_L: rows per workgroup of the chunked replay
@@ -33,7 +34,7 @@ _pu32 = C.POINTER(C.c_uint32)
 
 class SourceDesc(C.Structure):
     _fields_ = [("kind", C.c_int32), ("n_arr", C.c_int32), ("src_id", C.c_int64),
-                ("seed", C.c_uint32), ("reserved", C.c_uint32), ("p0", C.c_double),
+                ("seed", C.c_uint32), ("flags", C.c_uint32), ("p0", C.c_double),
                 ("p1", C.c_double), ("p2", C.c_double), ("a", _pd), ("b", _pd)]
 
 
@@ -56,7 +57,7 @@ class BatchDesc(C.Structure):
                 ("n_seg", C.c_int32), ("period", C.c_double), ("s_pw", _pd),
                 ("n_rd", C.c_int32), ("rd_src_id", _pi64), ("rd_cap", _pi64), ("rd_times", _P),
                 ("rd_off", _P), ("rep_lo", C.c_int64), ("rep_cnt", C.c_int64),
-                ("ws_budget", C.c_int64)]
+                ("ws_budget", C.c_int64), ("rep_idx", _pi64)]
 
 
 class Outputs(C.Structure):

@@ -154,9 +154,11 @@ struct rq_graph {
     int n_str = 0, ctrl_idx = -1, n_sinks = 0, n_fol = 0;
     int64_t n_edges = 0, ctrl_src_id = 0;
     double start = 0.0, end = 0.0;
-    // per stream (sorted by src_id); the controlled slot has kind RQ_SRC_NONE
+    // per stream (dynamic sources by src_id, then static ones by src_id); the controlled
+    // slot has kind RQ_SRC_NONE
     std::vector<int64_t> src_id;
     std::vector<int> kind, orig_idx, arr_off, arr_n;
+    std::vector<int> is_static;   // 1: a static source (equal times play after the dynamic ones)
     std::vector<uint32_t> seed;
     std::vector<double> p0, p1, p2, arr_a, arr_b;
     std::vector<int> csr_ptr, csr_col, outdeg_f, fol;
@@ -171,6 +173,11 @@ struct rq_graph {
     // occurrences (layer 1), ...; every layer has distinct sinks.  lay_end[lay_ptr[j] ..
     // lay_ptr[j+1]) are the CSR ends of stream j's layers.  multi: some row has > 1 layer.
     bool multi = false, ctrl_dup = false;
+    // two of the graph's own RealData times are equal -- among the wall sources
+    // (rd_ties), or with the controlled slot's replayed times too (rd_ties_ctrl, runs with
+    // an RQ_SRC_REALDATA controller): every replica meets that tie, so such runs go to the
+    // exact sequential sweep directly
+    bool rd_ties = false, rd_ties_ctrl = false;
     std::vector<int> lay_ptr, lay_end;
     DevBuf<int> d_lay_ptr, d_lay_end;
     // per-stream sink bitsets (32 sinks per word) for the K=1 bitset sweep, n_sinks <= 2048
@@ -241,7 +248,7 @@ struct Plan {
     size_t off_set0 = 0, set_stride = 0, off_ord = 0;
     size_t off_pwc = 0, off_pwmax = 0;
     size_t off_invc = 0, off_streams = 0, off_slen = 0, off_rt = 0, off_rs = 0, off_rv = 0,
-           off_rc = 0, off_sall = 0, off_wq = 0, off_stoff = 0, off_cap = 0, off_rdk = 0, off_gs = 0,
+           off_rc = 0, off_sall = 0, off_wq = 0, off_stoff = 0, off_cap = 0, off_rdk = 0, off_repidx = 0, off_gs = 0,
            total = 0;
 };
 
@@ -336,6 +343,13 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p, double budget)
     if (b->replica0 < 0 || b->n_local < 0 || b->replica0 + b->n_local > Rall) return RQ_EINVAL;
     p->R = b->n_local > 0 ? b->n_local : Rall - b->replica0;
     if (p->R < 1) return RQ_EINVAL;
+    // a replica list (ABI v6): n_local global ids of the whole n_grid x n_rep grid
+    if (b->rep_idx) {
+        if (b->replica0 != 0 || b->rep_cnt != 0 || b->n_local < 1) return RQ_EINVAL;
+        const int64_t nall = (int64_t)b->n_grid * b->n_rep;
+        for (int64_t k = 0; k < b->n_local; ++k)
+            if (b->rep_idx[k] < 0 || b->rep_idx[k] >= nall) return RQ_EINVAL;
+    }
     p->chunk = b->chunk > 0 ? std::min<int64_t>(b->chunk, p->R) : std::min<int64_t>(p->R, 16384);
     p->cap.assign(g->n_str, 0);
     p->st_off.assign(g->n_str, 0);
@@ -410,13 +424,14 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p, double budget)
     const size_t per_wave = (size_t)p->n_sinks_pad * 4;
     p->wpb = per_wave * 4 <= 64 * 1024 ? 4 : per_wave * 2 <= 80 * 1024 ? 2 : 1;
 
-    // the sequential exact variant also whenever equal event times are likely:
-    // RealData streams (recorded times repeat); the fast sweep flags RQ_ST_TIE
-    bool has_rd = b->ctrl_kind == RQ_SRC_REALDATA;
-    for (int k : g->kind) has_rd = has_rd || k == RQ_SRC_REALDATA;
-    // the fast sweeps (fused and general) write the event log themselves
-    p->log = b->max_events >= 0 ||
-             b->sweep_mode == 2 || (has_rd && b->sweep_mode != 1 && b->sweep_mode != 5);
+    // the sequential exact variant when equal event times are certain: the graph's own
+    // RealData times (every replica plays them) repeat a time; otherwise RealData and
+    // the per-replica plugin streams play on the fast sweeps, which flag RQ_ST_TIE on any
+    // equal-time pair, and the caller reruns the flagged replicas on the exact sequential
+    // sweep (rq_batch_desc.rep_idx).  max_events cuts the fast sweeps' tiles
+    // (truncate_tile); the fast sweeps write the event log themselves.
+    const bool rd_ties = ck == RQ_SRC_REALDATA ? g->rd_ties_ctrl : g->rd_ties;
+    p->log = b->sweep_mode == 2 || (rd_ties && b->sweep_mode != 1 && b->sweep_mode != 5);
     for (int q = 0; q < b->nK; ++q) p->log = p->log || b->Ks[q] > 32767;   // int16 ranks
     // a multigraph (duplicate edges make fractional pivot cells, the exact sequential
     // sweep's business); > 512 sources: the fast general sweep plays the two-level merged
@@ -683,6 +698,8 @@ void plan_layout(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     p->off_stoff = o;   o = o + sizeof(int64_t) * g->n_str;
     p->off_cap = o;     o = o + sizeof(int) * g->n_str;
     p->off_rdk = o;     o = o + sizeof(int) * g->n_str;
+    o = align_up(o, 8);
+    p->off_repidx = o;  o = o + sizeof(int64_t) * (b->rep_idx ? (size_t)p->R : 0);
     const size_t nseg = b->ctrl_kind == RQ_SRC_OPTPW ? (size_t)b->n_seg : 0;
     o = align_up(o, 8);
     p->off_pwc = o;     o = o + sizeof(double) * (size_t)b->n_grid * g->n_str * nseg;
@@ -780,22 +797,36 @@ int rq_graph_build(const rq_graph_desc* d, rq_graph_t* out)
     std::unordered_map<int64_t, int> col;
     for (int c = 0; c < g->n_sinks; ++c) col[sinks[c]] = c;
 
-    // sources: other sources + the controlled slot, sorted by src_id
-    struct S { int64_t id; int orig; };
+    // sources: other sources + the controlled slot, in the order run_dynamic plays equal
+    // times (opt_model.py:279-290): the dynamic sources (Poisson, Hawkes, a dynamic
+    // broadcaster's replayed times) by src_id, then the static ones (Poisson2,
+    // PiecewiseConst, RealData; the controlled slot -- a RedQueen controller's ties are
+    // the sweep's cbf flags, the other controlled kinds are static) by src_id.  The merge
+    // and the sequential sweep play equal times in stream order.
+    struct S { int64_t id; int orig; int cls; };
     std::vector<S> order;
     for (int k = 0; k < d->n_sources; ++k) {
         const rq_source_desc& s = d->sources[k];
         if (s.kind < RQ_SRC_POISSON || s.kind > RQ_SRC_REALDATA) return RQ_EUNSUPPORTED;
+        if ((s.flags & ~(uint32_t)RQ_SRCF_DYNAMIC) || ((s.flags & RQ_SRCF_DYNAMIC) && s.kind != RQ_SRC_REALDATA))
+            return RQ_EINVAL;
         if (s.kind == RQ_SRC_PWCONST || s.kind == RQ_SRC_REALDATA) {
             if (s.n_arr < (s.kind == RQ_SRC_PWCONST ? 1 : 0) || (s.n_arr > 0 && !s.a)) return RQ_EINVAL;
             if (s.kind == RQ_SRC_PWCONST && !s.b) return RQ_EINVAL;
         }
-        order.push_back({s.src_id, k});
+        const bool stat = s.kind == RQ_SRC_POISSON2 || s.kind == RQ_SRC_PWCONST ||
+                          (s.kind == RQ_SRC_REALDATA && !(s.flags & RQ_SRCF_DYNAMIC));
+        order.push_back({s.src_id, k, stat ? 1 : 0});
     }
-    order.push_back({d->ctrl_src_id, -1});
-    std::sort(order.begin(), order.end(), [](const S& x, const S& y) { return x.id < y.id; });
-    for (size_t k = 1; k < order.size(); ++k)
-        if (order[k].id == order[k - 1].id) return RQ_EINVAL;          // "Duplicates in sources."
+    order.push_back({d->ctrl_src_id, -1, 1});
+    {
+        std::vector<int64_t> ids;
+        for (const S& o : order) ids.push_back(o.id);
+        std::sort(ids.begin(), ids.end());
+        if (std::adjacent_find(ids.begin(), ids.end()) != ids.end()) return RQ_EINVAL;   // "Duplicates in sources."
+    }
+    std::sort(order.begin(), order.end(),
+              [](const S& x, const S& y) { return x.cls != y.cls ? x.cls < y.cls : x.id < y.id; });
     g->n_str = (int)order.size();
     std::unordered_map<int64_t, int> sidx;
     for (int j = 0; j < g->n_str; ++j) {
@@ -803,6 +834,7 @@ int rq_graph_build(const rq_graph_desc* d, rq_graph_t* out)
         sidx[o.id] = j;
         g->src_id.push_back(o.id);
         g->orig_idx.push_back(o.orig);
+        g->is_static.push_back(o.cls);
         g->arr_off.push_back((int)g->arr_a.size());
         if (o.orig < 0) {
             g->ctrl_idx = j;
@@ -854,6 +886,20 @@ int rq_graph_build(const rq_graph_desc* d, rq_graph_t* out)
             if (!(s.p0 >= 0.0) || !(s.p1 >= 0.0) || !(s.p2 >= 0.0)) return RQ_EINVAL;
         }
         g->arr_n.push_back(n);
+    }
+
+    {
+        std::vector<double> tw, tc;
+        for (int j = 0; j < g->n_str; ++j)
+            if (g->kind[j] == RQ_SRC_REALDATA)
+                tw.insert(tw.end(), g->arr_a.begin() + g->arr_off[j], g->arr_a.begin() + g->arr_off[j] + g->arr_n[j]);
+        if (!d->ctrl_b)   // replayed controller times (change times of a piecewise one are not events)
+            tc.assign(g->arr_a.begin() + g->ctrl_arr_off, g->arr_a.begin() + g->ctrl_arr_off + g->ctrl_arr_n);
+        std::sort(tw.begin(), tw.end());
+        g->rd_ties = std::adjacent_find(tw.begin(), tw.end()) != tw.end();
+        tc.insert(tc.end(), tw.begin(), tw.end());
+        std::sort(tc.begin(), tc.end());
+        g->rd_ties_ctrl = std::adjacent_find(tc.begin(), tc.end()) != tc.end();
     }
 
     // edges: "Unknown sources/sinks in edge_list." ; CSR in edge-list order
@@ -927,11 +973,7 @@ int rq_graph_build(const rq_graph_desc* d, rq_graph_t* out)
     // or has a larger src_id (opt_model.py:279-281, :289-290): the sweeps' per-stream flag,
     // in global memory for the GT instances (the others build it in LDS)
     std::vector<int> cbf(g->n_str);
-    for (int j = 0; j < g->n_str; ++j) {
-        const int kj = g->kind[j];
-        cbf[j] = kj == RQ_SRC_POISSON2 || kj == RQ_SRC_PWCONST || kj == RQ_SRC_REALDATA ||
-                 g->ctrl_src_id < g->src_id[j];
-    }
+    for (int j = 0; j < g->n_str; ++j) cbf[j] = g->is_static[j] || g->ctrl_src_id < g->src_id[j];
 
     int rc;
     if (g->nw > 0 && (rc = g->d_mask.upload(g->masks))) return rc;
@@ -1108,6 +1150,7 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
         std::memcpy(tab + p.off_stoff, p.st_off.data(), p.st_off.size() * sizeof(int64_t));
         std::memcpy(tab + p.off_cap, p.cap.data(), p.cap.size() * sizeof(int));
         std::memcpy(tab + p.off_rdk, p.rd_k.data(), p.rd_k.size() * sizeof(int));
+        if (b->rep_idx) std::memcpy(tab + p.off_repidx, b->rep_idx, sizeof(int64_t) * (size_t)p.R);
         if (!pwc.empty()) {
             std::memcpy(tab + p.off_pwc, pwc.data(), pwc.size() * sizeof(double));
             std::memcpy(tab + p.off_pwmax, pwmax.data(), pwmax.size() * sizeof(double));
@@ -1165,6 +1208,7 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
         ga.n_rep = b->n_rep;
         ga.rep_lo = p.rep_lo;
         ga.rep_cnt = p.rep_cnt;
+        ga.rep_idx = b->rep_idx ? (const int64_t*)(ws + p.off_repidx) : nullptr;
         ga.n_str = g->n_str;
         ga.ctrl_idx = g->ctrl_idx;
         ga.ctrl_stream_kind = ctrl_stream_kind;

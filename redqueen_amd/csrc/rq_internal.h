@@ -20,6 +20,7 @@ __host__ __device__ __forceinline__ int64_t rq_global_replica(int64_t s, int64_t
 struct GenArgs {
     int64_t n_chunk, chunk0, rep0;   // local replica = chunk0 + rl, space position = rep0 + local
     int64_t n_rep, rep_lo, rep_cnt;  // global id = rq_global_replica(rep0 + local, ...)
+    const int64_t* rep_idx;          // rq_batch_desc.rep_idx (device copy): global id = rep_idx[local]
     int n_str, ctrl_idx, ctrl_stream_kind, randomize;
     int64_t seed_mod;
     const uint32_t* ctrl_seed;
@@ -47,6 +48,13 @@ struct GenArgs {
     const double* rd_times;
     const int64_t* rd_off;
 };
+
+// global id of a call's local replica: the replica list (rq_batch_desc.rep_idx) or the
+// replica space position rep0 + local
+__host__ __device__ __forceinline__ int64_t rq_replica_of(const GenArgs& a, int64_t local)
+{
+    return a.rep_idx ? a.rep_idx[local] : rq_global_replica(a.rep0 + local, a.n_rep, a.rep_lo, a.rep_cnt);
+}
 
 #define RQ_MAX_STREAMS 2048   // 512 per fast instance (8 per lane); LOG instances 16 / 32 per lane
 

@@ -45,7 +45,7 @@ __global__ __launch_bounds__(256) void rq_gen_streams(GenArgs a)
     const int j = blockIdx.y;
     if (rl >= a.n_chunk) return;
     const int64_t o = a.chunk0 + rl;      // local output index
-    const int64_t i = rq_global_replica(a.rep0 + o, a.n_rep, a.rep_lo, a.rep_cnt);   // global id (seeds)
+    const int64_t i = rq_replica_of(a, o);   // global id (seeds)
     SrcGen gen;
     gen.init(a, j, i, rq_exp_tab_c);
 
@@ -158,9 +158,7 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
         // when that source is static (run_dynamic plays a static time only if it is
         // strictly earlier, opt_model.py:289-290) or has a larger src_id (the sorted
         // (t_delta, src_id) of the dynamic sources, :279-281)
-        const int kj = a.gen.kind[j];
-        cbf[j] = kj == RQ_SRC_POISSON2 || kj == RQ_SRC_PWCONST || kj == RQ_SRC_REALDATA ||
-                 a.ctrl_src_id < a.src_id[j];
+        cbf[j] = a.cbf_g[j];   // the graph's table (static sources, RQ_SRCF_DYNAMIC)
     }
     // BL: the follower set as a sink bitset, shared by the block's waves
     uint32_t* fbl = reinterpret_cast<uint32_t*>(base + a.lds_fbits);
@@ -191,7 +189,7 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
     for (int64_t qi = (int64_t)blockIdx.x * a.wpb + w; qi < a.n_chunk;) {
     const int64_t rl = a.order ? (int64_t)a.order[qi] : qi;   // longest first (rq_order_replicas)
     const int64_t o = a.chunk0 + rl;
-    const int64_t i = rq_global_replica(a.rep0 + o, a.n_rep, a.gen.rep_lo, a.gen.rep_cnt);
+    const int64_t i = rq_replica_of(a.gen, o);
     const int g = (int)(i / a.n_rep);
     AggL agl;
     if (BL) {
@@ -573,7 +571,7 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
             }
         }
         const bool fin = LOG && !MRG ? n < 64 : fin_w;
-        const bool act = lane < n;
+        bool act = lane < n;
         int e0 = 0, e1 = 0, od = 0;
         if (act) {
             e0 = cptr_r[tj];
@@ -589,6 +587,11 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
         if (opt && a.dbg != 3)
             controller_tile<true>(n, act, tt, tj, invc_r, cbf_r, oseed, ndraw, opt_next, ownm, ot, pwc, pwm, a.n_seg,
                             a.period);
+        // max_events on the fast sweeps: the tile keeps the events numbered below it and
+        // the replica ends with it (the LOG sweep's event() counts them one by one)
+        bool cut = false;
+        if (!LOG && a.max_events >= 0)
+            cut = truncate_tile(a.max_events, n_events, n, act, tt, tj, ownm, ot, opt_next);
         ownm = sgpr_u64(ownm);   // wave-uniform: phase C's bookkeeping stays scalar
         // ---- C: apply the tile's events in order ----
         if (LOG) {
@@ -964,10 +967,10 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
             if (ma && place_rows<NK>(rs, ma, has_o, has_w, ot, tt, osum, oval, ocnt, wsum, wval, wcnt, status))
                 stop = true;
         }
-        if (stop || fin) break;
+        if (stop || fin || cut) break;
     }
-    // the controller's last post after the final arrival
-    if (!stop && opt && opt_next <= a.end) {
+    // the controller's last post after the final arrival (or the tile max_events cut)
+    if (!stop && opt && opt_next <= a.end && (LOG || a.max_events < 0 || n_events < a.max_events)) {
         if (LOG) {
             event(opt_next, true, 0, 0, 0);
         } else {

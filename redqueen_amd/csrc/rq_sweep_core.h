@@ -520,6 +520,34 @@ __device__ __forceinline__ void controller_tile(int n, bool act, double tt, int 
     opt_next = cur;
 }
 
+// ---- max_events inside a fast tile (run_dynamic's `while num_events < max_events`,
+//  opt_model.py:271).  After phase B, lane q's post (ownm bit q) is event number
+//  n_events + q + #posts before q, its wall event the next one.  Keeps the events
+//  numbered < M: the wall events of lanes < nk (a prefix: the numbers grow with the lane)
+//  with their posts; a post right before wall event nk that still fits becomes the
+//  replica's final post (opt_next, played by the post-loop path), else opt_next = INF.
+//  The tile shrinks to nk lanes; true = the replica ends with this tile.
+__device__ __forceinline__ bool truncate_tile(int64_t M, int64_t n_events, int& n, bool& act, double& tt,
+                                              int& tj, uint64_t& ownm, double ot, double& opt_next)
+{
+    if (M < 0) return false;
+    const int lane = lane_id();
+    const int64_t pp = n_events + lane + mbcnt64(ownm);
+    const int64_t pw = pp + (int64_t)((ownm >> lane) & 1ull);
+    const int nk = __popcll(__ballot(act && pw < M));
+    if (nk >= n) return false;
+    const bool lone = ((ownm >> nk) & 1ull) != 0ull && bcast_i64(pp, nk) < M;
+    opt_next = lone ? bcast_d(ot, nk) : RQ_INF;
+    ownm &= nk > 0 ? (~0ull >> (64 - nk)) : 0ull;
+    n = nk;
+    act = lane < nk;
+    if (!act) {
+        tt = RQ_INF;
+        tj = 0;
+    }
+    return true;
+}
+
 // ---- pivot rows of a tile: lane q may hold a post row (before its wall event,
 //  aggregates o*) and a wall row (w*).  pivot_table keeps one row per distinct t
 //  (the last): a row is dropped when the next row has the same time; a first row

@@ -69,9 +69,7 @@ __device__ __forceinline__ void sweep_fw_body(SweepArgs a)
         // when that source is static (run_dynamic plays a static time only if it is
         // strictly earlier, opt_model.py:289-290) or has a larger src_id (the sorted
         // (t_delta, src_id) of the dynamic sources, :279-281)
-        const int kj = a.gen.kind[j];
-        cbf[j] = kj == RQ_SRC_POISSON2 || kj == RQ_SRC_PWCONST || kj == RQ_SRC_REALDATA ||
-                 a.ctrl_src_id < a.src_id[j];
+        cbf[j] = a.cbf_g[j];   // the graph's table (static sources, RQ_SRCF_DYNAMIC)
     }
     __syncthreads();   // block-shared tables ready; no block barrier below this line
     char* wb = base + a.lds_wave + (size_t)w * a.lds_wave_stride;
@@ -90,7 +88,7 @@ __device__ __forceinline__ void sweep_fw_body(SweepArgs a)
     for (int64_t qi = (int64_t)blockIdx.x * a.wpb + w; qi < a.n_chunk;) {
     const int64_t rl = a.order ? (int64_t)a.order[qi] : qi;   // longest first (rq_order_replicas)
     const int64_t o = a.chunk0 + rl;
-    const int64_t i = rq_global_replica(a.rep0 + o, a.n_rep, a.gen.rep_lo, a.gen.rep_cnt);
+    const int64_t i = rq_replica_of(a.gen, o);
     const int g = (int)(i / a.n_rep);
     for (int j = lane; j < a.n_str; j += 64) invc[j] = a.inv_c[(int64_t)g * a.n_str + j];
     if (!BITS)
@@ -309,6 +307,9 @@ __device__ __forceinline__ void sweep_fw_body(SweepArgs a)
                             a.period);
 
         RQ_CLK(3);   // B controller
+        // max_events: the tile keeps the events numbered below it, the replica ends here
+        if (a.max_events >= 0 && truncate_tile(a.max_events, n_events, n, act, tt, tj, ownm, ot, opt_next))
+            fin = true;
         // ---- C: aggregates after each event ----
         const bool own_b = act && ((ownm >> lane) & 1ull);       // controller post before #lane
         if (a.ev_t) {
@@ -451,8 +452,8 @@ __device__ __forceinline__ void sweep_fw_body(SweepArgs a)
         for (int q = 0; q < 8; ++q) atomicAdd(&a.clk[q], ck[q]);
 #endif
     if (BITS) agb.T = lane < a.nw ? ft[lane].y : 0u;   // the top-1 set back in its lane words
-    // the controller's last post after the final arrival
-    if (!stop && opt && opt_next <= a.end) {
+    // the controller's last post after the final arrival (or the tile max_events cut)
+    if (!stop && opt && opt_next <= a.end && (a.max_events < 0 || n_events < a.max_events)) {
         if (a.ev_t && lane == 0) {
             if (n_events < a.ev_cap) {
                 a.ev_t[o * a.ev_cap + n_events] = opt_next;

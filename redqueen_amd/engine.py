@@ -56,9 +56,13 @@ class Graph:
         self.has_realdata = False
         # registered static plugin broadcasters: (position in other_sources, class, kwargs)
         self.plugins = []
+        # src_ids of the static wall sources (run_dynamic plays their times only when
+        # strictly earlier than the dynamic sources' next event, opt_model.py:289-290)
+        self.static_src_ids = set()
         for idx, (name, kw) in enumerate(other_sources):
             kind = _source_kind(name)
             cls = _source_class(name)
+            dyn_plugin = False
             if cls is not None and getattr(cls, "_rq_kind", None) is None:
                 # graph-level times: the instance its own kwargs make (the seed as given);
                 # randomized batches replace them per replica (run(randomize=True)).  A
@@ -67,16 +71,23 @@ class Graph:
                 inst = cls(**kw)
                 dyn = bool(getattr(inst, "is_dynamic", True))
                 self.plugins.append((idx, cls, dict(kw), int(kw["src_id"]), dyn))
+                dyn_plugin = dyn
                 kw = {"src_id": kw["src_id"],
                       "times": source_times(inst, float(start_time), sink_ids, edge_list,
                                             float(end_time))}
             self.has_realdata = self.has_realdata or kind == L.SRC_REALDATA
+            # a dynamic broadcaster replayed from its times (a dynamic plugin, or RealData
+            # kwargs dynamic=True): equal times order it as a dynamic source
+            dyn_rd = kind == L.SRC_REALDATA and (bool(kw.get("dynamic")) or dyn_plugin)
+            if kind in (L.SRC_POISSON2, L.SRC_PWCONST) or (kind == L.SRC_REALDATA and not dyn_rd):
+                self.static_src_ids.add(int(kw["src_id"]))
             if kind == L.SRC_OPT:
                 raise NotImplementedError("an Opt broadcaster among the other sources")
             d = L.SourceDesc()
             d.kind = kind
             d.src_id = int(kw["src_id"])
             d.seed = int(kw.get("seed", 0)) & 0xFFFFFFFF
+            d.flags = L.SRCF_DYNAMIC if dyn_rd else 0
             if kind in (L.SRC_POISSON, L.SRC_POISSON2):
                 d.p0 = float(kw.get("rate", 1.0))
             elif kind == L.SRC_HAWKES:
@@ -142,7 +153,7 @@ class Graph:
         # one workspace per caller stream: batches enqueued on different streams may run
         # at the same time and must not share buffers
         self._wss = {}
-        self._cap_scale = {}   # (controller kind, max_events) -> cap_scale an overflow needed
+        self._cap_scale = {}   # _cap_key(...) -> cap_scale an overflow rerun needed (reset_capacity_memo)
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -296,60 +307,127 @@ class Graph:
         return self._run_loop(lib, b, keep, dev, R, Ks, n_grid, n_rep, ck, event_log,
                               gids, check, stream)
 
+    def _launch(self, lib, b, dev, R, Ks, n_grid, n_rep, event_log, use):
+        """One rq_run_batch of R output replicas on stream ``use``.  The outputs (and the
+        event log) are allocated first, so the workspace budget is what is left after them."""
+        sk = use.cuda_stream
+        metrics = torch.empty((R, Ks.size + 2), dtype=torch.float64, device=dev)
+        counts = torch.empty((R, 4), dtype=torch.int64, device=dev)
+        status = torch.empty(R, dtype=torch.int32, device=dev)
+        out = L.Outputs()
+        out.metrics, out.counts, out.status = metrics.data_ptr(), counts.data_ptr(), status.data_ptr()
+        ev_t = ev_src = None
+        if event_log:
+            cap = C.c_int64()
+            L.check("rq_event_capacity", lib.rq_event_capacity(self._h, C.byref(b), C.byref(cap)))
+            ev_t = torch.empty((R, cap.value), dtype=torch.float64, device=dev)
+            ev_src = torch.empty((R, cap.value), dtype=torch.int32, device=dev)
+            out.ev_t, out.ev_src, out.ev_cap = ev_t.data_ptr(), ev_src.data_ptr(), cap.value
+        nbytes = C.c_size_t()
+        b.ws_budget = self._ws_budget(dev, sk)
+        L.check("rq_workspace_size", lib.rq_workspace_size(self._h, C.byref(b), C.byref(nbytes)))
+        ws = self._wss.get(sk)
+        if ws is None or ws.numel() < nbytes.value:
+            self._wss[sk] = ws = None
+            ws = self._wss[sk] = torch.empty(max(256, nbytes.value), dtype=torch.uint8, device=dev)
+        L.check("rq_run_batch", lib.rq_run_batch(self._h, C.byref(b), C.byref(out),
+                                                 ws.data_ptr(), ws.numel(), sk))
+        return BatchResult(self, metrics, counts, status, ev_t, ev_src, Ks, n_grid, int(n_rep))
+
+    # an overflow memo is kept only when at least this share of a batch overflowed (a
+    # few flagged replicas rerun alone, cheaply; a batch mostly over capacity would pay a
+    # second pass every call)
+    CAP_MEMO_SHARE = 1.0 / 16
+
+    def _cap_key(self, b, ck):
+        """Capacity-relevant inputs of a run: controller kind, max_events set, sweep
+        mode, and the octave of the controller's rate parameter (RedQueen: the q range;
+        Poisson: the largest rate) -- an overflow at one q says nothing about another."""
+        qk = None
+        if ck in (L.SRC_OPT, L.SRC_OPTPW) and b.n_grid > 0:
+            qs = np.ctypeslib.as_array(b.q, shape=(b.n_grid,))
+            qk = (int(np.floor(np.log2(max(qs.min(), 1e-300)))), int(np.floor(np.log2(max(qs.max(), 1e-300)))))
+        elif ck == L.SRC_POISSON2:
+            qk = int(np.floor(np.log2(max(b.ctrl_rate_max, 1e-300))))
+        return (ck, b.max_events >= 0, int(b.sweep_mode), qk)
+
+    def reset_capacity_memo(self):
+        """Forget the capacity scales earlier overflow reruns of this graph remembered."""
+        self._cap_scale.clear()
+
     def _run_loop(self, lib, b, keep, dev, R, Ks, n_grid, n_rep, ck, event_log, gids,
                   check, use):
-        # start from the capacity scale an earlier overflow rerun of this graph needed
-        key = (ck, b.max_events >= 0)
+        """The batch, then -- with ``check`` -- only its flagged replicas again
+        (rq_batch_desc.rep_idx: the same global ids, so the same seeds and inputs): an
+        overflowed one (RQ_ST_*_OVERFLOW) at doubled capacities, a tie-flagged one of a
+        fast sweep (RQ_ST_TIE: equal event times) on the exact sequential sweep; their
+        rows replace the flagged rows.  ``self.reruns`` counts the replicas rerun."""
+        key = self._cap_key(b, ck)
         b.cap_scale = max(b.cap_scale, self._cap_scale.get(key, 1.0))
-        sk = use.cuda_stream
+        res = self._launch(lib, b, dev, R, Ks, n_grid, n_rep, event_log, use)
+        res.replica0 = int(gids[0]) if len(gids) else 0
+        res.global_ids = gids
+        self.reruns = 0
+        if not check:
+            return res
+        gids = np.asarray(gids, dtype=np.int64)
+        # per output replica: the sweep mode it last ran with, and whether that run was the
+        # exact sequential sweep (from the library's own plan: rq_plan_info variant 1 / 4)
+        mode = np.full(R, int(b.sweep_mode), dtype=np.int64)
+        seq = np.full(R, b.sweep_mode == 2 or self._plan_variant(lib, b) % 10 in (1, 4))
+        scale = np.full(R, float(b.cap_scale))
         while True:
-            nbytes = C.c_size_t()
-            b.ws_budget = self._ws_budget(dev, sk)
-            L.check("rq_workspace_size", lib.rq_workspace_size(self._h, C.byref(b), C.byref(nbytes)))
-            ws = self._wss.get(sk)
-            if ws is None or ws.numel() < nbytes.value:
-                self._wss[sk] = ws = None
-                ws = self._wss[sk] = torch.empty(max(256, nbytes.value), dtype=torch.uint8, device=dev)
-            metrics = torch.empty((R, Ks.size + 2), dtype=torch.float64, device=dev)
-            counts = torch.empty((R, 4), dtype=torch.int64, device=dev)
-            status = torch.empty(R, dtype=torch.int32, device=dev)
-            out = L.Outputs()
-            out.metrics, out.counts, out.status = metrics.data_ptr(), counts.data_ptr(), status.data_ptr()
-            ev_t = ev_src = None
-            if event_log:
-                cap = C.c_int64()
-                L.check("rq_event_capacity", lib.rq_event_capacity(self._h, C.byref(b), C.byref(cap)))
-                ev_t = torch.empty((R, cap.value), dtype=torch.float64, device=dev)
-                ev_src = torch.empty((R, cap.value), dtype=torch.int32, device=dev)
-                out.ev_t, out.ev_src, out.ev_cap = ev_t.data_ptr(), ev_src.data_ptr(), cap.value
-            st = use.cuda_stream
-            L.check("rq_run_batch", lib.rq_run_batch(self._h, C.byref(b), C.byref(out),
-                                                     ws.data_ptr(), ws.numel(), st))
-            res = BatchResult(self, metrics, counts, status, ev_t, ev_src, Ks, n_grid, int(n_rep))
-            res.replica0 = int(gids[0]) if len(gids) else 0
-            res.global_ids = gids
-            if not check:
-                return res
             use.synchronize()
-            if int((status & L.ST_UNORDERED).any().item()):
+            st = res.status.cpu().numpy()
+            if (st & L.ST_UNORDERED).any():
                 raise NotImplementedError(
                     "more than 2048 arrivals at one time in a sequential run over > 2048 sources "
                     "(RQ_ST_UNORDERED): their play order is not the reference's")
-            ovf = int((status & (L.ST_ROWS_OVERFLOW | L.ST_STREAM_OVERFLOW)).any().item())
-            if not ovf:
-                # equal event times in a fast tiled sweep: redo with the exact sequential
-                # sweep (never taken by continuous-time worlds).  Whether this run was the
-                # sequential variant comes from the library's own plan (rq_plan_info
-                # variant 1), not from a re-derivation of its rules here.
-                if int((status & L.ST_TIE).any().item()) and b.sweep_mode != 2 \
-                        and self._plan_variant(lib, b) % 10 not in (1, 4):
-                    b.sweep_mode = 2
-                    continue
+            ovf = (st & (L.ST_ROWS_OVERFLOW | L.ST_STREAM_OVERFLOW)) != 0
+            tie = ((st & L.ST_TIE) != 0) & ~seq & ~ovf
+            if not ovf.any() and not tie.any():
                 return res
-            if b.cap_scale > 64:
-                raise L.RQError("rq_run_batch", L.RQ_EOVERFLOW)
-            b.cap_scale = b.cap_scale * 2.0
-            self._cap_scale[key] = max(self._cap_scale.get(key, 1.0), b.cap_scale)
+            if ovf.any():
+                if scale[ovf].max() > 64:
+                    raise L.RQError("rq_run_batch", L.RQ_EOVERFLOW)
+                scale[ovf] *= 2.0
+                if ovf.sum() >= self.CAP_MEMO_SHARE * R:
+                    self._cap_scale[key] = max(self._cap_scale.get(key, 1.0), float(scale[ovf].max()))
+            # equal event times in a fast tiled sweep: those replicas on the exact sequential sweep
+            mode[tie] = 2
+            seq[tie] = True
+            # one rerun per (sweep mode, capacity scale) group of flagged replicas
+            flagged = np.flatnonzero(ovf | tie)
+            for m_, s_ in sorted({(int(mode[k]), float(scale[k])) for k in flagged}):
+                pick = flagged[(mode[flagged] == m_) & (scale[flagged] == s_)]
+                self._rerun_into(lib, b, dev, res, pick, gids[pick], s_, m_, Ks, n_grid, n_rep,
+                                 event_log, use)
+                self.reruns += int(pick.size)
+
+    def _rerun_into(self, lib, b, dev, res, pick, ids, scale, mode, Ks, n_grid, n_rep, event_log, use):
+        """Rerun global replicas ``ids`` (outputs ``pick`` of ``res``) and scatter them in."""
+        sub = L.BatchDesc.from_buffer_copy(b)
+        idx = np.ascontiguousarray(ids, dtype=np.int64)
+        sub.rep_idx = idx.ctypes.data_as(L._pi64)
+        sub.replica0, sub.n_local, sub.rep_lo, sub.rep_cnt = 0, int(idx.size), 0, 0
+        sub.cap_scale = float(scale)
+        sub.sweep_mode = int(mode)
+        sub.chunk = 0
+        r = self._launch(lib, sub, dev, int(idx.size), Ks, n_grid, n_rep, event_log, use)
+        at = torch.from_numpy(np.asarray(pick, dtype=np.int64)).to(dev)
+        res.metrics.index_copy_(0, at, r.metrics)
+        res.counts.index_copy_(0, at, r.counts)
+        res.status.index_copy_(0, at, r.status)
+        if event_log:
+            cap, cap2 = res.ev_t.shape[1], r.ev_t.shape[1]
+            if cap2 > cap:   # a larger event capacity: widen every replica's log row
+                t2 = torch.empty((res.ev_t.shape[0], cap2), dtype=res.ev_t.dtype, device=dev)
+                s2 = torch.empty((res.ev_src.shape[0], cap2), dtype=res.ev_src.dtype, device=dev)
+                t2[:, :cap] = res.ev_t
+                s2[:, :cap] = res.ev_src
+                res.ev_t, res.ev_src = t2, s2
+            res.ev_t[at, :cap2] = r.ev_t
+            res.ev_src[at, :cap2] = r.ev_src
 
     def _ws_budget(self, dev, sk=None):
         """The workspace's device-memory budget (rq_batch_desc.ws_budget): 0.9 x what this
@@ -473,6 +551,10 @@ class Graph:
         sm = int(kw.get("seed_mod", 0))
         me = kw.get("max_events")
         me = None if me is None or me == float("inf") else int(me)
+        ctrl = args[0] if args else kw.get("ctrl", "opt")
+        static_ids = set(self.static_src_ids)
+        if ctrl in ("poisson", "pwconst", "times"):
+            static_ids.add(self.src_id)   # a static controlled source (Poisson2 / PWConst / RealData)
 
         def make(i):
             if rand:
@@ -493,8 +575,8 @@ class Graph:
                     if p[4]:
                         new[c] = reactive_plugin_times(insts[c], self.start_time, self.sink_ids,
                                                        self._edges, self.end_time, t_ev, s_ev,
-                                                       max_events=me)
-                if any(not np.array_equal(a, b) for a, b in zip(new, cur)):
+                                                       max_events=me, static_ids=static_ids)
+                if any(not np.array_equal(a_, b_) for a_, b_ in zip(new, cur)):
                     times[i] = new
                     nxt.append(k)
             if not nxt:

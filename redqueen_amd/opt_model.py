@@ -279,14 +279,19 @@ REACTIVE_MAX_ITERATIONS = 1000
 
 
 def reactive_plugin_times(fresh, start_time, sink_ids, edge_list, end_time, ev_t, ev_src,
-                          max_events=None):
+                          max_events=None, static_ids=()):
     """Own event times of a dynamic plugin whose schedule may react to other sources'
     events, given the OTHER sources' events of a run (ev_t / ev_src in play order; the
     plugin's own entries in the log are dropped): run_dynamic's loop (opt_model.py:271-311)
     with this plugin beside that fixed sequence.  After every event -- its own and the
     others', event ids from 100, time_delta on the accumulated State.time -- the plugin's
     get_next_event_time(event) gives its delay r, and its next event comes at
-    State.time + r unless another event comes first (equal times: the lower src_id first).
+    State.time + r unless another event comes first.  Equal times: the plugin is dynamic,
+    so it plays before a STATIC source's event (run_dynamic plays a static time only when
+    it is strictly earlier, opt_model.py:289-290; ``static_ids``: the src_ids of the
+    Poisson2 / PiecewiseConst / RealData / static-plugin sources of the run) and, against a
+    dynamic source (Poisson, Hawkes, RedQueen, another dynamic plugin), in src_id order
+    (the sorted (t_delta, src_id) of the dynamic sources, :279-281).
     Exact when the other events do not depend on the plugin's; Graph.run / Manager.run_dynamic
     rerun with these times until the run reproduces them (the fixed point)."""
     sinks = {}
@@ -299,12 +304,14 @@ def reactive_plugin_times(fresh, start_time, sink_ids, edge_list, end_time, ev_t
     ev_src = np.asarray(ev_src)
     keep = ev_src != me
     ot, osrc = ev_t[keep], ev_src[keep]
+    static_ids = {int(x) for x in static_ids}
     out = []
     state_time = float(start_time)
     j, k, n_o = 0, 0, len(ot)
     while max_events is None or k < max_events:
         cand = state_time + r
-        if j < n_o and (float(ot[j]) < cand or (float(ot[j]) == cand and int(osrc[j]) < me)):
+        if j < n_o and (float(ot[j]) < cand or (float(ot[j]) == cand and int(osrc[j]) < me and
+                                                int(osrc[j]) not in static_ids)):
             t, src = float(ot[j]), int(osrc[j])
             j += 1
         else:
@@ -576,7 +583,10 @@ class Manager:
                 continue
             fresh = copy.deepcopy(s) if getattr(s, "is_dynamic", True) else None
             t = source_times(s, self.start_time, self.sink_ids, self.edge_list, self.end_time)
-            other_desc.append(("RealData", {"src_id": s.src_id, "times": t}))
+            kw = {"src_id": s.src_id, "times": t}
+            if fresh is not None:
+                kw["dynamic"] = True   # ties: played as the dynamic source it is (RQ_SRCF_DYNAMIC)
+            other_desc.append(("RealData", kw))
             if fresh is not None:
                 probes.append((fresh, t, len(other_desc) - 1))
         if isinstance(ctrl, (Opt, OptPWSignificance)):
@@ -621,9 +631,15 @@ class Manager:
 
         res = play(other_desc)
         t, src = res.events(0)
+        # the run's static sources (their equal-time events play after a dynamic plugin's)
+        static_ids = {s.src_id for s in self.sources
+                      if not getattr(s, "is_dynamic", True) and s is not ctrl}
+        if isinstance(ctrl, (Poisson2, PiecewiseConst, RealData)):
+            static_ids.add(ctrl.src_id)
         for it in range(REACTIVE_MAX_ITERATIONS + 1):
             new = [reactive_plugin_times(copy.deepcopy(fresh), self.start_time, self.sink_ids,
-                                         self.edge_list, self.end_time, t, src, max_events=maxev)
+                                         self.edge_list, self.end_time, t, src, max_events=maxev,
+                                         static_ids=static_ids)
                    for fresh, _times, _pos in probes]
             if all(np.array_equal(a, times) for a, (_f, times, _p) in zip(new, probes)):
                 break
@@ -633,7 +649,8 @@ class Manager:
                     % REACTIVE_MAX_ITERATIONS)
             probes = [(fresh, nt, pos) for (fresh, _t, pos), nt in zip(probes, new)]
             for _f, nt, pos in probes:
-                other_desc[pos] = ("RealData", {"src_id": other_desc[pos][1]["src_id"], "times": nt})
+                other_desc[pos] = ("RealData", {"src_id": other_desc[pos][1]["src_id"], "times": nt,
+                                                "dynamic": True})
             res = play(other_desc)
             t, src = res.events(0)
         for s in self.sources:

@@ -43,6 +43,8 @@ installed and there is no network) and records, as plain data:
   dynplugin.npz    a registered DYNAMIC self-driven broadcaster (Renewal) beside a static
                    one: df + metrics of the seeded world and of randomize_other_sources(u);
                    the same for a REACTIVE one (KnockedOff, knock_*)
+  gridtie.npz      a reactive dynamic plugin whose posts meet static sources' times exactly
+                   (all sources on binary grids): df + metrics, 32 randomized worlds
   dist_knock.npz   (--knock-dist N) the reactive plugin beside RedQueen: N reference runs
   errors.npz       reference behaviour on a scalar-s u_int_opt and on OptPWSignificance
                    events that reach no follower with positive significance
@@ -633,6 +635,46 @@ def gen_dynplugin():
     np.savez_compressed(os.path.join(HERE, "dynplugin.npz"), **rec)
 
 
+def gen_gridtie():
+    """gridtie.npz: a reactive dynamic plugin whose posts meet static sources' times
+    exactly (realdata_worlds.grid_tie_world): the reference's df of the seeded world and
+    the metrics + counts of randomize_other_sources(u), u = 0..31."""
+    from realdata_worlds import GridBurstyMixin, GridKnockMixin, grid_tie_world
+    from redqueen.opt_model import Broadcaster
+
+    class GridBursty(GridBurstyMixin, Broadcaster):
+        pass
+
+    class GridKnock(GridKnockMixin, Broadcaster):
+        pass
+    SimOpts.registerSource("GridBursty", GridBursty)
+    SimOpts.registerSource("GridKnock", GridKnock)
+    w, ctrl, us = grid_tie_world()
+    so = SimOpts(**w)
+    rec = {}
+    m = so.create_manager_with_times(np.asarray(ctrl))
+    m.run_dynamic()
+    df = m.state.get_dataframe()
+    _df_cols(rec, "base", df)
+    met, own, world = metrics(df, so)
+    rec["base_met"], rec["base_cnt"] = met, np.asarray([own, world, len(df)])
+    mets, cnts, ties = [], [], []
+    for u in us:
+        m = so.randomize_other_sources(u).create_manager_with_times(np.asarray(ctrl))
+        m.run_dynamic()
+        df = m.state.get_dataframe()
+        met, own, world = metrics(df, so)
+        mets.append(met)
+        cnts.append([own, world, m.state.get_num_events()])
+        # equal-time events of the plugin (src 7) and a static source: the order under test
+        g = df.groupby("event_id").first()
+        t7 = set(g.t[g.src_id == 7])
+        ties.append(sum(1 for t, s in zip(g.t, g.src_id) if s != 7 and t in t7))
+    rec["rand_met"], rec["rand_cnt"], rec["rand_u"] = np.asarray(mets), np.asarray(cnts), np.asarray(us)
+    rec["rand_ties"] = np.asarray(ties)
+    np.savez_compressed(os.path.join(HERE, "gridtie.npz"), **rec)
+
+
 KNOCK_SEED_STRIDE = 1000   # > 99 x the broadcaster count: no shared streams
 KNOCK_OPT_SEED_OFFSET = 500
 
@@ -1056,7 +1098,8 @@ if __name__ == "__main__":
     steps = {"npsum": gen_npsum, "draws": gen_draws, "readme": gen_readme, "kats": gen_kats,
              "adv": gen_adversarial, "graphs": gen_graphs, "frac": gen_frac,
              "oracle": gen_oracle, "sweepq": gen_sweepq, "sig": gen_sig, "realdata": gen_realdata,
-             "plugin": gen_plugin, "errors": gen_errors, "dynplugin": gen_dynplugin}
+             "plugin": gen_plugin, "errors": gen_errors, "dynplugin": gen_dynplugin,
+             "gridtie": gen_gridtie}
     if a.scale_logs:
         gen_scale_logs(a.procs)
         print("done scale logs", flush=True)

@@ -146,3 +146,48 @@ def dyn_plugin_world():
                         (4, 6)])
     ctrl = [0.0, 1.5, 4.0, 9.25, 12.0, 20.0, 27.5]
     return w, ctrl, list(range(16))
+
+
+class GridBurstyMixin(BurstyMixin):
+    """Bursty on the 0.25 grid: burst posts rounded to quarters (exact in binary), so
+    its posts meet the other grid sources' times and each other's exactly."""
+
+    def initialize(self):
+        super().initialize()
+        self.times = np.round(self.times * 4.0) / 4.0
+
+
+class GridKnockMixin(KnockedOffMixin):
+    """KnockedOff on the 0.5 grid: when another source's event knocks it off its
+    followers' top it schedules its next post at the first half-integer at least
+    Exp(rate) later.  With every other source on the 0.25 grid, every time and every
+    difference run_dynamic forms is exact in binary, so its posts meet the static
+    sources' times EXACTLY: the equal-time order of a dynamic source against static ones
+    (opt_model.py:279-290) is exercised, not an ulp-level accident."""
+
+    def get_next_interval(self, event):
+        if event is None:
+            return 0.5 * np.ceil(2.0 * self.random_state.exponential(scale=1.0 / self.rate))
+        if event.src_id == self.src_id:
+            self.on_top = True
+            return float("inf")
+        if self.on_top and set(event.sink_ids) & set(self.sink_ids):
+            self.on_top = False
+            t = 0.5 * np.ceil(2.0 * (self.get_current_time(event) +
+                                     self.random_state.exponential(scale=1.0 / self.rate)))
+            return t - self.last_self_event_time
+        return None
+
+
+def grid_tie_world():
+    """A reactive dynamic plugin (GridKnock, src 7: the LARGEST src_id) beside a static
+    plugin (GridBursty, src 6) and a RealData controlled source (src 4), all on binary
+    grids: at an equal time the dynamic plugin plays first although its src_id is the
+    largest (run_dynamic plays a static time only when strictly earlier)."""
+    w = dict(src_id=4, end_time=30.0, s=1.0, q=1.0, sink_ids=[1, 2, 3, 4, 5, 6],
+             other_sources=[("GridBursty", {"src_id": 6, "seed": 12, "rate": 0.3, "size": 3}),
+                            ("GridKnock", {"src_id": 7, "seed": 21, "rate": 1.0})],
+             edge_list=[(7, 1), (7, 2), (7, 5), (6, 2), (6, 3), (6, 6), (4, 1), (4, 3), (4, 4),
+                        (4, 6)])
+    ctrl = [0.0, 1.5, 2.5, 4.0, 5.5, 7.0, 9.25, 12.0, 13.5, 16.0, 20.0, 22.5, 25.0, 27.5]
+    return w, ctrl, list(range(32))

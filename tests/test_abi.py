@@ -36,7 +36,7 @@ def test_status_bits_match_the_header():
 
 def test_version_and_errors():
     lib = L.lib()
-    assert lib.rq_abi_version() == L.ABI_VERSION == 5
+    assert lib.rq_abi_version() == L.ABI_VERSION == 6
     assert lib.rq_strerror(L.RQ_EINVAL) == b"invalid argument"
     assert lib.rq_strerror(-99) == b"unknown error"
 
@@ -98,6 +98,28 @@ def test_graph_build_validation(case, expect):
         assert rc not in (L.RQ_EINVAL, L.RQ_EUNSUPPORTED), rc
     else:
         assert rc == expect
+
+
+def test_source_flags_validation():
+    """rq_source_desc.flags (ABI v6): RQ_SRCF_DYNAMIC only on a RealData source (a dynamic
+    broadcaster's replayed times); any other bit is refused."""
+    def build(kind, flags):
+        d, keep = _desc([1, 2], [(2, 1)], [(kind, 2, None)])
+        d.sources[0].flags = flags
+        if kind == L.SRC_REALDATA:
+            t = np.asarray([0.5, 1.5])
+            keep.append(t)
+            d.sources[0].n_arr, d.sources[0].a = 2, t.ctypes.data_as(L._pd)
+        h = C.c_void_p()
+        return L.lib().rq_graph_build(C.byref(d), C.byref(h))
+    assert build(L.SRC_POISSON2, L.SRCF_DYNAMIC) == L.RQ_EINVAL
+    assert build(L.SRC_HAWKES, L.SRCF_DYNAMIC) == L.RQ_EINVAL
+    assert build(L.SRC_REALDATA, 2) == L.RQ_EINVAL
+    assert build(L.SRC_REALDATA, L.SRCF_DYNAMIC) not in (L.RQ_EINVAL, L.RQ_EUNSUPPORTED)
+    src = open(os.path.join(ROOT, "include", "rq.h")).read()
+    assert re.search(r"#define RQ_SRCF_DYNAMIC\s+%d\b" % L.SRCF_DYNAMIC, src)
+    assert "const int64_t* rep_idx;" in src   # the replica list closes rq_batch_desc
+    assert [f[0] for f in L.BatchDesc._fields_][-1] == "rep_idx"
 
 
 def test_workspace_queries_validate():

@@ -162,9 +162,10 @@ def test_65000_sources_fast_equals_sequential():
 
 def test_more_than_2048_sources_what_needs_the_sequential_sweep():
     """Past 2048 sources the runs that need the exact sequential sweep run on the merged
-    sequence (round 4: RQ_EUNSUPPORTED): a RealData source among 3000, max_events, and a
-    multigraph -- each == the engine oracle, and a 3000-source fast run == its sequential
-    twin on a continuous world."""
+    sequence (round 4: RQ_EUNSUPPORTED): a RealData source with repeated times among 3000
+    and a multigraph -- == the engine oracle; max_events among 3000 sources runs the fast
+    general sweep since round 6 (truncate_tile) -- == the engine oracle too; and a
+    3000-source fast run == its sequential twin on a continuous world."""
     torch, engine, graphs, O = _ctx()
     so = _many_sources(3000)
     # a RealData broadcaster (recorded times, with repeats) and a duplicated edge
@@ -172,10 +173,10 @@ def test_more_than_2048_sources_what_needs_the_sequential_sweep():
     so_rd = dict(so, other_sources=so["other_sources"] + [("RealData", {"src_id": 9000, "times": rd})],
                  edge_list=so["edge_list"] + [(9000, 3), (9000, 7), (1000, so["edge_list"][30][1])])
     Ks = (1, 3)
-    for world, kw in ((so_rd, {}), (so, dict(max_events=400))):
+    for world, kw, seq in ((so_rd, {}, True), (so, dict(max_events=400), False)):
         g = _graph(engine, world)
         plan = g.run("opt", q=1.0, s=1.0, n_rep=3, plan_only=True, **kw)
-        assert plan["variant"] in (1, 4) and plan["sources_per_lane"] == 0, plan
+        assert (plan["variant"] in (1, 4)) == seq and plan["sources_per_lane"] == 0, plan
         res = g.run("opt", q=1.0, s=1.0, n_rep=3, ctrl_seed=5, world_seed=5, randomize=True, Ks=Ks,
                     event_log=True, **kw)
         assert int((res.status & 3).max().item()) == 0

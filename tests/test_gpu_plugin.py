@@ -265,3 +265,55 @@ def test_dynamic_plugin_verified_beyond_replica_zero(n_rep, react):
     r5 = g2.run("times", n_rep=n_rep, world_seed=0, randomize=True, Ks=KS, replica0=0, n_local=5)
     assert not hasattr(g2, "reactive_reruns")
     assert np.array_equal(r5.metrics.cpu().numpy(), res.metrics.cpu().numpy()[:5])
+
+
+def _grid_setup():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from realdata_worlds import GridBurstyMixin, GridKnockMixin, grid_tie_world
+    from redqueen_amd import engine
+    from redqueen_amd.opt_model import Broadcaster, SimOpts
+
+    class GridBursty(GridBurstyMixin, Broadcaster):
+        pass
+
+    class GridKnock(GridKnockMixin, Broadcaster):
+        pass
+    SimOpts.registerSource("GridBursty", GridBursty)
+    SimOpts.registerSource("GridKnock", GridKnock)
+    return engine, SimOpts, grid_tie_world()
+
+
+def test_reactive_plugin_equal_time_order(golden):
+    """a reactive dynamic plugin whose posts land EXACTLY on static sources'
+    times (every source on a binary grid; tests/golden/gridtie.npz, 2-12 such ties per
+    world).  run_dynamic plays a static time only when it is strictly earlier than the
+    dynamic sources' next event (opt_model.py:289-290), so at an equal time the plugin
+    (src 7, the largest id) plays BEFORE the RealData controlled source (4) and the static
+    plugin (6): the host fixed point (reactive_plugin_times, static_ids), the stream
+    order of the graph (dynamic sources first, RQ_SRCF_DYNAMIC) and the controller flags
+    all follow it.  The manager's df and the 32-replica randomized batch equal the
+    reference's bit for bit."""
+    engine, SimOpts, (w, ctrl, us) = _grid_setup()
+    from redqueen_amd import utils as U
+    d = golden("gridtie.npz")
+    assert (d["rand_ties"] > 0).all()
+    so = SimOpts(**w)
+    m = so.create_manager_with_times(np.asarray(ctrl))
+    m.run_dynamic()
+    df = m.state.get_dataframe()
+    for c in COLS:
+        assert np.array_equal(df[c].values, d["base_" + c]), c
+    got = U.replay_metrics(df, so.src_id, so.end_time, KS)
+    assert np.array_equal(np.asarray(got["top_k"] + [got["avg_rank"], got["r_2"]]), d["base_met"])
+    g = engine.Graph(w["src_id"], w["other_sources"], w["sink_ids"], w["edge_list"],
+                     w["end_time"], ctrl_a=ctrl)
+    assert g.static_src_ids == {6}
+    # the stream order: the dynamic plugin's stream before every static one
+    assert list(g.stream_src_ids) == [7, 4, 6]
+    res = g.run("times", n_rep=len(us), world_seed=0, randomize=True, Ks=KS)
+    mm = res.metrics.cpu().numpy()
+    c = res.counts.cpu().numpy()
+    assert np.array_equal(mm, d["rand_met"]), mm - d["rand_met"]
+    assert np.array_equal(c[:, :3], d["rand_cnt"])
