@@ -6,8 +6,50 @@ there is no CPU fallback.
 """
 import ctypes as C
 import os
+import warnings
 
 import torch  # noqa: F401  -- load torch's HIP runtime first so librq.so binds to it
+
+# HIP hardware queues per process.  rq_run_batch pipelines a batch's chunks on two
+# streams and an RCCL group adds its own; at HIP's default of 4 queues the engine's two
+# streams then share one queue and the pipeline serialises (C3: 2.93 -> 3.42 ms per step
+# with a world-size-1 group, profiles/r05_dist_queues.txt).  HIP reads the count when it
+# initialises, so the package raises it to HW_QUEUES_MIN at import when the caller has
+# not set it and HIP is not up yet; otherwise dist.run_sharded warns once (hw_queue_advice).
+HW_QUEUES_MIN = 8
+HW_QUEUES_SET_BY_PACKAGE = False
+if "GPU_MAX_HW_QUEUES" not in os.environ and not torch.cuda.is_initialized():
+    os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES_MIN)
+    HW_QUEUES_SET_BY_PACKAGE = True
+# the count this process's HIP runtime uses: None = unknown (HIP was up before the import
+# and the variable unset, i.e. HIP's default of 4)
+HW_QUEUES = int(os.environ["GPU_MAX_HW_QUEUES"]) if "GPU_MAX_HW_QUEUES" in os.environ else None
+
+
+def hw_queue_advice(group_live, queues=-1):
+    """The warning an engine run under a live process group deserves when its HIP
+    runtime has fewer than HW_QUEUES_MIN hardware queues (None: no warning).  queues:
+    the count to judge (None: unset, HIP's default); -1: this process's (HW_QUEUES)."""
+    q = HW_QUEUES if queues == -1 else queues
+    if not group_live or (q is not None and q >= HW_QUEUES_MIN):
+        return None
+    return ("redqueen_amd: GPU_MAX_HW_QUEUES=%s with a process group open: the RCCL streams and "
+            "the engine's two pipeline streams share HIP's hardware queues and the pipeline "
+            "serialises (C3: ~17%% slower per step).  Set GPU_MAX_HW_QUEUES=%d before HIP "
+            "initialises (before the first torch.cuda call)."
+            % ("unset (4)" if q is None else q, HW_QUEUES_MIN))
+
+
+_warned_queues = False
+
+
+def warn_hw_queues(group_live):
+    global _warned_queues
+    msg = hw_queue_advice(group_live)
+    if msg and not _warned_queues:
+        _warned_queues = True
+        warnings.warn(msg, RuntimeWarning, stacklevel=3)
+    return msg
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 SO_PATH = os.environ.get("RQ_SO_PATH") or os.path.join(_HERE, "librq.so")   # env: A/B builds only

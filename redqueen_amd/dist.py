@@ -96,6 +96,8 @@ def run_sharded(graph, n_grid, n_rep, world=None, rank=None, group=None, force=F
     [n_grid*n_rep, nK+2] and counts [n_grid*n_rep, 4] (and this rank's BatchResult).
     ``force``: exchange through the collective even for a world of one."""
     world, rank = _world_rank(world, rank, group)
+    from . import _lib as L
+    L.warn_hw_queues(dist.is_initialized() and dist.get_backend(group) != "gloo")
     lo, hi = grid_shard(n_rep, world, rank)
     if hi > lo:
         res = graph.run(n_rep=n_rep, rep_lo=lo, rep_cnt=hi - lo, **run_kw)

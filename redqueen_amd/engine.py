@@ -205,7 +205,8 @@ class Graph:
     def _run(self, ctrl="opt", q=1.0, s=None, n_rep=1, ctrl_seed=0, world_seed=0,
             randomize=False, seed_mod=0, ctrl_rate=None, Ks=(1,), max_events=None,
             event_log=False, cap_scale=1.0, chunk=0, stream=None, check=True, sweep_mode=0, replica0=0, n_local=0,
-            plan_only=False, s_pw=None, period=None, rep_lo=0, rep_cnt=0, rd_override=None):
+            plan_only=False, s_pw=None, period=None, rep_lo=0, rep_cnt=0, rd_override=None,
+            rd_streams=None, rep_idx=None):
         """Enqueue one batch.  ``q``: scalar or [n_grid]; ``s``: per grid point
         row(s) over the sorted followers ([n_grid, F]) or anything ``s_matrix``
         takes.  Seeds: int base (seed + replica id) or a device uint32 tensor.
@@ -213,7 +214,14 @@ class Graph:
         sorted followers and ``period`` T.
         ``rep_lo`` / ``rep_cnt``: run only replicas [rep_lo, rep_lo + rep_cnt) of every grid
         point (a balanced multi-GPU shard, rq_batch_desc.rep_lo); ``replica0`` / ``n_local``
-        then index that n_grid x rep_cnt space, and so do the outputs."""
+        then index that n_grid x rep_cnt space, and so do the outputs.
+        ``rd_streams = (src_ids, times, off, caps)``: per-replica times of the graph's
+        RealData sources ``src_ids`` (declared with no times) already on the device --
+        replica i (global id) plays times[off[i * n + k] .. off[i * n + k + 1]) for source
+        k, sorted, within [start_time, end_time]; ``caps[k]`` >= any replica's count
+        (rq_batch_desc.rd_*, read in place: no host pass per replica).
+        ``rep_idx``: run exactly these global replica ids (rq_batch_desc.rep_idx; replica0,
+        n_local and the rep_lo / rep_cnt window are then ignored); output k = rep_idx[k]."""
         dev = torch.device("cuda", torch.cuda.current_device())
         ck = CTRL_BY_NAME[ctrl] if isinstance(ctrl, str) else int(ctrl)
         qv = _arr(np.atleast_1d(q), np.float64)
@@ -245,6 +253,11 @@ class Graph:
         # global replica ids of this call's outputs (rq_global_replica)
         sp = np.arange(int(replica0), int(replica0) + R, dtype=np.int64)
         gids = sp if cnt == int(n_rep) else (sp // cnt) * int(n_rep) + lo + sp % cnt
+        if rep_idx is not None:
+            gids = _arr(rep_idx, np.int64)
+            R, replica0, n_local, lo, rep_cnt = gids.size, 0, gids.size, 0, 0
+            if R < 1 or gids.min() < 0 or gids.max() >= R_all:
+                raise ValueError("rep_idx: global ids in [0, n_grid * n_rep) expected")
         Ks = _arr(Ks, np.int32)
         if not 1 <= Ks.size <= L.MAX_K:
             raise ValueError("1..%d K values per run" % L.MAX_K)
@@ -269,7 +282,25 @@ class Graph:
         else:
             b.world_seed0 = int(world_seed) & 0xFFFFFFFF
         b.seed_mod = int(seed_mod)
-        if self.plugins and (randomize or rd_override is not None):
+        if rd_streams is not None:
+            if self.plugins:
+                raise ValueError("rd_streams and registered plugin broadcasters are exclusive")
+            sids, td, to, caps = rd_streams
+            sid = _arr(sids, np.int64)
+            cap = _arr(caps, np.int64)
+            if not (torch.is_tensor(td) and torch.is_tensor(to) and td.dtype == torch.float64 and
+                    to.dtype == torch.int64 and td.is_cuda and to.is_cuda and to.is_contiguous()
+                    and td.is_contiguous() and to.numel() == R_all * sid.size + 1
+                    and cap.size == sid.size and 1 <= sid.size <= L.MAX_RD):
+                raise ValueError("rd_streams: (src_ids[n], device f64 times, device i64 "
+                                 "off[n_grid * n_rep * n + 1], caps[n]) expected")
+            keep += [sid, cap, td, to]
+            b.n_rd = sid.size
+            b.rd_src_id = sid.ctypes.data_as(L._pi64)
+            b.rd_cap = cap.ctypes.data_as(L._pi64)
+            b.rd_times = td.data_ptr()
+            b.rd_off = to.data_ptr()
+        elif self.plugins and (randomize or rd_override is not None):
             self._plugin_streams(b, keep, dev, R_all, gids, world_seed, int(seed_mod), rd_override)
         if ck == L.SRC_POISSON2:
             if ctrl_rate is None:
@@ -292,6 +323,9 @@ class Graph:
         b.n_local = int(n_local)
         b.rep_lo = lo
         b.rep_cnt = int(rep_cnt)
+        if rep_idx is not None:
+            keep.append(gids)
+            b.rep_idx = gids.ctypes.data_as(L._pi64)
         if spw is not None:
             b.n_seg = spw.shape[2]
             b.period = float(period)
@@ -414,20 +448,7 @@ class Graph:
         sub.sweep_mode = int(mode)
         sub.chunk = 0
         r = self._launch(lib, sub, dev, int(idx.size), Ks, n_grid, n_rep, event_log, use)
-        at = torch.from_numpy(np.asarray(pick, dtype=np.int64)).to(dev)
-        res.metrics.index_copy_(0, at, r.metrics)
-        res.counts.index_copy_(0, at, r.counts)
-        res.status.index_copy_(0, at, r.status)
-        if event_log:
-            cap, cap2 = res.ev_t.shape[1], r.ev_t.shape[1]
-            if cap2 > cap:   # a larger event capacity: widen every replica's log row
-                t2 = torch.empty((res.ev_t.shape[0], cap2), dtype=res.ev_t.dtype, device=dev)
-                s2 = torch.empty((res.ev_src.shape[0], cap2), dtype=res.ev_src.dtype, device=dev)
-                t2[:, :cap] = res.ev_t
-                s2[:, :cap] = res.ev_src
-                res.ev_t, res.ev_src = t2, s2
-            res.ev_t[at, :cap2] = r.ev_t
-            res.ev_src[at, :cap2] = r.ev_src
+        _scatter(res, pick, r, dev, event_log)
 
     def _ws_budget(self, dev, sk=None):
         """The workspace's device-memory budget (rq_batch_desc.ws_budget): 0.9 x what this
@@ -537,12 +558,15 @@ class Graph:
         """A batch whose dynamic plugins react to other sources' events, played to the
         fixed point of run_dynamic's loop: every replica's plugin times are recomputed
         from its run's other events (opt_model.reactive_plugin_times, a fresh plugin
-        instance per replica) and the replicas whose times moved are replayed with them
-        (per-replica RealData streams), until no replica's times move; events before a
-        plugin event whose time changed never change (every source sees only earlier
-        events), so each rerun fixes at least one more plugin event of every replica still
-        moving.  At most REACTIVE_MAX_ITERATIONS reruns, else NotImplementedError.  Cost:
-        one event-logged run and a host pass over every moving replica's events per rerun."""
+        instance per replica) and ONLY the replicas whose times moved are replayed with
+        them (per-replica RealData streams, a replica list: rq_batch_desc.rep_idx), until
+        no replica's times move; events before a plugin event whose time changed never
+        change (every source sees only earlier events), so each rerun fixes at least one
+        more plugin event of every replica still moving.  Each replica's result is the
+        probe in which its times reproduced themselves (no extra final run).  At most
+        max(REACTIVE_MAX_ITERATIONS, 2 x the most plugin events of a replica + 16) reruns,
+        else NotImplementedError.  Cost per rerun: one event-logged run of the moving
+        replicas and a host pass over their events."""
         from .opt_model import REACTIVE_MAX_ITERATIONS, reactive_plugin_times
         gids = np.asarray(res.global_ids, dtype=np.int64)
         ws = kw.get("world_seed", 0)
@@ -562,13 +586,26 @@ class Graph:
             return [cls(**kw_) for _idx, cls, kw_, _sid, _dyn in self.plugins]
         times = {int(i): [self._plugin_source_times(inst) for inst in make(int(i))] for i in gids}
         probe_kw = dict(kw, event_log=True, check=True)
-        moving = range(len(gids))
-        for it in range(REACTIVE_MAX_ITERATIONS + 1):
-            probe = self._run(*args, **dict(probe_kw, rd_override=times))
+        dev = torch.device("cuda", torch.cuda.current_device())
+        out = None
+        moving = np.arange(len(gids))
+        n_max = max((len(t) for ts in times.values() for t in ts), default=0)
+        cap_it = max(REACTIVE_MAX_ITERATIONS, 2 * n_max + 16)
+        self.reactive_replayed = 0
+        for it in range(cap_it + 1):
+            pk = dict(probe_kw, rd_override=times)
+            if out is not None:   # only the replicas still moving
+                pk["rep_idx"] = gids[moving]
+            probe = self._run(*args, **pk)
+            if out is None:
+                out = probe
+            else:
+                _scatter(out, moving, probe, dev, True)
+            self.reactive_replayed += len(moving)
             nxt = []
-            for k in moving:
+            for kl, k in enumerate(moving):
                 i = int(gids[k])
-                t_ev, s_ev = probe.events(k)
+                t_ev, s_ev = probe.events(kl)
                 insts, cur = make(i), times[i]
                 new = list(cur)
                 for c, p in enumerate(self.plugins):
@@ -581,12 +618,16 @@ class Graph:
                     nxt.append(k)
             if not nxt:
                 break
-            if it == REACTIVE_MAX_ITERATIONS:
+            if it == cap_it:
                 raise NotImplementedError("reactive dynamic broadcasters: no fixed point after %d "
-                                          "reruns" % REACTIVE_MAX_ITERATIONS)
-            moving = nxt
+                                          "reruns" % cap_it)
+            moving = np.asarray(nxt, dtype=np.int64)
         self.reactive_reruns = it
-        return self._run(*args, **dict(kw, rd_override=times))
+        if not kw.get("event_log"):
+            out.ev_t = out.ev_src = None
+        out.global_ids = gids
+        out.replica0 = int(gids[0]) if len(gids) else 0
+        return out
 
     def _plan_variant(self, lib, b):
         info = (C.c_int64 * 8)()
@@ -697,3 +738,22 @@ def expected_events(graph_kw):
             br = kw.get("alpha", 1.0) / kw.get("beta", 10.0)
             tot += kw.get("l_0", 1.0) * span / max(1e-9, 1 - br)
     return tot if math.isfinite(tot) else 0.0
+
+
+def _scatter(res, pick, r, dev, event_log):
+    """Rows of BatchResult ``r`` into outputs ``pick`` of ``res`` (event logs widened to
+    the larger capacity when ``event_log``)."""
+    at = torch.from_numpy(np.asarray(pick, dtype=np.int64)).to(dev)
+    res.metrics.index_copy_(0, at, r.metrics)
+    res.counts.index_copy_(0, at, r.counts)
+    res.status.index_copy_(0, at, r.status)
+    if event_log:
+        cap, cap2 = res.ev_t.shape[1], r.ev_t.shape[1]
+        if cap2 > cap:   # a larger event capacity: widen every replica's log row
+            t2 = torch.empty((res.ev_t.shape[0], cap2), dtype=res.ev_t.dtype, device=dev)
+            s2 = torch.empty((res.ev_src.shape[0], cap2), dtype=res.ev_src.dtype, device=dev)
+            t2[:, :cap] = res.ev_t
+            s2[:, :cap] = res.ev_src
+            res.ev_t, res.ev_src = t2, s2
+        res.ev_t[at, :cap2] = r.ev_t
+        res.ev_src[at, :cap2] = r.ev_src

@@ -1,16 +1,20 @@
 """Secondary measurements (not the bench line): the HBM-facing kernels of the path.
 
-  * sweep with the event log on (RQ_RUN_EVENT_LOG, the sequential-exact variant):
-    writes 12 B per event (t f64 + source i32) + 24 B per pivot row
+  * sweep with the event log on (RQ_RUN_EVENT_LOG, the fast merged sweep since round 6;
+    10k replicas): writes 12 B per event (t f64 + source i32) + 24 B per pivot row and
+    reads 10 B per merged wall entry
   * rq_log_rows + rq_log_expand: State.get_dataframe rows for a whole batch,
     12 B read per event + 40 B written per (event, sink) row
   * rq_scan: 24 B read per pivot row (timed inside the plain C3 run)
   * rq_metrics_replay_batch on the 256 exported C3 dataframes (24 B read per df row,
     32 B with event ids) and rq_metrics_replay on one df through the pandas facade
   * rq_oracle_dp: n = 8000 walls, 64 instances
-  * the exact sequential sweep (the fallback for multigraphs, > 512 sources and
-    max_events): the C3 network with duplicated edges, a 600-source world, C3 with a
-    max_events cap -- replicas/s and events/s
+  * the exact sequential sweep (the fallback for multigraphs and repeated RealData
+    times): the C3 network with duplicated edges, a 600-source world, C3 with a
+    max_events cap forced onto it (seq_max_events_c3) -- replicas/s and events/s
+  * the fast paths round 6 opened: C3 with max_events = 4000 (fast_max_events_c3: the
+    tile cut), C3 with a per-replica RealData stream handed over as device arrays
+    (fast_realdata_c3: rq_batch_desc.rd_*)
 Per-kernel times come from the library's HIP events (rq_timing) on the launch stream.
 --only a,b runs just those sections, so a rocprofv3 PMC pass can hold ONE workload
 (scripts/gpu_paths_pmc.sh).
@@ -34,7 +38,8 @@ PEAK = 8000.0
 SECTIONS = ["sweep_event_log", "log_expand", "scan", "replay_batch", "replay_batch_eid", "replay_batch_1024",
             "replay_batch_eid_chunked", "replay_one_df", "replay_one_df_one_workgroup",
             "replay_one_df_facade", "oracle_dp", "seq_multigraph_c3", "seq_600_sources",
-            "seq_max_events_c3", "fast_600_sources", "fast_3000_sources"]
+            "seq_max_events_c3", "fast_max_events_c3", "fast_realdata_c3", "fast_600_sources",
+            "fast_3000_sources"]
 REPLAY = {"log_expand", "replay_batch", "replay_batch_eid", "replay_batch_1024", "replay_batch_eid_chunked",
           "replay_one_df", "replay_one_df_one_workgroup", "replay_one_df_facade"}
 
@@ -61,15 +66,19 @@ def graph_of(so):
 
 
 def sweep_event_log(g, so, a, res):
-    R = 2048
+    R = 10000
     run = lambda: g.run("opt", q=so["q"], s=so["s"], n_rep=R, ctrl_seed=0, world_seed=0,  # noqa: E731
                         randomize=True, event_log=True, check=False)
     r, ms, wall = timed(run, a.reps)
     ev = int(r.counts[:, 2].sum())
     rows = int(r.counts[:, 3].sum())
-    b = 12 * ev + 24 * rows
-    res["sweep_event_log"] = {"replicas": R, "events": ev, "ms": ms[1], "bytes": b,
-                              "GBps": b / ms[1] / 1e6, "frac": b / ms[1] / 1e6 / PEAK}
+    walls = int(r.counts[:, 2].sum() - r.counts[:, 0].sum())
+    b = 12 * ev + 24 * rows + 10 * walls
+    plan = g.run("opt", q=so["q"], s=so["s"], n_rep=R, event_log=True, randomize=True, plan_only=True)
+    res["sweep_event_log"] = {"replicas": R, "events": ev, "rows": rows, "ms": ms[1],
+                              "launches_per_run": 2, "bytes": b,
+                              "bytes_note": "12 B/event logged + 24 B/pivot row + 10 B/merged wall entry read",
+                              "GBps": b / ms[1] / 1e6, "frac": b / ms[1] / 1e6 / PEAK, "plan": plan}
 
 
 def scan(g, so, a, res):
@@ -194,8 +203,15 @@ def seq_world(name):
     if name == "fast_3000_sources":
         return graphs.followers_graph(num_followers=3000, num_sources=3000, degree=5,
                                       end_time=4.0, world_rate=1.0, alpha=1.0, beta=10.0), None
-    if name == "seq_max_events_c3":
+    if name in ("seq_max_events_c3", "fast_max_events_c3"):
         return graphs.c3(), 4000
+    if name == "fast_realdata_c3":
+        # C3 + one RealData broadcaster (src 9000, declared without times) into 40
+        # followers; each replica plays its own ~100 times (rate 1 over T = 100)
+        so = graphs.c3()
+        fol = sorted({b for a_, b in so["edge_list"] if a_ != so["src_id"]})[::25]
+        return dict(so, other_sources=so["other_sources"] + [("RealData", {"src_id": 9000, "times": []})],
+                    edge_list=so["edge_list"] + [(9000, f) for f in fol]), None
     raise KeyError(name)
 
 
@@ -203,15 +219,24 @@ def seq(name, a, res, R=4096):
     so, max_ev = seq_world(name)
     g = graph_of(so)
     kw = dict(q=so["q"], s=so["s"], n_rep=R, ctrl_seed=0, world_seed=0, randomize=True,
-              max_events=max_ev, Ks=(1,), sweep_mode=2 if name == "seq_600_sources" else 0)
-    plan = g.run("opt", plan_only=True, **kw)
+              max_events=max_ev, Ks=(1,),
+              sweep_mode=2 if name in ("seq_600_sources", "seq_max_events_c3") else 0)
+    if name == "fast_realdata_c3":
+        n = 100
+        gen = torch.Generator(device="cuda").manual_seed(9)
+        t = torch.sort(torch.rand((R, n), generator=gen, device="cuda", dtype=torch.float64) *
+                       so["end_time"], dim=1).values.contiguous().reshape(-1)
+        off = torch.arange(0, R * n + 1, n, dtype=torch.int64, device="cuda")
+        kw["rd_streams"] = ([9000], t, off, [n])
+    plan = g.run("opt", plan_only=True, **{k: v for k, v in kw.items() if k != "rd_streams"})
     r, ms, wall = timed(lambda: g.run("opt", check=False, **kw), a.reps)
     ev = int(r.counts[:, 2].sum())
     res[name] = {"replicas": R, "sources": len(so["other_sources"]), "sinks": len(so["sink_ids"]),
                  "edges": len(so["edge_list"]), "max_events": max_ev, "events": ev,
                  "events_per_replica": ev / R, "sweep_ms": ms[1], "step_ms": wall * 1e3,
                  "replicas_per_s": R / wall, "events_per_s": ev / wall,
-                 "status_max": int(r.status.max().item()), "plan": plan}
+                 "status_max": int(r.status.max().item()),
+                 "tie_replicas": int(((r.status & L.ST_TIE) != 0).sum().item()), "plan": plan}
 
 
 def main():
@@ -236,8 +261,8 @@ def main():
         scan(g, so, a, res)
     if want("oracle_dp"):
         oracle(a, res)
-    for k in ("seq_multigraph_c3", "seq_600_sources", "seq_max_events_c3", "fast_600_sources",
-              "fast_3000_sources"):
+    for k in ("seq_multigraph_c3", "seq_600_sources", "seq_max_events_c3", "fast_max_events_c3",
+              "fast_realdata_c3", "fast_600_sources", "fast_3000_sources"):
         if want(k):
             seq(k, a, res)
     print(json.dumps(res))

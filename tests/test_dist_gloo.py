@@ -9,6 +9,8 @@ import torch.multiprocessing as mp
 
 from redqueen_amd import dist as D
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
 
 def _port():
     s = socket.socket()
@@ -86,3 +88,30 @@ def test_grid_shards_see_every_grid_point():
             assert all(wins[k][1] == wins[k + 1][0] for k in range(w - 1))
             sizes = [n_grid * (hi - lo) for lo, hi in wins]
             assert max(sizes) - min(sizes) <= n_grid
+
+
+def test_hw_queue_requirement_without_the_callers_help():
+    """the engine's two pipeline streams need >= 8 HIP hardware
+    queues beside an RCCL group.  Importing the package raises GPU_MAX_HW_QUEUES to 8
+    when the caller left it unset (HIP not up yet); a caller who set fewer is warned once
+    by dist.run_sharded under a live nccl group (gloo groups exchange host tensors)."""
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k != "GPU_MAX_HW_QUEUES"}
+    out = subprocess.run([sys.executable, "-c",
+                          "import os, redqueen_amd._lib as L; "
+                          "print(os.environ['GPU_MAX_HW_QUEUES'], L.HW_QUEUES, L.HW_QUEUES_SET_BY_PACKAGE)"],
+                         env=env, capture_output=True, text=True, cwd=ROOT, timeout=300)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.split() == ["8", "8", "True"]
+    env["GPU_MAX_HW_QUEUES"] = "4"   # the caller's own choice is kept, and reported
+    out = subprocess.run([sys.executable, "-c",
+                          "import os, redqueen_amd._lib as L; "
+                          "print(os.environ['GPU_MAX_HW_QUEUES'], L.HW_QUEUES_SET_BY_PACKAGE, "
+                          "L.hw_queue_advice(True) is not None, L.hw_queue_advice(False))"],
+                         env=env, capture_output=True, text=True, cwd=ROOT, timeout=300)
+    assert out.stdout.split() == ["4", "False", "True", "None"], out.stdout + out.stderr
+    from redqueen_amd import _lib as L
+    assert L.hw_queue_advice(True, 8) is None and L.hw_queue_advice(True, 32) is None
+    assert "GPU_MAX_HW_QUEUES=8" in L.hw_queue_advice(True, 4)
+    assert "unset" in L.hw_queue_advice(True, None)

@@ -130,3 +130,39 @@ def test_tie_flagged_replicas_rerun_on_the_exact_sweep():
     assert g.reruns == tied
     seq = g.run("opt", sweep_mode=2, **kw)
     _same(torch, got, seq)
+
+
+def test_device_realdata_streams_on_the_fast_sweep():
+    """Per-replica RealData times handed over as device arrays (Graph.run(rd_streams=...),
+    rq_batch_desc.rd_*): the fast sweep plays them (no graph-level repeats), and replica
+    k equals a one-replica run whose graph carries replica k's times as its own RealData
+    source (same seeds), and the engine oracle."""
+    torch, L, engine, graphs = _ctx()
+    from oracle import oracle as O
+    so = graphs.c3()
+    fol = sorted({b for a_, b in so["edge_list"] if a_ != so["src_id"]})[::25]
+    base = dict(so, edge_list=so["edge_list"] + [(9000, f) for f in fol])
+    world = dict(base, other_sources=so["other_sources"] + [("RealData", {"src_id": 9000, "times": []})])
+    g = _graph(engine, world)
+    R, n = 6, 40
+    rs = np.random.RandomState(11)
+    host = [np.sort(rs.uniform(0, so["end_time"], n)) for _ in range(R)]
+    t = torch.from_numpy(np.concatenate(host)).cuda()
+    off = torch.arange(0, R * n + 1, n, dtype=torch.int64, device="cuda")
+    kw = dict(q=so["q"], s=so["s"], ctrl_seed=40, world_seed=40, randomize=True, Ks=(1, 2))
+    plan = g.run("opt", n_rep=R, plan_only=True, **kw)
+    assert plan["variant"] % 10 not in (1, 4), plan
+    res = g.run("opt", n_rep=R, event_log=True, rd_streams=([9000], t, off, [n]), **kw)
+    assert int(res.status.max().item()) == 0
+    for k in (0, 3, R - 1):
+        wk = dict(base, other_sources=so["other_sources"] + [("RealData", {"src_id": 9000, "times": host[k]})])
+        gk = _graph(engine, wk)
+        one = gk.run("opt", n_rep=1, q=so["q"], s=so["s"], ctrl_seed=40 + k, world_seed=40 + k,
+                     randomize=True, Ks=(1, 2), event_log=True)
+        assert torch.equal(one.metrics[0], res.metrics[k]) and torch.equal(one.counts[0], res.counts[k])
+        # the engine oracle of replica k's world (randomize_other_sources(40 + k))
+        sc_so = dict(wk, other_sources=[(nm, dict(x, seed=40 + k + 99 * j) if "seed" in x else x)
+                                        for j, (nm, x) in enumerate(wk["other_sources"])])
+        t_o, _dt, s_o = O.engine_run(O.Scenario(sc_so, ("opt", 40 + k)))
+        te, se = res.events(k)
+        assert np.array_equal(te, t_o) and np.array_equal(se, s_o)
