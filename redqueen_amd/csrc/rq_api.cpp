@@ -86,15 +86,36 @@ struct TimedLaunch {
 struct SidePipe {
     int dev = -1;
     hipStream_t caller = nullptr;
+    uint64_t used = 0;   // last use (SidePipes' LRU clock)
     hipStream_t s[2] = {nullptr, nullptr};
     hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};
+    // drop the streams and events (made on device `dev`) once their work is done
+    void release()
+    {
+        if (dev < 0) return;
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        if (cur != dev) (void)hipSetDevice(dev);
+        for (int k = 0; k < 2; ++k) {
+            if (s[k]) {
+                (void)hipStreamSynchronize(s[k]);
+                (void)hipStreamDestroy(s[k]);
+            }
+            if (join[k]) (void)hipEventDestroy(join[k]);
+            s[k] = nullptr;
+            join[k] = nullptr;
+        }
+        if (fork) (void)hipEventDestroy(fork);
+        fork = nullptr;
+        if (cur >= 0 && cur != dev) (void)hipSetDevice(cur);
+        dev = -1;
+    }
     int get(int n, hipStream_t* out)
     {
         int d = 0;
         if (hipGetDevice(&d) != hipSuccess) return RQ_EHIP;
-        if (dev != d) {   // first use (or another device): fresh streams and events
-            for (int k = 0; k < 2; ++k) s[k] = nullptr, join[k] = nullptr;
-            fork = nullptr;
+        if (dev != d) {   // first use (or another device's pipe re-homed): fresh streams and events
+            release();
             dev = d;
         }
         if (!fork && hipEventCreateWithFlags(&fork, hipEventDisableTiming) != hipSuccess) return RQ_EHIP;
@@ -106,22 +127,34 @@ struct SidePipe {
         return RQ_OK;
     }
 };
-// a few caller streams per thread (the engine's users run on one or two); past kPipes
-// the least recently added entry is reused
+// a few (device, caller stream) pairs per thread (the engine's users run on one or two
+// streams); the null stream has the same handle on every device, hence the device in the
+// key.  Past kPipes the least recently used entry is re-homed: on the same device its
+// streams and events are kept (only the owner changes), on another they are destroyed
+// once idle and made afresh.
 constexpr int kPipes = 4;
 struct SidePipes {
     SidePipe p[kPipes];
-    int next = 0, used = 0;
+    uint64_t clock = 0;
     SidePipe& of(hipStream_t caller)
     {
-        for (int k = 0; k < used; ++k)
-            if (p[k].caller == caller) return p[k];
-        SidePipe& x = p[next];
-        next = (next + 1) % kPipes;
-        used = used < kPipes ? used + 1 : kPipes;
-        x.caller = caller;   // its streams and events are kept: only the owner changes
-        return x;
+        int d = -1;
+        (void)hipGetDevice(&d);
+        SidePipe* lru = &p[0];
+        for (SidePipe& x : p) {
+            if (x.used && x.caller == caller && (x.dev == d || x.dev < 0)) {
+                x.used = ++clock;
+                return x;
+            }
+            if (x.used < lru->used) lru = &x;
+        }
+        if (lru->dev >= 0 && lru->dev != d) lru->release();
+        lru->caller = caller;
+        lru->used = ++clock;
+        return *lru;
     }
+    // no destructor: a thread's pipes live until the process ends (HIP may already be
+    // torn down when thread_local destructors run at exit)
 };
 thread_local SidePipes t_pipes;
 

@@ -166,3 +166,23 @@ def test_device_realdata_streams_on_the_fast_sweep():
         t_o, _dt, s_o = O.engine_run(O.Scenario(sc_so, ("opt", 40 + k)))
         te, se = res.events(k)
         assert np.array_equal(te, t_o) and np.array_equal(se, s_o)
+
+
+def test_more_caller_streams_than_side_pipes():
+    """Batches issued round-robin on six caller streams -- more than the library's four
+    side-stream pipes per thread (rq_api.cpp SidePipes: keyed by device and caller stream,
+    least recently used re-homed) -- give the same rows as one stream."""
+    torch, L, engine, graphs = _ctx()
+    so = graphs.c3()
+    g = _graph(engine, so)
+    kw = dict(q=so["q"], s=so["s"], n_rep=2000, randomize=True, Ks=(1,), check=False)
+    ref = [g.run("opt", ctrl_seed=k, world_seed=k, **kw) for k in range(12)]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream() for _ in range(6)]
+    got = []
+    for k in range(12):
+        with torch.cuda.stream(streams[k % 6]):
+            got.append(g.run("opt", ctrl_seed=k, world_seed=k, **kw))
+    torch.cuda.synchronize()
+    for a, b in zip(ref, got):
+        assert torch.equal(a.metrics, b.metrics) and torch.equal(a.counts, b.counts)
