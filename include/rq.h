@@ -133,10 +133,11 @@ typedef struct rq_graph* rq_graph_t;
    the batch with doubled cap_scale (and remembers the scale for the graph's later runs);
    check=False hands the flagged rows back as they are, for the caller to mask or rerun. */
 #define RQ_ST_TIE 4              /* events at equal times shared a pivot row.  Exact (pivot cells
-                                    averaged like pandas) in the sequential sweep -- max_events,
-                                    sweep_mode 2, or any RealData stream; the fast
+                                    averaged like pandas) in the sequential sweep -- sweep_mode 2,
+                                    a multigraph, repeated graph-level RealData times; the fast
                                     tiled sweep keeps the last row, so for a replica flagged
-                                    here avg-rank / r^2 may differ: rerun it with sweep_mode 2 */
+                                    here avg-rank / r^2 may differ: rerun it with sweep_mode 2
+                                    (alone: rep_idx; Graph.run(check=True) does) */
 #define RQ_ST_EMPTY 8            /* no event reached any sink: the reference's df is empty      */
 #define RQ_ST_UNORDERED 16       /* a sequential run over > 2048 sources (merged streams) met more
                                     than 2048 arrivals at ONE time (replayed data only): their
@@ -172,8 +173,11 @@ typedef struct rq_batch_desc {
     int64_t n_local;             /* a shard of the grid (0 = all n_grid*n_rep); outputs are      */
                                  /* indexed locally, seeds and grid point use the global id     */
     int32_t sweep_mode;          /* 0 auto: a fast tiled sweep unless the run needs the exact
-                                    sequential one (max_events, RealData, a multigraph, > 512
-                                    sources); the fast sweeps write the event log themselves.
+                                    sequential one (a multigraph; the graph's own RealData
+                                    times repeat a time); max_events cuts the fast sweeps'
+                                    tiles, per-replica RealData streams play on them (a replica
+                                    meeting equal times is flagged RQ_ST_TIE); the fast sweeps
+                                    write the event log themselves.
                                     The fast sweeps play MERGED streams: rq_gen_streams writes
                                     every source's arrivals, rq_merge_streams merges them into
                                     one (t, stream) sequence per replica, and the sweep plays it

@@ -12,13 +12,16 @@ OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd "$ROOT"
-RND=${RND:-r05}
+RND=${RND:-r06}
 for WL in $WLS; do
   R=$([ "$WL" = c5 ] && echo 8192 || ([ "$WL" = c4 ] && echo 1000 || echo 10000))
   S=$([ "$WL" = c5 ] && echo 3 || echo 20)
   scripts/gpu_pmc.sh ${TAG}_pmc_$WL $WL $R > "$OUT/pmc_$WL.log" 2>&1 || { echo "pmc $WL failed"; tail -5 "$OUT/pmc_$WL.log"; exit 1; }
   cp "$ROOT/gpurun_out/pmc_${TAG}_pmc_$WL/summary.json" "profiles/${RND}_${WL}_pmc_summary.json"
   cp "$ROOT/gpurun_out/pmc_${TAG}_pmc_$WL/summary.txt" "$OUT/${WL}_pmc_summary.txt"
+  # the serialised kernel trace's stats (AMD_SERIALIZE_KERNEL=3: every launch alone on the
+  # chip, the duration bench.py's serial probe and roofline use)
+  find "$ROOT/gpurun_out/pmc_${TAG}_pmc_$WL/kts" -name "*kernel_stats.csv" -exec cp {} "$OUT/${WL}_kernel_stats_serial.csv" \;
   echo "pmc $WL ok"
   CPU=$([ "$WL" = c3 ] && echo "" || echo "--no-cpu")
   timeout -k 10 400 python3 -u bench.py --workload $WL --steps $S --warmup 2 $CPU > "$OUT/${WL}_bench.log" 2>&1 || { echo "$WL bench failed"; tail -5 "$OUT/${WL}_bench.log"; exit 1; }
