@@ -257,7 +257,7 @@ struct Plan {
     // flags, 1/c_j) in global memory: graphs whose tables do not fit LDS (the GT instances;
     // the sequential ones on merged streams always)
     bool gt = false;
-    size_t off_mt = 0, off_mj = 0, off_mlen = 0;
+    size_t off_mt = 0, off_mj = 0, off_mjh = 0, off_mlen = 0;
     int64_t mrg_stride = 0;   // merged entries per replica (capacity)
     int n_grp = 1;            // > RQ_MG_B sources: groups of the two-level merge
     int64_t sub_stride = 0;   //   entries per (replica, group) of the first level
@@ -761,6 +761,8 @@ void plan_layout(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     const int64_t mrgc = p->mrg ? C : 0;   // merged sequences: t f64, stream u16, length
     p->off_mt = o;      o = align_up(o + sizeof(double) * (size_t)mrgc * p->mrg_stride, A);
     p->off_mj = o;      o = align_up(o + sizeof(uint16_t) * (size_t)mrgc * p->mrg_stride, A);
+    // > 65535 streams: each entry's stream bits 16-23
+    p->off_mjh = o;     o = align_up(o + (g->n_str > 65535 ? (size_t)mrgc * p->mrg_stride : 0), A);
     p->off_mlen = o;    o = align_up(o + sizeof(int) * (size_t)mrgc, A);
     p->off_ord = o;     o = align_up(o + sizeof(int) * (size_t)(p->order ? C : 0), A);
     const size_t o_rows = o;
@@ -1294,6 +1296,7 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
             ma.end = g->end;
             ma.out_t = (double*)(wsb + p.off_mt);
             ma.out_j = (uint16_t*)(wsb + p.off_mj);
+            ma.out_jh = g->n_str > 65535 ? (uint8_t*)(wsb + p.off_mjh) : nullptr;
             ma.out_len = (int*)(wsb + p.off_mlen);
             ma.mrg_stride = p.mrg_stride;
             ma.status = out->status;
@@ -1306,7 +1309,8 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
                 // level 1: each group of RQ_MG_B streams into its own sequence
                 MergeArgs m1 = ma;
                 m1.out_t = (double*)(wsb + p.off_sub_t);
-                m1.out_j = (uint16_t*)(wsb + p.off_sub_j);
+                m1.out_j = (uint16_t*)(wsb + p.off_sub_j);   // group-local streams: u16 always
+                m1.out_jh = nullptr;
                 m1.out_len = (int*)(wsb + p.off_sub_len);
                 m1.mrg_stride = p.sub_stride;
                 if (rq_launch_merge_groups(m1, s) != hipSuccess) return RQ_EHIP;
@@ -1360,6 +1364,7 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
         if (p.mrg) {
             sa.mrg_t = (const double*)(wsb + p.off_mt);
             sa.mrg_j = (const uint16_t*)(wsb + p.off_mj);
+            sa.mrg_jh = g->n_str > 65535 ? (const uint8_t*)(wsb + p.off_mjh) : nullptr;
             sa.mrg_len = (const int*)(wsb + p.off_mlen);
             sa.mrg_stride = p.mrg_stride;
             if (p.order) {

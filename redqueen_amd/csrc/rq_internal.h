@@ -129,6 +129,7 @@ struct SweepArgs {
     // every source in play order, mrg_t / mrg_j [rl * mrg_stride + k], k < mrg_len[rl]
     const double* mrg_t;
     const uint16_t* mrg_j;
+    const uint8_t* mrg_jh;     // > 65535 streams: bits 16-23 of each entry's stream (else null)
     const int* mrg_len;
     int64_t mrg_stride;        // entries per replica of mrg_t / mrg_j
     // longest-first play order of the chunk's replicas (rq_order_replicas over mrg_len):
@@ -150,7 +151,8 @@ struct MergeArgs {
     int64_t slen_stride;
     double end;
     double* out_t;          // [C][mrg_stride]
-    uint16_t* out_j;        // [C][mrg_stride]
+    uint16_t* out_j;        // [C][mrg_stride] the stream (a group-local one at a two-level merge's first level)
+    uint8_t* out_jh;        // > 65535 streams: bits 16-23 of the stream (else null)
     int* out_len;           // [C]
     int64_t mrg_stride;     // capacity per replica: past it the replica is flagged RQ_ST_STREAM_OVERFLOW
     int32_t* status;        // RQ_ST_TIE (strict_ties: RQ_ST_UNORDERED) when > RQ_MG_CAP arrivals share one time
@@ -211,7 +213,9 @@ hipError_t rq_launch_merge(const MergeArgs& a, hipStream_t s);
 // the second level over the groups' sequences (a.sub_*, a.n_grp "streams")
 hipError_t rq_launch_merge_groups(const MergeArgs& a, hipStream_t s);
 hipError_t rq_launch_merge_sub(const MergeArgs& a, hipStream_t s);
-#define RQ_MAX_STREAMS_MRG 65535   // merged entries carry the stream as u16
+// merged entries carry the stream as u16 (+ a u8 of its high bits past 65535 streams);
+// the two-level merge takes up to RQ_MG_B groups of RQ_MG_B streams
+#define RQ_MAX_STREAMS_MRG (RQ_MG_B * RQ_MG_B)
 // longest-first order of n <= 65536 replicas by len (descending; ties in any order)
 hipError_t rq_launch_order(const int* len, int64_t n, int* order, hipStream_t s);
 hipError_t rq_launch_sweep_fw(const SweepArgs& a, int nK, int col16, int W, int bits, hipStream_t s);

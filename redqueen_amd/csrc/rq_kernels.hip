@@ -30,6 +30,7 @@
 #include "rq_sweep_core.h"
 #include "rq_gen.h"
 #include <type_traits>
+#include <algorithm>
 #include <cstdlib>
 
 #pragma clang fp contract(off)
@@ -42,8 +43,8 @@ using namespace rq;
 __global__ __launch_bounds__(256) void rq_gen_streams(GenArgs a)
 {
     const int64_t rl = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int j = blockIdx.y;
-    if (rl >= a.n_chunk) return;
+    const int j = (int)(blockIdx.z * gridDim.y + blockIdx.y);   // > 32768 streams fold into z
+    if (rl >= a.n_chunk || j >= a.n_str) return;
     const int64_t o = a.chunk0 + rl;      // local output index
     const int64_t i = rq_replica_of(a, o);   // global id (seeds)
     SrcGen gen;
@@ -280,6 +281,7 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
         __asm__ volatile("" : "+v"(x));
         t_ = a.mrg_t[x + e];
         j_ = a.mrg_j[x + e];
+        if (a.mrg_jh) j_ |= (int)a.mrg_jh[x + e] << 16;   // > 65535 streams
     };
     const int mlen = MRG ? a.mrg_len[rl] : 0;
     int mpos = 0;
@@ -1229,7 +1231,8 @@ static int occ_m(int nK, int bits, int wpb, size_t lds)
 hipError_t rq_launch_gen(const GenArgs& a, hipStream_t s)
 {
     if (a.n_chunk <= 0 || a.n_str <= 0) return hipSuccess;
-    dim3 grid((unsigned)((a.n_chunk + 255) / 256), (unsigned)a.n_str);
+    const unsigned gy = (unsigned)std::min(a.n_str, 32768);
+    dim3 grid((unsigned)((a.n_chunk + 255) / 256), gy, (unsigned)((a.n_str + gy - 1) / gy));
     hipLaunchKernelGGL(rq_gen_streams, grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }

@@ -115,9 +115,9 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
     constexpr int MG_TARGET = MgCfg<MG_B>::TARGET;
     __shared__ double bt[MG_CAP];          // round buffer (arrival order)
     __shared__ uint32_t bs[MG_CAP];        // (sub-bucket << MG_SB) | slot
-    __shared__ uint16_t bj[MG_CAP];
+    __shared__ uint32_t bj[MG_CAP];        // the arrival's stream
     __shared__ double st[MG_CAP];          // bucket order
-    __shared__ uint32_t sk[MG_CAP];        // (stream << MG_SB) | buffer index
+    __shared__ uint32_t sk[MG_CAP];        // (stream << MG_SB) | buffer index (streams < 2^21)
     __shared__ uint32_t cnt[MG_M];
     __shared__ uint32_t bbase[MG_M + 1];
     __shared__ double wmin[MG_W];
@@ -130,6 +130,10 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
     // [group MG_B, group MG_B + MG_B); one level: gridDim.y == 1
     const int grp = SUB ? 0 : (int)blockIdx.y, ngrp = SUB ? 1 : (int)gridDim.y;
     const int j = (SUB ? 0 : grp * MG_B) + tid;
+    // the stream id an entry carries out: group-local at a two-level merge's first level
+    // (< RQ_MG_B: u16 whatever the source count), global otherwise; the second level
+    // (SUB) turns its group g's local ids back into global ones, g RQ_MG_B + local
+    const uint32_t jout = SUB ? (uint32_t)tid * RQ_MG_B : (uint32_t)(j - grp * MG_B);
     int L = 0;
     const double* src = a.streams;
     const uint16_t* srcj = nullptr;   // SUB: the entries' own stream ids
@@ -258,7 +262,7 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
                     const int sb = sub_of<MG_M>(cv[k], t_lo, scale);
                     const uint32_t slot = atomicAdd(&cnt[sb], 1u);
                     bt[idx] = cv[k];
-                    bj[idx] = (uint16_t)(SUB ? selj16(cj, nxj, k) : (uint32_t)j);
+                    bj[idx] = SUB ? jout + selj16(cj, nxj, k) : jout;
                     bs[idx] = ((uint32_t)sb << MG_SB) | slot;
                 }
             }
@@ -288,7 +292,7 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
                     const int sb = sub_of<MG_M>(head, t_lo, scale);
                     const uint32_t slot = atomicAdd(&cnt[sb], 1u);
                     bt[idx] = head;
-                    bj[idx] = (uint16_t)(SUB ? selj16(cj, nxj, p - p8) : (uint32_t)j);
+                    bj[idx] = SUB ? jout + selj16(cj, nxj, p - p8) : jout;
                     bs[idx] = ((uint32_t)sb << MG_SB) | slot;
                     ++p;
                     if (p - p8 == 16 && p < L) RQ_MG_RELOAD(p);   // a burst: both chunks consumed
@@ -406,6 +410,7 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
                 out_t[outpos + g0 + r] = x;
                 out_j[outpos + g0 + r] = (uint16_t)(kx >> MG_SB);
             }
+            if (a.out_jh) a.out_jh[(rl * ngrp + grp) * a.mrg_stride + outpos + g0 + r] = (uint8_t)(kx >> (MG_SB + 16));
         }
         RQ_MG_TICK(6);
         outpos += nr;

@@ -5,7 +5,7 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/ev06
 mkdir -p "$OUT"
 cd "$ROOT"
-timeout -k 10 700 python3 -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > "$OUT/pytest.log" 2>&1 || { echo "pytest failed"; grep -E "FAILED|Error" "$OUT/pytest.log" | head; tail -3 "$OUT/pytest.log"; exit 1; }
+timeout -k 10 700 python3 -u -m pytest tests -m gpu -q --durations=25 --timeout 300 --timeout-method thread > "$OUT/pytest.log" 2>&1 || { echo "pytest failed"; grep -E "FAILED|Error" "$OUT/pytest.log" | head; tail -3 "$OUT/pytest.log"; exit 1; }
 tail -1 "$OUT/pytest.log"
 timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { echo "smoke failed"; tail -5 "$OUT/smoke.log"; exit 1; }
 tail -1 "$OUT/smoke.log"

@@ -30,6 +30,8 @@ installed and there is no network) and records, as plain data:
   dist_c3.npz      (--c3-dist N) N-replica RedQueen ensemble on the C3 bench network
   dist_g120.npz    (--g120-dist N) N-replica RedQueen ensemble on graphs.g120 (> 64
                    sources: the general sweep's instances)
+  dist_c5m.npz     (--c5m-dist N) RedQueen ensemble on graphs.c5_mid: C5's 500 bursty
+                   Hawkes broadcasters at T = 1000 on 100 followers (grown in chunks)
   dist_c5s.npz     (--c5s-dist N) RedQueen ensemble on graphs.c5_small: C5's bursty
                    Hawkes (l_0 0.5, alpha 1, beta 2) at T = 1000 on 4 followers
   dist_hawkes0.npz (--hawkes-seed0) the 10k-replica Hawkes world draw at seed0 0 that
@@ -865,6 +867,42 @@ def gen_scale_logs(procs=0):
     np.savez_compressed(os.path.join(HERE, "scale_logs.npz"), **rec)
 
 
+C5M_SEED_STRIDE = 100000   # > 99 x the 500 broadcasters: no shared streams
+C5M_OPT_SEED_OFFSET = 77777
+
+
+def _c5m_worker(r):
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from redqueen_amd import graphs as G
+    so = SimOpts(**G.c5_mid())
+    u = C5M_SEED_STRIDE * (r + 1000)   # disjoint from scale_logs' c5m runs (r = 0, 1)
+    m = so.randomize_other_sources(u).create_manager_with_opt(seed=u + C5M_OPT_SEED_OFFSET)
+    m.run_dynamic()
+    df = m.state.get_dataframe()
+    met, own, world = metrics(df, so)
+    return np.concatenate([[own, world, m.state.get_num_events()], met])
+
+
+def gen_c5m_dist(n, start=0, procs=0):
+    """graphs.c5_mid (C5's 500 bursty Hawkes broadcasters at T = 1000, 100 followers)
+    through the reference itself (~8 min per replica per core): replica r runs world
+    randomize_other_sources(100000 (r + 1000)) and RedQueen seed that + 77777.  start > 0
+    appends to dist_c5m.npz (which must hold exactly start rows)."""
+    path = os.path.join(HERE, "dist_c5m.npz")
+    with mp.Pool(procs or os.cpu_count()) as pool:
+        res = np.asarray(pool.map(_c5m_worker, range(start, start + n), chunksize=1))
+    if start:
+        old = np.load(path)["data"]
+        assert old.shape[0] == start, (old.shape, start)
+        res = np.concatenate([old, res])
+    cols = ["posts", "world", "events"] + ["top%d" % k for k in KS] + ["avg", "r2"]
+    tmp = path + ".tmp.npz"
+    np.savez_compressed(tmp, data=res, cols=np.asarray(cols),
+                        seed_stride=np.asarray([C5M_SEED_STRIDE]), seed_base=np.asarray([1000]),
+                        opt_seed_offset=np.asarray([C5M_OPT_SEED_OFFSET]))
+    os.replace(tmp, path)
+
+
 # C4 corners: README graph at the extreme q of the reference's grid (opt_runs.py:289-291)
 # x three follower-significance vectors (the notebook's sim_opts_unequal (0.5, 1.5),
 # opt_broadcast.ipynb:5550, and a strongly unequal (1, 0.25)).  Replica r runs world
@@ -1092,6 +1130,8 @@ if __name__ == "__main__":
                     help="only dist_knock.npz: N reference runs of the reactive plugin beside RedQueen")
     ap.add_argument("--hawkes-seed0", action="store_true",
                     help="only dist_hawkes0.npz: the discarded 10k seed0-0 Hawkes world draw")
+    ap.add_argument("--c5m-dist", type=int, default=0, help="only dist_c5m.npz: N more replicas")
+    ap.add_argument("--c5m-start", type=int, default=0, help="append to dist_c5m.npz from here")
     ap.add_argument("--scale-logs", action="store_true",
                     help="only scale_logs.npz: whole reference runs of C3 and c5_mid")
     a = ap.parse_args()
@@ -1100,7 +1140,11 @@ if __name__ == "__main__":
              "oracle": gen_oracle, "sweepq": gen_sweepq, "sig": gen_sig, "realdata": gen_realdata,
              "plugin": gen_plugin, "errors": gen_errors, "dynplugin": gen_dynplugin,
              "gridtie": gen_gridtie}
-    if a.scale_logs:
+    if a.c5m_dist:
+        gen_c5m_dist(a.c5m_dist, a.c5m_start, a.procs)
+        print("done c5m dist", flush=True)
+        a.worlds = True   # nothing else
+    elif a.scale_logs:
         gen_scale_logs(a.procs)
         print("done scale logs", flush=True)
         a.worlds = True   # nothing else

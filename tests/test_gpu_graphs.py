@@ -6,7 +6,7 @@ GPU, bit for bit against the engine-semantics oracle (oracle/rq_oracle.c):
   (:74-76) and the pivot cells average the repeated rows' ranks; the all-RealData
   multigraph worlds equal the REFERENCE's own df (tests/test_gpu_realdata.py,
   realdata.npz rdmg*);
-* more than 512 sources (the two-level merge feeding the fast sweep, up to 65535; the
+* more than 512 sources (the two-level merge feeding the fast sweep, up to 262144; the
   sequential sweep at 16 and 32 sources per lane up to 2048, on the merged sequence
   above);
 * the repeat-stream skip of the per-wave sink-bit sweep (a stream's second event
@@ -158,6 +158,32 @@ def test_65000_sources_fast_equals_sequential():
         ta, sa = a.events(r)
         tb, sb = b.events(r)
         assert np.array_equal(ta, tb) and np.array_equal(sa, sb)
+
+
+@pytest.mark.parametrize("n_src", [70000, 140000])
+def test_more_than_65535_sources(n_src):
+    """Past the u16 stream ids (round 6): the two-level merge carries group-local ids at
+    its first level and global ones at the second, with each entry's bits 16-23 in a side
+    array the sweeps read (rq_batch_desc limit: 512 groups of 512 = 262144 sources).  The
+    fast and the sequential sweep agree bit for bit, events included, and replica 0 ==
+    the engine oracle."""
+    torch, engine, graphs, O = _ctx()
+    so = _many_sources(n_src, T=0.5)
+    g = _graph(engine, so)
+    assert g.n_streams == n_src + 1
+    kw = dict(q=1.0, s=1.0, n_rep=2, ctrl_seed=4, world_seed=4, randomize=True, Ks=(1, 2),
+              event_log=True)
+    a = g.run("opt", **kw)
+    b = g.run("opt", sweep_mode=2, **kw)
+    assert int(a.status.max().item()) == 0 and int((b.status & 3).max().item()) == 0
+    assert torch.equal(a.metrics, b.metrics) and torch.equal(a.counts, b.counts)
+    for r in range(2):
+        ta, sa = a.events(r)
+        tb, sb = b.events(r)
+        assert np.array_equal(ta, tb) and np.array_equal(sa, sb)
+    assert int(sa.max()) > 1000 + 65535   # streams past the u16 range did play
+    met_o, t_o, s_o = _oracle(O, _world_with_seeds(so, 4), ("opt", 4), (1, 2))
+    _cmp_replica(a, 0, met_o, t_o, s_o, (1, 2))
 
 
 def test_more_than_2048_sources_what_needs_the_sequential_sweep():
