@@ -27,8 +27,13 @@ namespace rq {
 
 struct SrcGen {
     uint32_t k0, k1;        // Philox key (seed, kind salt)
-    uint32_t w2, w3;        // second half of the last call
     uint32_t d;             // next draw index (< 2^32 draws per source)
+    // the draws are turned into exponentials ahead of their use, so the Philox rounds and
+    // the logarithm run beside the dependent chain of the candidate before (the generator
+    // is latency-bound, not issue-bound): Poisson takes both halves of a call at its even
+    // draw (en: the odd draw's exponential); Hawkes / PiecewiseConst (one call per
+    // candidate) hold the next candidate's exponential and acceptance uniform (e1n, u2n)
+    double en, e1n, u2n;
     int kind;
     bool done;
     double t;               // candidate base time
@@ -46,6 +51,16 @@ struct SrcGen {
         kind = RQ_SRC_NONE;
         done = true;
         d = 0u;
+        en = e1n = u2n = 0.0;
+    }
+    // Philox call `call` of this stream -> the exponential of its first half and the
+    // uniform of its second
+    __device__ __forceinline__ void draw2(uint32_t call, double& e, double& u) const
+    {
+        uint32_t c[4] = {call, 0u, 0u, 0u};
+        philox4x32_10(c, k0, k1);
+        e = rq_std_exponential(rq_uniform53(c[0], c[1]));
+        u = rq_uniform53(c[2], c[3]);
     }
 
     __device__ __forceinline__ void init(const GenArgs& a, int j, int64_t i, const uint64_t* etab_)
@@ -65,8 +80,8 @@ struct SrcGen {
         }
         k0 = seed;
         k1 = kind_salt(kind, is_ctrl);
-        w2 = w3 = 0u;
         d = 0u;
+        en = e1n = u2n = 0.0;
         done = false;
         t = a.start;
         tau = a.start;
@@ -110,6 +125,7 @@ struct SrcGen {
         } else {
             done = true;   // the controlled slot of an Opt / wall-only run: no stream
         }
+        if (!done && (kind == RQ_SRC_HAWKES || kind == RQ_SRC_PWCONST)) draw2(0u, e1n, u2n);
     }
 
     // one candidate; true (and *out) when it is an arrival.  Sets done past `end`.
@@ -122,21 +138,26 @@ struct SrcGen {
             done = ri >= na;
             return true;
         }
-        double u1, u2 = 0.0;
-        if ((d & 1u) == 0u) {
-            const uint32_t call = d >> 1;
-            uint32_t c[4] = {call, 0u, 0u, 0u};
-            philox4x32_10(c, k0, k1);
-            w2 = c[2];
-            w3 = c[3];
-            u1 = rq_uniform53(c[0], c[1]);
-            u2 = rq_uniform53(c[2], c[3]);
-        } else {
-            u1 = rq_uniform53(w2, w3);
-        }
         const bool poisson = kind == RQ_SRC_POISSON || kind == RQ_SRC_POISSON2;
-        d += poisson ? 1u : 2u;
-        const double tc = t + rq_std_exponential(u1) * inv;
+        double e, u2 = 0.0;
+        if (poisson) {
+            if ((d & 1u) == 0u) {
+                uint32_t c[4] = {d >> 1, 0u, 0u, 0u};
+                philox4x32_10(c, k0, k1);
+                e = rq_std_exponential(rq_uniform53(c[0], c[1]));
+                en = rq_std_exponential(rq_uniform53(c[2], c[3]));
+            } else {
+                e = en;
+            }
+            d += 1u;
+        } else {
+            // two draws per candidate (d even): this candidate's came one call ahead
+            e = e1n;
+            u2 = u2n;
+            d += 2u;
+            draw2(d >> 1, e1n, u2n);
+        }
+        const double tc = t + e * inv;
         if (!(tc <= end)) {
             done = true;
             return false;

@@ -42,13 +42,18 @@ using namespace rq;
 // ============================================================================
 __global__ __launch_bounds__(256) void rq_gen_streams(GenArgs a)
 {
+    // rq_exp's table in LDS: a Hawkes candidate's exp looks up two per-lane words in its
+    // dependent chain (from __constant__ memory these were vector loads at L1/L2 latency)
+    __shared__ uint64_t etab[RQ_EXP_TAB_N];
+    for (int e = threadIdx.x; e < RQ_EXP_TAB_N; e += blockDim.x) etab[e] = rq_exp_tab_c[e];
+    __syncthreads();
     const int64_t rl = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int j = (int)(blockIdx.z * gridDim.y + blockIdx.y);   // > 32768 streams fold into z
     if (rl >= a.n_chunk || j >= a.n_str) return;
     const int64_t o = a.chunk0 + rl;      // local output index
     const int64_t i = rq_replica_of(a, o);   // global id (seeds)
     SrcGen gen;
-    gen.init(a, j, i, rq_exp_tab_c);
+    gen.init(a, j, i, etab);
 
     double* out = a.streams + rl * a.capsum + a.st_off[j];   // 128-byte aligned (host pads)
     const int cap = a.cap[j];                                   // multiple of 16

@@ -26,5 +26,5 @@ fi
 for v in "$@"; do
   name=${v%%=*}; envs=${v#*=}
   env $envs timeout -k 10 300 python3 -u bench.py --workload "$WL" --steps "$STEPS" --warmup 3 --no-cpu > "$OUT/bench_$name.log" 2>&1 || { echo "bench $name failed"; tail -5 "$OUT/bench_$name.log"; exit 1; }
-  python3 -c "import json,sys; l=json.loads(open('$OUT/bench_$name.log').read().strip().splitlines()[-1]); print('$name', '$envs', round(l['value']), 'replicas/s', round(l['ms_per_step'],3), 'ms/step', {k: round(v,3) for k,v in l['kernels_ms_per_launch'].items()}, 'plan chunk', l['sweep_plan']['chunk'])"
+  python3 -c "import json,sys; l=json.loads(open('$OUT/bench_$name.log').read().strip().splitlines()[-1]); print('$name', '$envs', round(l['value']), 'replicas/s', round(l['ms_per_step'],3), 'ms/step', {k: round(v,3) for k,v in l['kernels_ms_per_launch'].items()}, 'plan chunk', l['sweep_plan']['chunk'], 'sweep alone', l['roofline'].get('duration_ms'), 'frac', l['roofline'].get('frac'))"
 done
