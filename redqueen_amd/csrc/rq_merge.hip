@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <cstdlib>
+#include <type_traits>
 
 #include "rq_device.h"
 #include "rq_internal.h"
@@ -113,13 +114,21 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
 {
     constexpr int MG_W = MgCfg<MG_B>::W, MG_CAP = MgCfg<MG_B>::CAP, MG_M = MgCfg<MG_B>::M;
     constexpr int MG_TARGET = MgCfg<MG_B>::TARGET;
+    // the one-wave instance (<= 64 streams, rounds of <= 256) keeps its slot / sub-bucket
+    // pair, stream and bucket bases in 16 bits: 7.7 instead of 9.2 KB per block, so 20
+    // blocks share a CU (its VGPR bound) instead of 17
+    constexpr bool NARROW = MG_B <= 64 && !SUB;
+    constexpr int BS_SH = NARROW ? 8 : MG_SB;   // bs = (sub-bucket << BS_SH) | slot
+    static_assert(!NARROW || (MG_CAP <= 256 && MG_M <= 256), "16-bit fields");
+    using BS_T = typename std::conditional<NARROW, uint16_t, uint32_t>::type;
+    using BJ_T = typename std::conditional<SUB, uint32_t, uint16_t>::type;   // SUB: global ids
     __shared__ double bt[MG_CAP];          // round buffer (arrival order)
-    __shared__ uint32_t bs[MG_CAP];        // (sub-bucket << MG_SB) | slot
-    __shared__ uint32_t bj[MG_CAP];        // the arrival's stream
+    __shared__ BS_T bs[MG_CAP];            // (sub-bucket << BS_SH) | slot
+    __shared__ BJ_T bj[MG_CAP];            // the arrival's stream
     __shared__ double st[MG_CAP];          // bucket order
     __shared__ uint32_t sk[MG_CAP];        // (stream << MG_SB) | buffer index (streams < 2^21)
     __shared__ uint32_t cnt[MG_M];
-    __shared__ uint32_t bbase[MG_M + 1];
+    __shared__ BS_T bbase[MG_M + 1];
     __shared__ double wmin[MG_W];
     __shared__ uint32_t wsum[MG_W];
     __shared__ uint32_t nb;
@@ -263,7 +272,7 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
                     const uint32_t slot = atomicAdd(&cnt[sb], 1u);
                     bt[idx] = cv[k];
                     bj[idx] = SUB ? jout + selj16(cj, nxj, k) : jout;
-                    bs[idx] = ((uint32_t)sb << MG_SB) | slot;
+                    bs[idx] = (BS_T)(((uint32_t)sb << BS_SH) | slot);
                 }
             }
             p += take;
@@ -293,7 +302,7 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
                     const uint32_t slot = atomicAdd(&cnt[sb], 1u);
                     bt[idx] = head;
                     bj[idx] = SUB ? jout + selj16(cj, nxj, p - p8) : jout;
-                    bs[idx] = ((uint32_t)sb << MG_SB) | slot;
+                    bs[idx] = (BS_T)(((uint32_t)sb << BS_SH) | slot);
                     ++p;
                     if (p - p8 == 16 && p < L) RQ_MG_RELOAD(p);   // a burst: both chunks consumed
                     head = RQ_MG_HEAD();
@@ -369,19 +378,19 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
         for (int k = 0; k < MG_W; ++k) wo += k < w ? wsum[k] : 0u;
         {
             const uint32_t b = wo + incl - tsum;
-            bbase[4 * tid] = b;
-            bbase[4 * tid + 1] = b + v0;
-            bbase[4 * tid + 2] = b + v0 + v1;
-            bbase[4 * tid + 3] = b + v0 + v1 + v2;
+            bbase[4 * tid] = (BS_T)b;
+            bbase[4 * tid + 1] = (BS_T)(b + v0);
+            bbase[4 * tid + 2] = (BS_T)(b + v0 + v1);
+            bbase[4 * tid + 3] = (BS_T)(b + v0 + v1 + v2);
             cnt[4 * tid] = cnt[4 * tid + 1] = cnt[4 * tid + 2] = cnt[4 * tid + 3] = 0;
-            if (tid == 0) bbase[MG_M] = nr;
+            if (tid == 0) bbase[MG_M] = (BS_T)nr;
         }
         __syncthreads();
         RQ_MG_TICK(2);
         // ---- into bucket order ----
         for (int i = tid; i < (int)nr; i += MG_B) {
             const uint32_t x = bs[i];
-            const uint32_t pos = bbase[x >> MG_SB] + (x & ((1u << MG_SB) - 1u));
+            const uint32_t pos = (uint32_t)bbase[x >> BS_SH] + (x & ((1u << BS_SH) - 1u));
             st[pos] = bt[i];
             sk[pos] = ((uint32_t)bj[i] << MG_SB) | (uint32_t)i;
         }
