@@ -586,6 +586,9 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p, double budget)
             p->log = true;   // no fast instance fits this graph: the exact sequential sweep
             goto replan;
         }
+        // stream ids past 16 bits are read (mrg_jh) by the GT instances only; such graphs'
+        // tables never fit LDS, so they always get one
+        if (p->mrg && g->n_str > 65535 && !p->gt) return RQ_EUNSUPPORTED;
         // BL on merged streams: a per-wave stamp (the reset epoch a stream last played in)
         // and first-lane table per stream let a tile skip the events whose stream already
         // played since the last post -- their sinks are out of the top-1 set and valid.

@@ -286,7 +286,7 @@ __global__ __launch_bounds__(LOG ? 256 : (MRG ? RQ_MRG_LB : (SPL >= 4 ? 512 : 10
         __asm__ volatile("" : "+v"(x));
         t_ = a.mrg_t[x + e];
         j_ = a.mrg_j[x + e];
-        if (a.mrg_jh) j_ |= (int)a.mrg_jh[x + e] << 16;   // > 65535 streams
+        if (GT && a.mrg_jh) j_ |= (int)a.mrg_jh[x + e] << 16;   // > 65535 streams: always the GT instances
     };
     const int mlen = MRG ? a.mrg_len[rl] : 0;
     int mpos = 0;

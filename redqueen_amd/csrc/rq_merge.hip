@@ -109,7 +109,8 @@ __device__ __forceinline__ uint32_t selj16(uint4 c, uint4 nx, int k)
 
 // SUB: the second level of a two-level merge (> RQ_MG_B sources): thread g owns the
 // merged sequence of stream group g (its entries carry their own stream ids)
-template <int MG_B, bool SUB>
+// WIDE: more than 65535 streams (the second level writes bits 16-23 to out_jh)
+template <int MG_B, bool SUB, bool WIDE = false>
 __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
 {
     constexpr int MG_W = MgCfg<MG_B>::W, MG_CAP = MgCfg<MG_B>::CAP, MG_M = MgCfg<MG_B>::M;
@@ -121,7 +122,7 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
     constexpr int BS_SH = NARROW ? 8 : MG_SB;   // bs = (sub-bucket << BS_SH) | slot
     static_assert(!NARROW || (MG_CAP <= 256 && MG_M <= 256), "16-bit fields");
     using BS_T = typename std::conditional<NARROW, uint16_t, uint32_t>::type;
-    using BJ_T = typename std::conditional<SUB, uint32_t, uint16_t>::type;   // SUB: global ids
+    using BJ_T = typename std::conditional<WIDE, uint32_t, uint16_t>::type;   // global ids > 65535
     __shared__ double bt[MG_CAP];          // round buffer (arrival order)
     __shared__ BS_T bs[MG_CAP];            // (sub-bucket << BS_SH) | slot
     __shared__ BJ_T bj[MG_CAP];            // the arrival's stream
@@ -419,7 +420,7 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
                 out_t[outpos + g0 + r] = x;
                 out_j[outpos + g0 + r] = (uint16_t)(kx >> MG_SB);
             }
-            if (a.out_jh) a.out_jh[(rl * ngrp + grp) * a.mrg_stride + outpos + g0 + r] = (uint8_t)(kx >> (MG_SB + 16));
+            if (WIDE) a.out_jh[(rl * ngrp + grp) * a.mrg_stride + outpos + g0 + r] = (uint8_t)(kx >> (MG_SB + 16));
         }
         RQ_MG_TICK(6);
         outpos += nr;
@@ -544,10 +545,14 @@ hipError_t rq_launch_merge_sub(const MergeArgs& a, hipStream_t s)
 {
     if (a.n_chunk <= 0) return hipSuccess;
     if (a.n_grp < 1 || a.n_grp > RQ_MG_B || !a.sub_t || !a.sub_j || !a.sub_len) return hipErrorInvalidValue;
-    if (a.n_grp <= 64)
+    // <= 64 groups are <= 32768 streams: 16-bit ids; past 65535 streams the WIDE instance
+    if (a.n_grp <= 64) {
         hipLaunchKernelGGL((rq_merge_streams<64, true>), dim3((unsigned)a.n_chunk), dim3(64), 0, s, a);
-    else
+    } else if (a.out_jh) {
+        hipLaunchKernelGGL((rq_merge_streams<RQ_MG_B, true, true>), dim3((unsigned)a.n_chunk), dim3(RQ_MG_B), 0, s, a);
+    } else {
         hipLaunchKernelGGL((rq_merge_streams<RQ_MG_B, true>), dim3((unsigned)a.n_chunk), dim3(RQ_MG_B), 0, s, a);
+    }
     return hipGetLastError();
 }
 
