@@ -260,6 +260,7 @@ struct Plan {
     size_t off_mt = 0, off_mj = 0, off_mjh = 0, off_mlen = 0;
     int64_t mrg_stride = 0;   // merged entries per replica (capacity)
     int n_grp = 1;            // > RQ_MG_B sources: groups of the two-level merge
+    int grp_sz = RQ_MG_B;     //   streams per group (64 up to 64 groups: MergeArgs.grp_sz)
     int64_t sub_stride = 0;   //   entries per (replica, group) of the first level
     size_t off_sub_t = 0, off_sub_j = 0, off_sub_len = 0;
     // the fused sweep's phases B / C on merged streams (rq_gen_streams + rq_merge_streams
@@ -494,7 +495,13 @@ int make_plan(const rq_graph* g, const rq_batch_desc* b, Plan* p, double budget)
     // the fast general sweep plays the merged (t, stream) sequence: the merge kernel reads
     // every stream line once (one source per thread, <= RQ_MG_B sources)
     p->mrg = (!p->log && b->sweep_mode != 6) || p->lmrg;
-    p->n_grp = g->n_str > RQ_MG_B ? (g->n_str + RQ_MG_B - 1) / RQ_MG_B : 1;
+    // > RQ_MG_B sources: two levels; groups of 64 streams (one-wave first-level blocks) while
+    // <= 64 of them cover the graph, so the second level walks up to 64 sequences a round
+    // instead of 2-8 (600 sources: 2 groups of <= 512 -> 10 of <= 64)
+    p->grp_sz = g->n_str <= 64 * 64 ? 64 : RQ_MG_B;
+    if (const char* e = getenv("RQ_MG_GRP"))   // A/B only
+        p->grp_sz = atoi(e) == 64 && g->n_str <= 64 * 64 ? 64 : RQ_MG_B;
+    p->n_grp = g->n_str > RQ_MG_B ? (g->n_str + p->grp_sz - 1) / p->grp_sz : 1;
     if (const char* e = getenv("RQ_MRG")) p->mrg = p->lmrg || (p->mrg && atoi(e) != 0);   // A/B only
     // without the merged streams the windowed sweep owns <= 8 sources per lane
     if (!p->mrg && !p->log && g->n_str > 512) {
@@ -754,7 +761,7 @@ void plan_layout(const rq_graph* g, const rq_batch_desc* b, Plan* p)
     if (p->mrg && p->n_grp > 1)
         for (int gq = 0; gq < p->n_grp; ++gq) {
             int64_t c = 0;
-            for (int j = gq * RQ_MG_B; j < std::min(g->n_str, (gq + 1) * RQ_MG_B); ++j) c += p->cap[j];
+            for (int j = gq * p->grp_sz; j < std::min(g->n_str, (gq + 1) * p->grp_sz); ++j) c += p->cap[j];
             p->sub_stride = std::max(p->sub_stride, (c + 15) & ~(int64_t)15);
         }
     const int64_t subc = p->sub_stride > 0 ? C * p->n_grp : 0;
@@ -1309,7 +1316,8 @@ int rq_run_batch(rq_graph_t g, const rq_batch_desc* b, const rq_outputs* out, vo
 #endif
             TimedLaunch tl(K_MERGE, s);
             if (p.n_grp > 1) {
-                // level 1: each group of RQ_MG_B streams into its own sequence
+                // level 1: each group of grp_sz streams into its own sequence
+                ma.grp_sz = p.grp_sz;
                 MergeArgs m1 = ma;
                 m1.out_t = (double*)(wsb + p.off_sub_t);
                 m1.out_j = (uint16_t*)(wsb + p.off_sub_j);   // group-local streams: u16 always

@@ -166,6 +166,9 @@ struct MergeArgs {
     const int* sub_len;
     int n_grp;
     int64_t sub_stride;
+    // streams per first-level group: RQ_MG_B, or 64 (one-wave blocks) up to 64 groups of
+    // them -- the second level then has more streams walking (a lane per group) per round
+    int grp_sz;
     unsigned long long* clk;   // RQ_PHASE_CLOCK builds only: per-phase s_memtime sums [8]
 };
 #define RQ_NPSUM1_LDS 516   // doubles of wave_npsum<1> scratch (== rq::npsum_lds_doubles<1>())

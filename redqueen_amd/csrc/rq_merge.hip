@@ -143,7 +143,7 @@ __global__ __launch_bounds__(MG_B) void rq_merge_streams(MergeArgs a)
     // the stream id an entry carries out: group-local at a two-level merge's first level
     // (< RQ_MG_B: u16 whatever the source count), global otherwise; the second level
     // (SUB) turns its group g's local ids back into global ones, g RQ_MG_B + local
-    const uint32_t jout = SUB ? (uint32_t)tid * RQ_MG_B : (uint32_t)(j - grp * MG_B);
+    const uint32_t jout = SUB ? (uint32_t)tid * (uint32_t)a.grp_sz : (uint32_t)(j - grp * MG_B);
     int L = 0;
     const double* src = a.streams;
     const uint16_t* srcj = nullptr;   // SUB: the entries' own stream ids
@@ -534,10 +534,14 @@ hipError_t rq_launch_merge(const MergeArgs& a, hipStream_t s)
 hipError_t rq_launch_merge_groups(const MergeArgs& a, hipStream_t s)
 {
     if (a.n_chunk <= 0) return hipSuccess;
-    const int ng = (a.n_str + RQ_MG_B - 1) / RQ_MG_B;
+    if (a.grp_sz != 64 && a.grp_sz != RQ_MG_B) return hipErrorInvalidValue;
+    const int ng = (a.n_str + a.grp_sz - 1) / a.grp_sz;
     if (ng < 2 || ng > RQ_MG_B || a.n_str > RQ_MAX_STREAMS_MRG) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((rq_merge_streams<RQ_MG_B, false>), dim3((unsigned)a.n_chunk, (unsigned)ng), dim3(RQ_MG_B), 0,
-                       s, a);
+    if (a.grp_sz == 64)
+        hipLaunchKernelGGL((rq_merge_streams<64, false>), dim3((unsigned)a.n_chunk, (unsigned)ng), dim3(64), 0, s, a);
+    else
+        hipLaunchKernelGGL((rq_merge_streams<RQ_MG_B, false>), dim3((unsigned)a.n_chunk, (unsigned)ng), dim3(RQ_MG_B), 0,
+                           s, a);
     return hipGetLastError();
 }
 
