@@ -320,3 +320,20 @@ def test_realdata_worlds_both_restatements_exact(golden):
                                              cols["event_id"], w["src_id"], w["end_time"], KS)
             assert np.array_equal(np.asarray(top + [avg, r2]), d[name + "_met"]), name
             assert np.array_equal(O.state_time_deltas(t), dt)
+
+
+def test_engine_c5_mid_matches_reference_distribution(golden):
+    """Engine semantics on C5's source side (graphs.c5_mid: 500 bursty Hawkes broadcasters
+    at T = 1000, ~3.2 x 10^5 events per replica) vs the reference's own replicas of it
+    (dist_c5m.npz)."""
+    d = golden("dist_c5m.npz")
+    cols = [str(c) for c in d["cols"]]
+    ref = {c: d["data"][:, i] for i, c in enumerate(cols)}
+    so = graphs.c5_mid()
+    out, cnt, _ = O.engine_batch(O.Scenario(so, ("opt", 0)), 96, 700000, True, KS, 8,
+                                 seed_stride=int(d["seed_stride"][0]))
+    eng = {"posts": cnt[:, 0], "world": cnt[:, 1], "events": cnt[:, 2], "avg": out[:, len(KS)],
+           "r2": out[:, len(KS) + 1]}
+    for i, k in enumerate(KS):
+        eng["top%d" % k] = out[:, i]
+    E.compare("oracle_c5m", eng, ref, z_bound=2.576)
