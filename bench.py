@@ -160,6 +160,7 @@ def serial_probe(L, g, pkw, chunk, steps):
     launch's HIP-event time; these are the durations the kernel itself needs (the same
     figure as a rocprofv3 kernel trace under AMD_SERIALIZE_KERNEL=3).
     Returns (ms per launch [gen, sweep, scan, -, merge], launches)."""
+    pkw = {k: v for k, v in pkw.items() if k != "chunk"}
     old = os.environ.get("RQ_PIPE")
     os.environ["RQ_PIPE"] = "1"
     try:
@@ -182,7 +183,7 @@ def serial_probe(L, g, pkw, chunk, steps):
     return ms / np.maximum(nl, 1), nl
 
 
-def make_step(wl, g, so, R, world, rank, dev, Ks, group=None, force=False):
+def make_step(wl, g, so, R, world, rank, dev, Ks, group=None, force=False, chunk=0):
     """The bench step of a workload, on this rank: (step(k) -> (this rank's BatchResult,
     ensemble means), replicas per step over all ranks, plan kwargs).
     c2 / c3 / c5: R replicas per GPU with their own seeds, one all-gather of the
@@ -190,7 +191,8 @@ def make_step(wl, g, so, R, world, rank, dev, Ks, group=None, force=False):
     c4: the 64 q x 4 s grid with R replicas per grid point per GPU -- rank k runs the
     k-th replica window of EVERY grid point (dist.run_sharded), one all-gather, then
     per-grid-point means in fixed replica order (dist.grid_means).
-    force: the all-gather runs through the process group even for one rank (--dist)."""
+    force: the all-gather runs through the process group even for one rank (--dist).
+    chunk: replicas per pipelined chunk inside one call (0: the library's plan)."""
     from redqueen_amd import dist as D
     if wl == "c4":
         from redqueen_amd import graphs
@@ -199,7 +201,7 @@ def make_step(wl, g, so, R, world, rank, dev, Ks, group=None, force=False):
         sm = np.asarray([list(s) for _, s in grid])
         n_rep = R * world
         lo, hi = D.grid_shard(n_rep, world, rank)
-        kw = dict(q=qs, s=sm, randomize=True, Ks=Ks, seed_mod=n_rep)
+        kw = dict(q=qs, s=sm, randomize=True, Ks=Ks, seed_mod=n_rep, chunk=chunk)
 
         def step(k):
             base = k * n_rep
@@ -212,14 +214,14 @@ def make_step(wl, g, so, R, world, rank, dev, Ks, group=None, force=False):
     def step(k):
         base = (k * world + rank) * R
         res = g.run("opt", q=so["q"], s=so["s"], n_rep=R, ctrl_seed=base, world_seed=base,
-                    randomize=True, Ks=Ks, check=False)
+                    randomize=True, Ks=Ks, check=False, chunk=chunk)
         m = res.metrics
         if world > 1 or force:
             # RCCL over xGMI: the only exchange
             m = D.gather_rows(m, world * R, world, rank, group, force=force)
         # ensemble means (redqueen_amd.dist.grid_means): identical on every rank
         return res, D.grid_means(m, 1, m.shape[0])[0]
-    return step, R * world, dict(q=so["q"], s=so["s"], n_rep=R, randomize=True, Ks=Ks)
+    return step, R * world, dict(q=so["q"], s=so["s"], n_rep=R, randomize=True, Ks=Ks, chunk=chunk)
 
 
 def main():
@@ -243,6 +245,13 @@ def main():
     ap.add_argument("--probe-steps", type=int, default=0,
                     help="steps of the serialised probe after the timed region (per-launch "
                          "kernel times with each kernel alone on the chip; default 3, C5 1)")
+    ap.add_argument("--chunk", type=int, default=-1,
+                    help="replicas per pipelined chunk inside one call: -1 = the whole call "
+                         "when the steps alternate over >= 2 caller streams (the steps then "
+                         "overlap each other, and the library's two-chunk split inside a call "
+                         "only adds launches: C3 2.71 -> 2.58 ms per step, C4 25.1 -> 24.7, "
+                         "gpurun_out/chunkab, chunkc4), else the library's plan; 0 = the "
+                         "library's plan")
     ap.add_argument("--dist", action="store_true",
                     help="at N = 1 too: a world-size-1 RCCL group, the step's all-gather "
                          "runs through it")
@@ -272,8 +281,10 @@ def main():
     # replicas/s against 15.8k at 4096 (profiles/r04_c5_ab.txt)
     R = a.replicas or {"c5": 8192, "c4": 1000}.get(a.workload, 10000)
     Ks = (1,)
+    n_streams = a.streams or (1 if a.workload == "c5" else 2)
+    chunk = a.chunk if a.chunk >= 0 else (1 << 30 if n_streams >= 2 else 0)   # clamped to the call
     step, rep_step, pkw = make_step(a.workload, g, so, R, world, rank, dev, Ks,
-                                    force=grouped)
+                                    force=grouped, chunk=chunk)
     plan = g.run("opt", plan_only=True, **pkw)
 
     # capacity check once at full size (overflow -> the engine reruns with doubled
@@ -305,7 +316,6 @@ def main():
     # its own workspace and side stream) fill the wave slots this step's sweep tail and
     # scan leave; every step still runs all of its work inside the timed region, which
     # ends with a device-wide synchronize
-    n_streams = a.streams or (1 if a.workload == "c5" else 2)
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream(device=dev)
                                                 for _ in range(n_streams - 1)]
 
@@ -429,7 +439,8 @@ def main():
             "config": {"workload": desc, "replicas_per_gpu": rep_step // world, "global_batch": rep_step,
                        "parallelism": ("grid-window sharded dp%d (each rank: every grid point's "
                                        "replica window)" if a.workload == "c4" else
-                                       "replica-sharded dp%d") % world, "Ks": list(Ks)},
+                                       "replica-sharded dp%d") % world, "Ks": list(Ks),
+                       "replicas_per_chunk": int(plan["chunk"])},
             "events_per_sec": ev_rate,
             "events_per_replica": local_ev / replicas,
             "overflow": int(status.item()),
